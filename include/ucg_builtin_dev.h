@@ -1,0 +1,234 @@
+/*
+ * ucg_builtin_dev.h - C-ABI of the MI355X device combine behind UCG's builtin
+ * planner (the "device shim").
+ *
+ * This header is the drop-in boundary for ONE path of openucx/xucg: the local
+ * element-wise reduce/combine `dst[i] = src[i] (op) dst[i]` that builtin/ops
+ * applies to every incoming fragment of a reduce/allreduce step.
+ *
+ * Reference interfaces each entry point replaces or serves (paths relative to
+ * the reference tree):
+ *
+ *   ucg_builtin_dev_reduce()        <- ucg_builtin_mpi_reduce()
+ *                                      builtin/ops/builtin_comp_step.inl:96-102,
+ *                                      i.e. the reduce_cb_f contract
+ *                                      api/ucg.h:149-150, for buffers that are
+ *                                      already device-resident.
+ *   ucg_builtin_dev_combine_host()  <- ucg_builtin_mpi_reduce_single()
+ *                                      builtin/ops/builtin_comp_step.inl:104-110
+ *                                      (one whole-buffer call on host memory,
+ *                                      H2D -> kernel -> D2H, pipelined).
+ *   ucg_builtin_dev_stage_begin/
+ *   ucg_builtin_dev_combine/
+ *   ucg_builtin_dev_stage_end()     <- ucg_builtin_mpi_reduce_fragment()
+ *                                      builtin/ops/builtin_comp_step.inl:112-120
+ *                                      called per fragment from
+ *                                      ucg_builtin_step_recv_handle_chunk()
+ *                                      :184-232; src is borrowed (released at
+ *                                      :443-449) so it is copied into a pinned
+ *                                      ring before the call returns.
+ *   ucg_builtin_dev_reduce_multi()  <- the per-element association that the
+ *                                      recursive-doubling plan produces over
+ *                                      2^k ranks (builtin/plan/
+ *                                      builtin_recursive.c:158-169), evaluated
+ *                                      in one pass (one-shot reduce-scatter).
+ *   ucg_builtin_dev_ctx_create/
+ *   ucg_builtin_dev_ctx_destroy()   <- per-group state that lives in
+ *                                      struct ucg_builtin_group_ctx
+ *                                      builtin/builtin.c:66-90, created and
+ *                                      destroyed by ucg_builtin_create/destroy
+ *                                      :376-524.
+ *
+ * Semantics (the oracle in oracle/combine_ref.c restates them on the CPU and
+ * tests/golden pins them against MPICH 3.3.2 MPI_Reduce_local):
+ *   - dst is the in/out accumulator, src the incoming operand, count elements.
+ *   - SUM/PROD on integers wrap modulo 2^n; on floats they are one IEEE-754
+ *     round-to-nearest-even op, subnormals preserved, and NaN results follow
+ *     the x86-SSE rule of the host MPI library: a NaN dst is returned quieted,
+ *     else a NaN src is returned quieted, else an invalid op gives the default
+ *     NaN (sign set, quiet bit set).
+ *   - MAX is dst = (dst > src) ? dst : src, MIN is dst = (dst < src) ? dst :
+ *     src (so NaN and signed-zero behaviour is that of the C ternary).
+ *   - fp16 / bf16 compute in fp32 and round once (RNE) to the storage type.
+ *   - LAND/LOR/LXOR/BAND/BOR/BXOR are defined for integer types only.
+ *
+ * All entry points are plain C: pointers, sizes, enums. No HIP or torch types
+ * appear in a signature; a HIP stream is passed as `void *`.
+ */
+#ifndef UCG_BUILTIN_DEV_H_
+#define UCG_BUILTIN_DEV_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * Status codes. Inside a UCX build define UCG_BUILTIN_DEV_HAVE_UCS and include
+ * <ucs/type/status.h> first; the values below are UCX's own (ucs_status_t).
+ */
+#ifdef UCG_BUILTIN_DEV_HAVE_UCS
+#include <ucs/type/status.h>
+#else
+#ifndef UCG_BUILTIN_DEV_UCS_STATUS_DEFINED
+#define UCG_BUILTIN_DEV_UCS_STATUS_DEFINED
+typedef enum {
+    UCS_OK                  =   0,
+    UCS_INPROGRESS          =   1,
+    UCS_ERR_NO_RESOURCE     =  -2,
+    UCS_ERR_IO_ERROR        =  -3,
+    UCS_ERR_NO_MEMORY       =  -4,
+    UCS_ERR_INVALID_PARAM   =  -5,
+    UCS_ERR_NOT_IMPLEMENTED =  -8,
+    UCS_ERR_NO_DEVICE       = -14,
+    UCS_ERR_BUSY            = -15,
+    UCS_ERR_OUT_OF_RANGE    = -19,
+    UCS_ERR_UNSUPPORTED     = -22
+} ucs_status_t;
+#endif
+#endif
+
+/* Element types the device path can classify (see ucg_builtin_combine.h for
+ * the mapping from the opaque MPI datatype of api/ucg.h:131-137). */
+typedef enum ucg_dev_dtype {
+    UCG_DEV_DT_INT8 = 0,
+    UCG_DEV_DT_UINT8,
+    UCG_DEV_DT_INT16,
+    UCG_DEV_DT_UINT16,
+    UCG_DEV_DT_INT32,
+    UCG_DEV_DT_UINT32,
+    UCG_DEV_DT_INT64,
+    UCG_DEV_DT_UINT64,
+    UCG_DEV_DT_FLOAT16,
+    UCG_DEV_DT_BFLOAT16,
+    UCG_DEV_DT_FLOAT32,
+    UCG_DEV_DT_FLOAT64,
+    UCG_DEV_DT_LAST
+} ucg_dev_dtype_t;
+
+/* Reduction operators (MPI predefined ops without MINLOC/MAXLOC, which the
+ * reference rejects: builtin/ops/builtin_control.c:881-884). */
+typedef enum ucg_dev_op {
+    UCG_DEV_OP_SUM = 0,
+    UCG_DEV_OP_PROD,
+    UCG_DEV_OP_MAX,
+    UCG_DEV_OP_MIN,
+    UCG_DEV_OP_LAND,
+    UCG_DEV_OP_LOR,
+    UCG_DEV_OP_LXOR,
+    UCG_DEV_OP_BAND,
+    UCG_DEV_OP_BOR,
+    UCG_DEV_OP_BXOR,
+    UCG_DEV_OP_LAST
+} ucg_dev_op_t;
+
+/* Synthetic input distributions. */
+typedef enum ucg_dev_dist {
+    UCG_DEV_DIST_EXACT = 0, /* integers uniform in [-1024, 1024], cast */
+    UCG_DEV_DIST_ROUND,     /* random mantissa x 2^U[-8,8], random sign;
+                               integer types: full-range random bits */
+    UCG_DEV_DIST_SPECIAL,   /* the fixed special-value table, hashed index */
+    UCG_DEV_DIST_LAST
+} ucg_dev_dist_t;
+
+typedef struct ucg_builtin_dev_ctx ucg_builtin_dev_ctx_t;
+
+typedef struct ucg_builtin_dev_ctx_params {
+    int      device;       /* HIP device ordinal; -1 = the calling thread's */
+    void    *stream;       /* hipStream_t to launch on; NULL = create one */
+    size_t   stage_bytes;  /* pinned staging slot size; 0 = 8 MiB */
+    unsigned stage_slots;  /* staging ring depth; 0 = 4 */
+} ucg_builtin_dev_ctx_params_t;
+
+/* ---- introspection (no GPU needed) ---------------------------------------*/
+size_t      ucg_builtin_dev_dtype_size(ucg_dev_dtype_t dt);
+int         ucg_builtin_dev_is_supported(ucg_dev_dtype_t dt, ucg_dev_op_t op);
+const char *ucg_builtin_dev_version(void);
+/* Thread-local text of the last error reported by this library. */
+const char *ucg_builtin_dev_last_error(void);
+/* Number of HIP devices visible (0 when none); never initialises a context. */
+int         ucg_builtin_dev_device_count(void);
+
+/* ---- per-group device context --------------------------------------------*/
+ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *params,
+                                        ucg_builtin_dev_ctx_t **ctx_p);
+void         ucg_builtin_dev_ctx_destroy(ucg_builtin_dev_ctx_t *ctx);
+void        *ucg_builtin_dev_ctx_stream(ucg_builtin_dev_ctx_t *ctx);
+/* Wait for all work queued on the context's stream(s). */
+ucs_status_t ucg_builtin_dev_sync(ucg_builtin_dev_ctx_t *ctx);
+
+/* ---- device-resident combine ---------------------------------------------*/
+/* dst[i] = src[i] (op) dst[i] for i < count; dst/src are device pointers.
+ * Asynchronous on the context stream. dst == src is allowed (self-combine);
+ * partially overlapping ranges are not. */
+ucs_status_t ucg_builtin_dev_reduce(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
+                                    ucg_dev_dtype_t dt, void *dst,
+                                    const void *src, size_t count);
+
+/* One-shot multi-operand combine in the recursive-doubling association of
+ * builtin/plan/builtin_recursive.c:158-169 as seen from member `self`:
+ *   V(r,0) = srcs[r];  V(r,k) = V(r ^ 2^(k-1), k-1) (op) V(r, k-1)
+ * (left operand = src, right = dst of the reduce_cb_f contract), and writes
+ * dst[i] = V(self, log2(nsrc))[i]. nsrc must be a power of two <= 16; srcs may
+ * be peer-mapped device pointers (xGMI). dst may alias srcs[self]. */
+ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
+                                          ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                          void *dst, const void *const *srcs,
+                                          unsigned nsrc, unsigned self,
+                                          size_t count);
+
+/* ---- host-resident combine (the reduce_cb_f contract, staged) ------------*/
+/* Whole-buffer: dst_host[i] = src_host[i] (op) dst_host[i]. Chunks are copied
+ * H2D, combined and copied back D2H on two streams, overlapped. Pinned host
+ * buffers are DMA'd directly; pageable ones go through the pinned ring.
+ * Returns when dst_host holds the result. */
+ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
+                                          ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                          void *dst_host, const void *src_host,
+                                          size_t count);
+
+/* Per-step staging: the step's host accumulator (step->recv_buffer) is
+ * mirrored on the device between stage_begin and stage_end; each fragment
+ * combine copies the borrowed src into the pinned ring before returning and
+ * consecutive fragments are aggregated into one launch per ring slot. */
+ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
+                                         void *host_dst, size_t bytes);
+ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
+                                     ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                     size_t dst_offset, const void *host_src,
+                                     size_t count);
+ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx);
+
+/* ---- memory helpers --------------------------------------------------------*/
+void        *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
+void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);
+void        *ucg_builtin_dev_host_alloc(size_t bytes);      /* pinned */
+void         ucg_builtin_dev_host_free(void *ptr);
+ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
+                                    const void *src, size_t bytes); /* sync */
+
+/* Fill `count` elements with the counter-based synthetic generator
+ * (splitmix64; identical to ucg_oracle_fill() in oracle/combine_ref.c). */
+ucs_status_t ucg_builtin_dev_fill(ucg_builtin_dev_ctx_t *ctx, ucg_dev_dtype_t dt,
+                                  ucg_dev_dist_t dist, uint64_t seed,
+                                  void *dst, size_t count);
+
+/* ---- profiling hooks (the UCS_PROFILE_CALL_VOID analogue, :100-101) ------*/
+/* Launch `iters` back-to-back device combines between two HIP events on the
+ * context stream and return the average duration of one launch in us. */
+ucs_status_t ucg_builtin_dev_profile_reduce(ucg_builtin_dev_ctx_t *ctx,
+                                            ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                            void *dst, const void *src,
+                                            size_t count, unsigned iters,
+                                            double *avg_us);
+/* Counters since ctx creation: [0] kernel launches, [1] bytes combined on the
+ * device (3N basis), [2] H2D bytes, [3] D2H bytes. */
+void         ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx, uint64_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UCG_BUILTIN_DEV_H_ */
