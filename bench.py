@@ -1,0 +1,236 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X combine path (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+One step = one device-resident local combine dst[i] = src[i] + dst[i] of the
+BASELINE config-2 workload (2 x 256 MiB fp32, 2^26 elements) through the
+C-ABI (ucg_builtin_dev_reduce). With N > 1 (launched by torch.distributed.run)
+every rank combines its own shard-sized buffers: the path is element-wise, so
+it shards with no data-path collective (weak scaling); `value` is the
+aggregate over all ranks divided by the max-over-ranks wall time.
+
+Printed by rank 0 as ONE JSON line, with:
+  roofline      the combine kernel's average duration from HIP events on the
+                stream it is launched on -> algorithmic GB/s vs 8 TB/s HBM3E
+  cpu_baseline  the CPU restatement of the reference's combine (oracle/,
+                compiled -march=native on this host), 1 thread, bounded sample
+  extra         north-star 1 GiB fp32 combine, H2D/D2H-inclusive rate
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+GIB = float(1 << 30)
+WORKLOAD_COUNT = 1 << 26  # BASELINE.json configs[1]: two 256 MiB fp32 buffers
+
+
+def load_baseline_metric():
+    with open(os.path.join(ROOT, "BASELINE.json")) as f:
+        return json.load(f)["metric"]
+
+
+def pmc_traffic(count):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(str(count))
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(count, budget_s=10.0):
+    """Time the oracle's whole-buffer combine (the reduce_cb_f call shape) on
+    this host: 1 thread, fp32 SUM, same element count, ~budget_s of work."""
+    from oracle import oracle as O
+    os.environ.setdefault("UCG_ORACLE_LIB", O.build_native())
+    O.LIB_PATH = os.environ["UCG_ORACLE_LIB"]
+    O._lib = None
+    src = O.fill("float32", "round", 0x5EED0000, count)
+    dst = O.fill("float32", "round", 0x5EED0001, count)
+    best, med = O.time_reduce("sum", "float32", src, dst, reps=3)
+    reps = max(5, min(1000, int(budget_s / max(med, 1e-6))))
+    t0 = time.perf_counter()
+    best, med = O.time_reduce("sum", "float32", src, dst, reps=reps)
+    wall = time.perf_counter() - t0
+    frag = O.frag_length(8192, 4)
+    _, med_frag = O.time_reduce("sum", "float32", src, dst, frag_bytes=frag, reps=5)
+    threads = min(16, os.cpu_count() or 1)
+    _, med_mt = O.time_reduce("sum", "float32", src, dst, threads=threads, reps=5)
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    b = 3 * count * 4
+    return {
+        "value": round(b / med / GIB, 3),
+        "unit": "GiB/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle/combine_ref.c (-O3 -march=native) whole-buffer fp32 SUM of "
+                   f"2^{count.bit_length() - 1} elements (the reduce_cb_f call shape), "
+                   f"{reps} reps, median, {wall:.1f} s of CPU work"),
+        "best_gibs": round(b / best / GIB, 3),
+        "fragmented_8k_gibs": round(b / med_frag / GIB, 3),
+        f"threads_{threads}_gibs": round(b / med_mt / GIB, 3),
+        "cpu_model": cpu_model,
+        "online_cpus": os.cpu_count(),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--count", type=int, default=WORKLOAD_COUNT)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import xucg_amd
+
+    dist = None
+    if world > 1:
+        import datetime
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=600),
+                                device_id=torch.device(f"cuda:{local_rank}"))
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    n = args.count
+    ctx = xucg_amd.DevContext(device=local_rank)
+    src = ctx.alloc(n * 4)
+    dst = ctx.alloc(n * 4)
+    ctx.fill("float32", "round", 0x5EED0000 + 2 * rank, src, n)
+    ctx.fill("float32", "round", 0x5EED0001 + 2 * rank, dst, n)
+    ctx.sync()
+
+    for _ in range(args.warmup):
+        ctx.reduce_checked("sum", "float32", dst, src, n)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.reduce_checked("sum", "float32", dst, src, n)
+    ctx.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    bytes_per_step = 3 * n * 4  # algorithmic: read src, read dst, write dst
+    value = world * args.steps * bytes_per_step / elapsed / GIB
+
+    # roofline of the combine kernel: HIP events on the context's own stream
+    iters = 50
+    avg_us = ctx.profile_reduce("sum", "float32", dst, src, n, iters)
+    achieved = bytes_per_step / (avg_us * 1e-6) / 1e9
+
+    extra = {}
+    if not args.no_extra and rank == 0:
+        # north-star: 1 GiB fp32 combine, device-resident
+        nb = 1 << 28
+        s1, d1 = ctx.alloc(nb * 4), ctx.alloc(nb * 4)
+        ctx.fill("float32", "round", 11, s1, nb)
+        ctx.fill("float32", "round", 12, d1, nb)
+        ctx.profile_reduce("sum", "float32", d1, s1, nb, 5)
+        us1 = ctx.profile_reduce("sum", "float32", d1, s1, nb, 20)
+        g1 = 3 * nb * 4 / (us1 * 1e-6) / 1e9
+        extra["north_star_1gib_fp32_sum"] = {
+            "kernel_us": round(us1, 2), "achieved_gbs": round(g1, 1),
+            "gibs_3n": round(3 * nb * 4 / (us1 * 1e-6) / GIB, 1),
+            "frac_of_8tbs": round(g1 / HBM_PEAK_GBS, 4), "target_frac": 0.80}
+        s1.free()
+        d1.free()
+        # H2D/D2H-inclusive rate: host-resident (pinned) buffers, pipelined
+        hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)
+        ctx.combine_host("sum", "float32", hd, hs, n)  # warm the ring
+        reps = 5
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            rc = ctx.combine_host("sum", "float32", hd, hs, n)
+            assert rc == 0, xucg_amd._lib.last_error()
+        th = (time.perf_counter() - t1) / reps
+        extra["pcie_end_to_end_fp32_sum"] = {
+            "bytes": n * 4, "ms": round(th * 1e3, 3),
+            "gibs_3n": round(3 * n * 4 / th / GIB, 2),
+            "gibs_n": round(n * 4 / th / GIB, 2),
+            "note": "pinned host src/dst -> H2D -> kernel -> D2H, 8 MiB chunks on 2 streams"}
+        hs.free()
+        hd.free()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(n)
+
+    if rank == 0:
+        line = {
+            "metric": load_baseline_metric(),
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (counter-based splitmix64 generator, 'round' distribution)",
+            "config": {
+                "workload": "BASELINE config 2: device-resident local combine dst += src, "
+                            "2 x 256 MiB fp32 per GPU (ucg_builtin_dev_reduce)",
+                "count": n, "op": "sum", "bytes_per_step_per_gpu": bytes_per_step,
+                "parallelism": f"{world} independent per-rank shards (no data-path collective)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc_traffic(n),
+                "kernel": "ucgdev::k_reduce<float, SUM, 4, 0>",
+                "kernel_avg_us": round(avg_us, 3),
+                "algorithmic_bytes_per_launch": bytes_per_step,
+            },
+            "cpu_baseline": cpu,
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

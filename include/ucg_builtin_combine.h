@@ -1,0 +1,139 @@
+/*
+ * ucg_builtin_combine.h - host (C) side of the MI355X combine path inside
+ * UCG's builtin planner.
+ *
+ * This is what builtin/ops and builtin/plan call instead of invoking
+ * reduce_cb_f directly. It decides, per call, whether the combine runs on
+ * the device (through include/ucg_builtin_dev.h) or through the user's
+ * reduce_cb_f on the host, and restates the control-path rules the device
+ * path depends on. Reference anchors (paths relative to the reference tree):
+ *
+ *   ucg_builtin_combine_reduce()      replaces the body of
+ *                                     ucg_builtin_mpi_reduce(),
+ *                                     builtin/ops/builtin_comp_step.inl:96-102
+ *   ucg_builtin_combine_step_begin/
+ *   ucg_builtin_combine_fragment/
+ *   ucg_builtin_combine_step_end()    the REDUCE aggregation branch of
+ *                                     ucg_builtin_step_recv_handle_chunk(),
+ *                                     :184-232, around a whole step (begin at
+ *                                     ucg_builtin_step_execute, builtin/ops/
+ *                                     builtin_data.c:584; end before the next
+ *                                     step's send, builtin_comp_step.inl:60-95,
+ *                                     or completion, :8-38)
+ *   ucg_builtin_combine_create/
+ *   ucg_builtin_combine_destroy()     per-group state created in
+ *                                     ucg_builtin_create(), builtin/builtin.c:
+ *                                     376-456, freed in ucg_builtin_destroy()
+ *   ucg_builtin_step_fragment_length/
+ *   ucg_builtin_step_fragments_total() builtin/ops/builtin_control.c:434,462-465
+ *   ucg_builtin_recursive_*()         builtin/plan/builtin_recursive.c:20-228
+ *
+ * The callback types mirror ucg_params_t.datatype and .reduce_op
+ * (api/ucg.h:129-160) exactly; ucp_datatype_t is carried as uintptr_t.
+ */
+#ifndef UCG_BUILTIN_COMBINE_H_
+#define UCG_BUILTIN_COMBINE_H_
+
+#include "ucg_builtin_dev.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* api/ucg.h:129-160 (ucg_params_t.datatype / .reduce_op) */
+typedef struct ucg_builtin_reduce_params {
+    int (*reduce_cb_f)(void *reduce_op, char *src, char *dst, unsigned count,
+                       void *datatype);
+    int (*is_sum_f)(void *reduce_op);
+    int (*is_loc_expected_f)(void *reduce_op);
+    int (*is_commutative_f)(void *reduce_op);
+    int (*convert)(void *datatype, uintptr_t *ucp_datatype);
+    int (*is_integer_f)(void *datatype, int *is_signed);
+    int (*is_floating_point_f)(void *datatype);
+} ucg_builtin_reduce_params_t;
+
+/* Builtin-private knobs, read from the environment with the builtin
+ * planner's prefix (UCX_BUILTIN_, builtin/builtin.c:1015). */
+typedef struct ucg_builtin_combine_config {
+    int      dev_enable;     /* UCX_BUILTIN_DEV_COMBINE      y/n  (default y)  */
+    size_t   dev_min_bytes;  /* UCX_BUILTIN_DEV_MIN_BYTES    (default 1 MiB)   */
+    size_t   stage_bytes;    /* UCX_BUILTIN_DEV_STAGE_BYTES  (default 8 MiB)   */
+    unsigned stage_slots;    /* UCX_BUILTIN_DEV_STAGE_SLOTS  (default 4)       */
+    int      device;         /* UCX_BUILTIN_DEV_DEVICE       (default -1)      */
+} ucg_builtin_combine_config_t;
+
+typedef struct ucg_builtin_combine ucg_builtin_combine_t;
+
+/* builtin-private classifier (not part of api/): maps the opaque MPI handles
+ * to the device enums; return -1 when unknown. Without it only SUM (via
+ * is_sum_f) and size/int/float-classified types are device-eligible, and a
+ * 2-byte float is taken as fp16 (api/ cannot tell fp16 from bf16). */
+typedef int (*ucg_builtin_op_classifier_f)(void *reduce_op);
+typedef int (*ucg_builtin_dt_classifier_f)(void *datatype);
+
+void         ucg_builtin_combine_config_read(ucg_builtin_combine_config_t *cfg);
+ucs_status_t ucg_builtin_combine_create(const ucg_builtin_reduce_params_t *params,
+                                        const ucg_builtin_combine_config_t *cfg,
+                                        ucg_builtin_combine_t **cmb_p);
+void         ucg_builtin_combine_destroy(ucg_builtin_combine_t *cmb);
+void         ucg_builtin_combine_set_classifier(ucg_builtin_combine_t *cmb,
+                                                ucg_builtin_op_classifier_f op_cls,
+                                                ucg_builtin_dt_classifier_f dt_cls);
+/* 1 when (op, dtype) can run on the device; fills the enums. */
+int          ucg_builtin_combine_classify(ucg_builtin_combine_t *cmb,
+                                          void *reduce_op, void *datatype,
+                                          ucg_dev_op_t *op, ucg_dev_dtype_t *dt);
+/* 1 when a device context is attached (a GPU was found and enabled). */
+int          ucg_builtin_combine_has_device(ucg_builtin_combine_t *cmb);
+ucg_builtin_dev_ctx_t *ucg_builtin_combine_dev_ctx(ucg_builtin_combine_t *cmb);
+
+/* The combine itself: dst[i] = src[i] (op) dst[i] on host memory, the exact
+ * contract of reduce_cb_f. Whole-buffer calls of at least dev_min_bytes go
+ * to the device (H2D -> kernel -> D2H); everything else, and every op or
+ * type the device cannot classify, calls reduce_cb_f. The callback's return
+ * value is propagated here (the reference discards it). */
+ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
+                                        void *reduce_op, void *src, void *dst,
+                                        int dcount, void *datatype);
+
+/* Step-scoped device staging for fragmented REDUCE steps: between begin and
+ * end the step's receive buffer is mirrored on the device, every fragment is
+ * copied into the pinned ring before the call returns and consecutive ones
+ * are combined in one launch. Steps below dev_min_bytes, or not classified,
+ * fall back to reduce_cb_f per fragment with identical results. */
+ucs_status_t ucg_builtin_combine_step_begin(ucg_builtin_combine_t *cmb,
+                                            void *reduce_op, void *datatype,
+                                            void *recv_buffer, size_t length);
+ucs_status_t ucg_builtin_combine_fragment(ucg_builtin_combine_t *cmb,
+                                          size_t offset, const void *src,
+                                          size_t length);
+ucs_status_t ucg_builtin_combine_step_end(ucg_builtin_combine_t *cmb);
+
+/* [0] host calls, [1] host bytes, [2] device calls, [3] device bytes,
+ * [4] steps staged on the device, [5] callback errors seen */
+void         ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb,
+                                       uint64_t out[6]);
+
+/* ---- control-path rules the device path depends on ---------------------- */
+/* builtin/ops/builtin_control.c:434,462: whole-element AM-short fragment */
+size_t       ucg_builtin_step_fragment_length(size_t max_short, size_t dt_len);
+/* builtin/ops/builtin_control.c:463-465 */
+uint64_t     ucg_builtin_step_fragments_total(size_t length, size_t frag_len,
+                                              unsigned ep_cnt);
+/* Device launch granularity for a fragmented step: fragments are aggregated
+ * into runs of at most this many bytes (a whole number of fragments). */
+size_t       ucg_builtin_dev_chunk_bytes(size_t length, size_t frag_len,
+                                         size_t slot_bytes);
+/* builtin/plan/builtin_recursive.c:76-88: number of recursive steps for
+ * `count` members and `factor`, or 0 when count is not a power of factor */
+unsigned     ucg_builtin_recursive_steps(uint64_t count, unsigned factor);
+/* builtin/plan/builtin_recursive.c:158-169: peer #peer_idx (1..factor-1) of
+ * member `my` at 1-based step `step` */
+uint64_t     ucg_builtin_recursive_peer(uint64_t my, unsigned step,
+                                        unsigned factor, unsigned peer_idx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

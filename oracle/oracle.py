@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+LIB_PATH = os.environ.get("UCG_ORACLE_LIB", os.path.join(HERE, "_build", "liboracle.so"))
 
 DTYPES = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64",
           "uint64", "float16", "bfloat16", "float32", "float64"]
@@ -34,6 +34,13 @@ def build(force=False):
     if force or not os.path.exists(LIB_PATH):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB_PATH
+
+
+def build_native():
+    """Build oracle/_build/native/liboracle.so with -march=native on THIS host
+    (used by bench.py's cpu_baseline on the GPU box)."""
+    subprocess.run(["make", "-s", "-C", HERE, "native"], check=True)
+    return os.path.join(HERE, "_build", "native", "liboracle.so")
 
 
 def lib():

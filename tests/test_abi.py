@@ -1,0 +1,63 @@
+"""CPU: the C-ABI libraries load and export every symbol the headers declare;
+the introspection entry points work without a GPU. No compute calls."""
+import ctypes
+import os
+import re
+
+import pytest
+
+import xucg_amd
+from xucg_amd import _lib
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared(header):
+    text = open(os.path.join(ROOT, "include", header)).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ucg_builtin_\w+)\s*\(", text)))
+
+
+def test_dev_library_exports_every_declared_symbol():
+    names = declared("ucg_builtin_dev.h")
+    assert len(names) >= 20
+    lib = ctypes.CDLL(_lib.DEV_LIB)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the Python binding covers exactly the declared surface
+    assert sorted(_lib.DEV_API) == names
+
+
+def test_host_library_exports_every_declared_symbol():
+    names = declared("ucg_builtin_combine.h")
+    assert len(names) >= 10
+    lib = ctypes.CDLL(_lib.HOST_LIB)
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    from xucg_amd import host_api
+    assert sorted(host_api.HOST_API) == names
+
+
+def test_support_table_matches_oracle():
+    for dt in range(len(O.DTYPES)):
+        assert xucg_amd.dtype_size(dt) == O.lib().ucg_oracle_dtype_size(dt)
+        assert _lib.dev().ucg_builtin_dev_dtype_size(dt) == xucg_amd.dtype_size(dt)
+        for op in range(len(O.OPS)):
+            assert xucg_amd.is_supported(dt, op) == O.is_supported(dt, op)
+    assert not xucg_amd.is_supported(99, 0)
+    assert not xucg_amd.is_supported(0, 99)
+
+
+def test_version_and_errors_without_gpu():
+    assert b"gfx950" in _lib.dev().ucg_builtin_dev_version()
+    if xucg_amd.device_count() > 0:
+        pytest.skip("a GPU is visible; the no-device path is not reachable")
+    with pytest.raises(xucg_amd.UcsError) as e:
+        xucg_amd.DevContext(device=0)
+    assert e.value.status == xucg_amd.UCS_ERR_NO_DEVICE
+    # NULL context is rejected, not dereferenced
+    L = _lib.dev()
+    assert L.ucg_builtin_dev_reduce(None, 0, 10, None, None, 4) == _lib.UCS_ERR_INVALID_PARAM
+    assert L.ucg_builtin_dev_sync(None) == _lib.UCS_ERR_INVALID_PARAM
+    assert L.ucg_builtin_dev_stage_end(None) == _lib.UCS_ERR_INVALID_PARAM

@@ -1,0 +1,259 @@
+"""GPU parity: the HIP combine path (through the C-ABI) against the oracle and
+the golden vectors. Bit-exact for every dtype and op."""
+import os
+
+import numpy as np
+import pytest
+
+import xucg_amd
+from xucg_amd import _lib
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def bits(a):
+    return O.bits(a)
+
+
+def run_reduce(ctx, op, dt, src, dst, src_off=0, dst_off=0):
+    """Upload, combine on the device, download. Offsets in bytes."""
+    st = O.storage(dt)
+    n = src.size
+    nb = n * np.dtype(st).itemsize
+    bs = ctx.alloc(nb + 64)
+    bd = ctx.alloc(nb + 64)
+    bs.upload(src, src_off)
+    bd.upload(dst, dst_off)
+    rc = ctx.reduce(op, dt, bd.ptr + dst_off, bs.ptr + src_off, n)
+    assert rc == 0, _lib.last_error()
+    ctx.sync()
+    return bd.download(st, n, dst_off)
+
+
+@pytest.mark.parametrize("dt", O.DTYPES)
+def test_golden_vectors_on_gpu(dev_ctx, dt):
+    z = np.load(os.path.join(GOLDEN, f"golden_{dt}.npz"))
+    sz = np.dtype(O.storage(dt)).itemsize
+    for k, op in enumerate(O.OPS):
+        if not z["supported"][k]:
+            assert dev_ctx.reduce(op, dt, 0, 0, 4) == xucg_amd.UCS_ERR_UNSUPPORTED
+            continue
+        # aligned, dst-misaligned-with-src (same phase) and relative-misaligned
+        for so, do in ((0, 0), (sz, sz), (0, sz), (3 * sz, 5 * sz)):
+            got = run_reduce(dev_ctx, op, dt, z["src"], z["dst"], so, do)
+            bad = np.nonzero(bits(got) != bits(z["out"][k]))[0]
+            assert bad.size == 0, (op, so, do, [
+                (hex(int(bits(z["src"])[i])), hex(int(bits(z["dst"])[i])),
+                 hex(int(bits(got)[i])), hex(int(bits(z["out"][k])[i]))) for i in bad[:4]])
+
+
+@pytest.mark.parametrize("dt", O.DTYPES)
+def test_fill_matches_oracle(dev_ctx, dt):
+    n = 10007
+    buf = dev_ctx.alloc(n * 8)
+    for dist in O.DISTS:
+        dev_ctx.fill(dt, dist, 0xC0FFEE, buf, n)
+        dev_ctx.sync()
+        got = buf.download(O.storage(dt), n)
+        want = O.fill(dt, dist, 0xC0FFEE, n)
+        assert (bits(got) == bits(want)).all(), dist
+
+
+SIZES = [1, 2, 3, 7, 15, 16, 17, 31, 33, 255, 256, 257, 1000, 4099, 65537,
+         (1 << 20) + 3]
+
+
+@pytest.mark.parametrize("dt", O.DTYPES)
+def test_ragged_sizes_vs_oracle(dev_ctx, dt):
+    rng = np.random.default_rng(O.dt_index(dt))
+    st = O.storage(dt)
+    for n in SIZES:
+        for dist in ("round", "special"):
+            src = O.fill(dt, dist, 11 + n, n)
+            dst = O.fill(dt, dist, 12 + n, n)
+            ops = [op for op in O.OPS if O.is_supported(dt, op)]
+            op = ops[int(rng.integers(len(ops)))] if n > 4099 else None
+            for o in ([op] if op else ops):
+                off = int(rng.integers(0, 4)) * np.dtype(st).itemsize
+                got = run_reduce(dev_ctx, o, dt, src, dst, off, off)
+                want = O.reduce(o, dt, src, dst)
+                assert (bits(got) == bits(want)).all(), (o, n, dist)
+
+
+def test_zero_count_is_noop(dev_ctx):
+    assert dev_ctx.reduce("sum", "float32", 0, 0, 0) == 0
+
+
+def test_self_combine(dev_ctx):
+    n = 12345
+    x = O.fill("float32", "round", 3, n)
+    b = dev_ctx.alloc(n * 4)
+    b.upload(x)
+    assert dev_ctx.reduce("sum", "float32", b, b, n) == 0
+    dev_ctx.sync()
+    assert (bits(b.download(np.float32, n)) == bits(O.reduce("sum", "float32", x, x))).all()
+
+
+def test_argument_errors(dev_ctx):
+    b = dev_ctx.alloc(4096)
+    # partial overlap
+    assert dev_ctx.reduce("sum", "float32", b.ptr, b.ptr + 4, 100) == xucg_amd.UCS_ERR_INVALID_PARAM
+    # not element-aligned
+    assert dev_ctx.reduce("sum", "float32", b.ptr + 2, b.ptr + 2050, 10) == xucg_amd.UCS_ERR_INVALID_PARAM
+    # float bitwise
+    assert dev_ctx.reduce("bxor", "float64", b.ptr, b.ptr + 2048, 10) == xucg_amd.UCS_ERR_UNSUPPORTED
+    # multi: non power of two
+    assert dev_ctx.reduce_multi("sum", "int32", b, [b, b, b], 0, 10) == xucg_amd.UCS_ERR_INVALID_PARAM
+    # fragment outside a staged step
+    assert dev_ctx.combine("sum", "int32", 0, np.zeros(4, np.int32), 4) == xucg_amd.UCS_ERR_OUT_OF_RANGE
+
+
+def test_c2_full_size_fp32_sum(dev_ctx):
+    """BASELINE config 2 at full size: 2 x 256 MiB fp32, device-resident,
+    bit-exact against the oracle over all 2^26 elements."""
+    n = 1 << 26
+    bs, bd = dev_ctx.alloc(n * 4), dev_ctx.alloc(n * 4)
+    dev_ctx.fill("float32", "round", 0x5EED0000, bs, n)
+    dev_ctx.fill("float32", "round", 0x5EED0001, bd, n)
+    assert dev_ctx.reduce("sum", "float32", bd, bs, n) == 0
+    dev_ctx.sync()
+    got = bd.download(np.float32, n)
+    want = O.reduce("sum", "float32", O.fill("float32", "round", 0x5EED0000, n),
+                    O.fill("float32", "round", 0x5EED0001, n))
+    assert (bits(got) == bits(want)).all()
+
+
+@pytest.mark.parametrize("dt,op", [("float32", "sum"), ("float32", "prod"),
+                                   ("float64", "sum"), ("int32", "sum"),
+                                   ("float16", "sum"), ("bfloat16", "max"),
+                                   ("uint8", "bxor")])
+@pytest.mark.parametrize("nsrc", [1, 2, 4, 8, 16])
+def test_reduce_multi_recursive_doubling(dev_ctx, dt, op, nsrc):
+    n = 5003
+    st = O.storage(dt)
+    sz = np.dtype(st).itemsize
+    dist = "special" if dt.startswith("float") else "round"
+    xs = [O.fill(dt, dist, 900 + r, n) for r in range(nsrc)]
+    bufs = []
+    for r, x in enumerate(xs):
+        b = dev_ctx.alloc(n * sz + 64)
+        b.upload(x)
+        bufs.append(b)
+    out = dev_ctx.alloc(n * sz + 64)
+    for self_index in sorted({0, nsrc - 1, nsrc // 2}):
+        for off in (0, sz):  # aligned and shifted by one element (all agree)
+            for b, x in zip(bufs, xs):
+                b.upload(x, off)
+            srcs = [b.ptr + off for b in bufs]
+            rc = dev_ctx.reduce_multi(op, dt, out.ptr + off, srcs, self_index, n)
+            assert rc == 0, _lib.last_error()
+            dev_ctx.sync()
+            got = out.download(st, n, off)
+            want = O.reduce_multi(op, dt, xs, self_index)
+            assert (bits(got) == bits(want)).all(), (self_index, off)
+    # sources disagreeing mod 16 B -> scalar path
+    if nsrc > 1:
+        for b, x in zip(bufs, xs):
+            b.upload(x)
+        bufs[0].upload(xs[0], sz)
+        srcs = [bufs[0].ptr + sz] + [b.ptr for b in bufs[1:]]
+        assert dev_ctx.reduce_multi(op, dt, out.ptr, srcs, 0, n) == 0
+        dev_ctx.sync()
+        assert (bits(out.download(st, n)) == bits(O.reduce_multi(op, dt, xs, 0))).all()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_combine_host_pipeline(pinned):
+    """Host-resident whole-buffer combine: H2D -> kernel -> D2H in 1 MiB chunks."""
+    n = (3 << 20) + 5  # crosses many ring slots, ragged tail
+    ctx = xucg_amd.DevContext(device=0, stage_bytes=1 << 20, stage_slots=3)
+    try:
+        src = O.fill("float32", "round", 41, n)
+        dst = O.fill("float32", "round", 42, n)
+        want = O.reduce("sum", "float32", src, dst)
+        if pinned:
+            hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)
+            vs, vd = hs.view(np.float32, n), hd.view(np.float32, n)
+            vs[:] = src
+            vd[:] = dst
+            assert ctx.combine_host("sum", "float32", hd.ptr, hs.ptr, n) == 0, _lib.last_error()
+            got = vd.copy()
+        else:
+            d = dst.copy()
+            assert ctx.combine_host("sum", "float32", d, src, n) == 0, _lib.last_error()
+            got = d
+        assert (bits(got) == bits(want)).all()
+        c = ctx.counters()
+        assert c["h2d_bytes"] == 2 * n * 4 and c["d2h_bytes"] == n * 4
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("dt,op", [("float32", "sum"), ("float64", "prod"),
+                                   ("int32", "max"), ("float16", "sum")])
+def test_staged_fragments_like_the_am_handler(dt, op):
+    """Per-step staging: fragments of the reference's AM-short size arrive
+    from two peers in interleaved order (a tree fan-in with ep_cnt = 2) and
+    are combined in arrival order, exactly like ucg_builtin_step_recv_cb()."""
+    ctx = xucg_amd.DevContext(device=0, stage_bytes=64 << 10, stage_slots=4)
+    try:
+        st = O.storage(dt)
+        sz = np.dtype(st).itemsize
+        n = 40_000 + 3
+        acc = O.fill(dt, "round", 7, n)
+        peers = [O.fill(dt, "round", 8 + p, n) for p in range(2)]
+        frag = O.frag_length(256, sz)            # (max_short - 8) rounded
+        want = acc.copy()
+        host = acc.copy()
+        assert ctx.stage_begin(host, host.nbytes) == 0
+        order = []
+        for off in range(0, n * sz, frag):
+            for p in range(2):
+                order.append((p, off))
+        for p, off in order:
+            cnt = min(frag, n * sz - off) // sz
+            i0 = off // sz
+            piece = np.ascontiguousarray(peers[p][i0:i0 + cnt])
+            assert ctx.combine(op, dt, off, piece, cnt) == 0, _lib.last_error()
+            want[i0:i0 + cnt] = O.reduce(op, dt, piece, want[i0:i0 + cnt])
+        assert ctx.stage_end() == 0, _lib.last_error()
+        assert (bits(host) == bits(want)).all()
+        c = ctx.counters()
+        # aggregation: far fewer launches than fragments
+        assert c["launches"] < len(order) / 4
+    finally:
+        ctx.close()
+
+
+def test_staged_contiguous_fragments_one_launch_per_slot():
+    ctx = xucg_amd.DevContext(device=0, stage_bytes=1 << 20, stage_slots=2)
+    try:
+        n = 1 << 20  # 4 MiB of fp32 = 4 slots
+        acc = O.fill("float32", "exact", 1, n)
+        src = O.fill("float32", "exact", 2, n)
+        host = acc.copy()
+        assert ctx.stage_begin(host, host.nbytes) == 0
+        frag = O.frag_length(8192, 4)
+        for off in range(0, n * 4, frag):
+            cnt = min(frag, n * 4 - off) // 4
+            assert ctx.combine("sum", "float32", off, src[off // 4: off // 4 + cnt], cnt) == 0
+        assert ctx.stage_end() == 0
+        assert (bits(host) == bits(O.reduce("sum", "float32", src, acc))).all()
+        assert ctx.counters()["launches"] == 4
+    finally:
+        ctx.close()
+
+
+def test_profile_hook_and_counters(dev_ctx):
+    n = 1 << 22
+    bs, bd = dev_ctx.alloc(n * 4), dev_ctx.alloc(n * 4)
+    dev_ctx.fill("float32", "exact", 1, bs, n)
+    dev_ctx.fill("float32", "exact", 2, bd, n)
+    before = dev_ctx.counters()
+    us = dev_ctx.profile_reduce("sum", "float32", bd, bs, n, 10)
+    after = dev_ctx.counters()
+    assert 0 < us < 10_000
+    assert after["launches"] - before["launches"] == 10
+    assert after["combined_bytes"] - before["combined_bytes"] == 10 * 3 * n * 4

@@ -1,0 +1,980 @@
+/*
+ * dev_combine.hip - C-ABI device shim of the UCG builtin combine (MI355X).
+ *
+ * Implements include/ucg_builtin_dev.h. Every entry point is extern "C" with
+ * plain pointers and sizes; each replaces or serves one reference interface
+ * (see the header). Errors are returned as ucs_status_t and described by
+ * ucg_builtin_dev_last_error(); there is no CPU fallback in this library.
+ */
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <algorithm>
+#include <utility>
+
+#include "ucg_builtin_dev.h"
+#include "dev_kernels.h"
+
+using namespace ucgdev;
+
+/* ------------------------------------------------------------------------ */
+/* errors                                                                   */
+/* ------------------------------------------------------------------------ */
+static thread_local std::string g_last_error;
+
+static ucs_status_t set_error(ucs_status_t st, const char *what, const char *why)
+{
+    g_last_error = std::string(what) + ": " + why;
+    return st;
+}
+
+static ucs_status_t hip_status(hipError_t e, const char *what)
+{
+    if (e == hipSuccess) {
+        return UCS_OK;
+    }
+    ucs_status_t st;
+    switch (e) {
+    case hipErrorNoDevice:
+    case hipErrorInvalidDevice:
+        st = UCS_ERR_NO_DEVICE;
+        break;
+    case hipErrorOutOfMemory:
+        st = UCS_ERR_NO_MEMORY;
+        break;
+    case hipErrorInvalidValue:
+        st = UCS_ERR_INVALID_PARAM;
+        break;
+    default:
+        st = UCS_ERR_IO_ERROR;
+        break;
+    }
+    return set_error(st, what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(_call)                                                        \
+    do {                                                                      \
+        hipError_t _e = (_call);                                              \
+        if (_e != hipSuccess) {                                               \
+            return hip_status(_e, #_call);                                    \
+        }                                                                     \
+    } while (0)
+
+/* ------------------------------------------------------------------------ */
+/* launch configuration (builtin-private knobs, UCX_BUILTIN_DEV_*)          */
+/* ------------------------------------------------------------------------ */
+struct LaunchCfg {
+    int max_blocks;  /* grid cap for the streaming kernels */
+    int variant;     /* fp32-SUM tuning variant (0 = product default) */
+};
+
+static LaunchCfg g_cfg = {-1, -1};
+
+static const LaunchCfg &launch_cfg()
+{
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char *b = getenv("UCX_BUILTIN_DEV_MAX_BLOCKS");
+        const char *v = getenv("UCX_BUILTIN_DEV_VARIANT");
+        g_cfg.max_blocks = b ? atoi(b) : 2048;
+        if (g_cfg.max_blocks < 1) {
+            g_cfg.max_blocks = 2048;
+        }
+        g_cfg.variant = v ? atoi(v) : 0; /* U = 4, non-temporal */
+    });
+    return g_cfg;
+}
+
+static size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
+
+static unsigned grid_for(size_t work_items, size_t per_block, int cap)
+{
+    size_t g = div_up(work_items, per_block);
+    if (g < 1) {
+        g = 1;
+    }
+    if (g > (size_t)cap) {
+        g = (size_t)cap;
+    }
+    return (unsigned)g;
+}
+
+/* ------------------------------------------------------------------------ */
+/* reduce launchers                                                         */
+/* ------------------------------------------------------------------------ */
+typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
+                                  hipStream_t st, int variant);
+
+template <typename T, int OP, int U, int NT>
+static void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
+                       hipStream_t st)
+{
+    /* one tile of U vectors per lane: grid sized to the data (no cap) */
+    const unsigned grid = grid_for(nvec, (size_t)kBlock * U, 0x7fffffff);
+    hipLaunchKernelGGL((k_reduce<T, OP, U, NT>), dim3(grid), dim3(kBlock), 0, st,
+                       d, s, head, nvec, tail);
+}
+
+template <int DT, int OP>
+static hipError_t launch_reduce(void *dst, const void *src, size_t count,
+                                hipStream_t st, int variant)
+{
+    typedef typename DtType<DT>::T T;
+    constexpr size_t sz = sizeof(T);
+    constexpr size_t V  = 16 / sz;
+    T *d       = static_cast<T*>(dst);
+    const T *s = static_cast<const T*>(src);
+    const uintptr_t md = (uintptr_t)dst & 15, ms = (uintptr_t)src & 15;
+
+    if (md != ms) {
+        /* operands disagree mod 16 B: no common vector alignment */
+        const unsigned grid = grid_for(count, (size_t)kBlock * 4,
+                                       launch_cfg().max_blocks);
+        hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(grid), dim3(kBlock),
+                           0, st, d, s, count);
+        return hipGetLastError();
+    }
+    size_t head = md ? (16 - md) / sz : 0;
+    if (head > count) {
+        head = count;
+    }
+    const size_t rem  = count - head;
+    const size_t nvec = rem / V, tail = rem % V;
+
+    if (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM && variant >= 0) {
+        /* tuning variants of the headline kernel (UCX_BUILTIN_DEV_VARIANT) */
+        switch (variant) {
+        case 1: launch_vec<T, OP, 2, 1>(d, s, head, nvec, tail, st); break;
+        case 2: launch_vec<T, OP, 4, 0>(d, s, head, nvec, tail, st); break;
+        case 3: launch_vec<T, OP, 2, 0>(d, s, head, nvec, tail, st); break;
+        default: launch_vec<T, OP, kReduceU, 1>(d, s, head, nvec, tail, st); break;
+        }
+    } else {
+        launch_vec<T, OP, kReduceU, 1>(d, s, head, nvec, tail, st);
+    }
+    return hipGetLastError();
+}
+
+template <int DT, int OP>
+constexpr reduce_fn_t reduce_entry()
+{
+    if constexpr (pair_supported(DT, OP)) {
+        return &launch_reduce<DT, OP>;
+    } else {
+        return nullptr;
+    }
+}
+
+template <int DT, int... OPS>
+constexpr std::array<reduce_fn_t, UCG_DEV_OP_LAST>
+reduce_row(std::integer_sequence<int, OPS...>)
+{
+    return {reduce_entry<DT, OPS>()...};
+}
+
+template <int... DTS>
+constexpr std::array<std::array<reduce_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>
+reduce_table(std::integer_sequence<int, DTS...>)
+{
+    return {reduce_row<DTS>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>())...};
+}
+
+static const auto g_reduce =
+    reduce_table(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
+
+/* ---- multi-operand (recursive-doubling association) --------------------- */
+typedef hipError_t (*multi_fn_t)(void *dst, const SrcList &srcs, unsigned n,
+                                 unsigned self, size_t count, hipStream_t st);
+
+template <typename T, int OP, int N>
+static hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
+                                 size_t count, hipStream_t st)
+{
+    constexpr size_t sz = sizeof(T), V = 16 / sz;
+    const uintptr_t md = (uintptr_t)dst & 15;
+    bool aligned = true;
+    for (int m = 0; m < N; m++) {
+        aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
+    }
+    T *d = static_cast<T*>(dst);
+    if (!aligned) {
+        const unsigned grid = grid_for(count, kBlock, launch_cfg().max_blocks);
+        hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP, N>), dim3(grid),
+                           dim3(kBlock), 0, st, d, srcs, self, count);
+        return hipGetLastError();
+    }
+    size_t head = md ? (16 - md) / sz : 0;
+    if (head > count) {
+        head = count;
+    }
+    const size_t rem = count - head, nvec = rem / V, tail = rem % V;
+    const unsigned grid = grid_for(nvec, (size_t)kBlock * kMultiU, 0x7fffffff);
+    hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kBlock), 0,
+                       st, d, srcs, self, head, nvec, tail);
+    return hipGetLastError();
+}
+
+template <int DT, int OP>
+static hipError_t launch_multi(void *dst, const SrcList &srcs, unsigned n,
+                               unsigned self, size_t count, hipStream_t st)
+{
+    typedef typename DtType<DT>::T T;
+    switch (n) {
+    case 1:  return launch_multi_n<T, OP, 1>(dst, srcs, self, count, st);
+    case 2:  return launch_multi_n<T, OP, 2>(dst, srcs, self, count, st);
+    case 4:  return launch_multi_n<T, OP, 4>(dst, srcs, self, count, st);
+    case 8:  return launch_multi_n<T, OP, 8>(dst, srcs, self, count, st);
+    case 16: return launch_multi_n<T, OP, 16>(dst, srcs, self, count, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int DT, int OP>
+constexpr multi_fn_t multi_entry()
+{
+    if constexpr (pair_supported(DT, OP)) {
+        return &launch_multi<DT, OP>;
+    } else {
+        return nullptr;
+    }
+}
+
+template <int DT, int... OPS>
+constexpr std::array<multi_fn_t, UCG_DEV_OP_LAST>
+multi_row(std::integer_sequence<int, OPS...>)
+{
+    return {multi_entry<DT, OPS>()...};
+}
+
+template <int... DTS>
+constexpr std::array<std::array<multi_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>
+multi_table(std::integer_sequence<int, DTS...>)
+{
+    return {multi_row<DTS>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>())...};
+}
+
+static const auto g_multi =
+    multi_table(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
+
+/* ---- generator ---------------------------------------------------------- */
+typedef void (*fill_fn_t)(void *dst, int dist, uint64_t key, size_t count,
+                          hipStream_t st);
+
+template <int DT>
+static void launch_fill(void *dst, int dist, uint64_t key, size_t count,
+                        hipStream_t st)
+{
+    const unsigned grid = grid_for(count, kBlock, 4096);
+    hipLaunchKernelGGL((k_fill<DT>), dim3(grid), dim3(kBlock), 0, st, dst, dist,
+                       key, count);
+}
+
+template <int... DTS>
+constexpr std::array<fill_fn_t, UCG_DEV_DT_LAST>
+fill_table(std::integer_sequence<int, DTS...>)
+{
+    return {&launch_fill<DTS>...};
+}
+
+static const auto g_fill =
+    fill_table(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
+
+/* ------------------------------------------------------------------------ */
+/* context                                                                  */
+/* ------------------------------------------------------------------------ */
+static const size_t kDtSize[UCG_DEV_DT_LAST] = {1, 1, 2, 2, 4, 4, 8, 8, 2, 2, 4, 8};
+
+struct ucg_builtin_dev_ctx {
+    int          device;
+    hipStream_t  stream;       /* compute + H2D (owned unless passed in) */
+    hipStream_t  stream_d2h;   /* D2H of the host pipeline (always owned) */
+    bool         own_stream;
+
+    /* pinned staging ring (lazy) */
+    std::mutex   lock;
+    size_t       slot_bytes;
+    unsigned     nslots;
+    char        *h_ring;       /* pinned host, nslots * slot_bytes */
+    char        *d_ring;       /* device src slots                 */
+    char        *d_ring2;      /* device dst slots (host pipeline) */
+    hipEvent_t  *slot_ev;      /* slot free once this completes    */
+    bool        *slot_used;
+    unsigned     next_slot;
+
+    /* per-step accumulator mirror */
+    void        *host_dst;
+    size_t       stage_len;
+    char        *d_acc;
+    size_t       d_acc_cap;
+
+    /* pending fragment runs, each aggregated into one launch and flushed in
+     * the order they were started (see ucg_builtin_dev_combine) */
+    struct Run {
+        bool     active;
+        unsigned slot;
+        size_t   used, off;
+        int      op, dt;
+        uint64_t seq;
+    }            runs[4];
+    unsigned     max_runs;
+    uint64_t     run_seq;
+
+    std::atomic<uint64_t> counters[4];
+};
+
+static ucs_status_t set_device(ucg_builtin_dev_ctx_t *ctx)
+{
+    HIP_TRY(hipSetDevice(ctx->device));
+    return UCS_OK;
+}
+
+static ucs_status_t ring_init(ucg_builtin_dev_ctx_t *ctx)
+{
+    if (ctx->h_ring) {
+        return UCS_OK;
+    }
+    const size_t total = ctx->slot_bytes * ctx->nslots;
+    HIP_TRY(hipHostMalloc((void**)&ctx->h_ring, total, hipHostMallocDefault));
+    HIP_TRY(hipMalloc((void**)&ctx->d_ring, total));
+    HIP_TRY(hipMalloc((void**)&ctx->d_ring2, total));
+    ctx->slot_ev   = new hipEvent_t[ctx->nslots];
+    ctx->slot_used = new bool[ctx->nslots];
+    for (unsigned i = 0; i < ctx->nslots; i++) {
+        HIP_TRY(hipEventCreateWithFlags(&ctx->slot_ev[i], hipEventDisableTiming));
+        ctx->slot_used[i] = false;
+    }
+    return UCS_OK;
+}
+
+/* take the next ring slot, waiting until its previous use has drained */
+static ucs_status_t slot_acquire(ucg_builtin_dev_ctx_t *ctx, unsigned *slot)
+{
+    const unsigned k = ctx->next_slot;
+    ctx->next_slot   = (k + 1) % ctx->nslots;
+    if (ctx->slot_used[k]) {
+        HIP_TRY(hipEventSynchronize(ctx->slot_ev[k]));
+    }
+    ctx->slot_used[k] = true;
+    *slot = k;
+    return UCS_OK;
+}
+
+extern "C" {
+
+size_t ucg_builtin_dev_dtype_size(ucg_dev_dtype_t dt)
+{
+    return ((int)dt >= 0 && dt < UCG_DEV_DT_LAST) ? kDtSize[dt] : 0;
+}
+
+int ucg_builtin_dev_is_supported(ucg_dev_dtype_t dt, ucg_dev_op_t op)
+{
+    if ((int)dt < 0 || dt >= UCG_DEV_DT_LAST || (int)op < 0 || op >= UCG_DEV_OP_LAST) {
+        return 0;
+    }
+    return g_reduce[dt][op] != nullptr;
+}
+
+const char *ucg_builtin_dev_version(void)
+{
+    return "xucg_amd-dev 0.1.0 gfx950";
+}
+
+const char *ucg_builtin_dev_last_error(void)
+{
+    return g_last_error.c_str();
+}
+
+int ucg_builtin_dev_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        return 0;
+    }
+    return n;
+}
+
+ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *params,
+                                        ucg_builtin_dev_ctx_t **ctx_p)
+{
+    if (ctx_p == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ctx_create", "ctx_p is NULL");
+    }
+    *ctx_p = nullptr;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (ndev <= 0) {
+        return set_error(UCS_ERR_NO_DEVICE, "ctx_create", "no HIP device");
+    }
+    ucg_builtin_dev_ctx_t *ctx = new ucg_builtin_dev_ctx_t();
+    ctx->device      = -1;
+    ctx->stream      = nullptr;
+    ctx->stream_d2h  = nullptr;
+    ctx->own_stream  = true;
+    ctx->slot_bytes  = 8u << 20;
+    ctx->nslots      = 4;
+    ctx->h_ring = ctx->d_ring = ctx->d_ring2 = nullptr;
+    ctx->slot_ev     = nullptr;
+    ctx->slot_used   = nullptr;
+    ctx->next_slot   = 0;
+    ctx->host_dst    = nullptr;
+    ctx->stage_len   = 0;
+    ctx->d_acc       = nullptr;
+    ctx->d_acc_cap   = 0;
+    for (auto &r : ctx->runs) {
+        r.active = false;
+    }
+    ctx->run_seq     = 0;
+    for (auto &c : ctx->counters) {
+        c = 0;
+    }
+    void *user_stream = nullptr;
+    if (params) {
+        ctx->device = params->device;
+        user_stream = params->stream;
+        if (params->stage_bytes) {
+            ctx->slot_bytes = (params->stage_bytes + 255) & ~(size_t)255;
+        }
+        if (params->stage_slots) {
+            ctx->nslots = params->stage_slots < 2 ? 2 : params->stage_slots;
+        }
+    }
+    ctx->max_runs = ctx->nslots - 1 < 4 ? ctx->nslots - 1 : 4;
+    ucs_status_t st = UCS_OK;
+    hipError_t e;
+    if (ctx->device < 0) {
+        e = hipGetDevice(&ctx->device);
+    } else if (ctx->device >= ndev) {
+        e = hipErrorInvalidDevice;
+    } else {
+        e = hipSetDevice(ctx->device);
+    }
+    if (e == hipSuccess) {
+        if (user_stream) {
+            ctx->stream     = (hipStream_t)user_stream;
+            ctx->own_stream = false;
+        } else {
+            e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+        }
+    }
+    if (e == hipSuccess) {
+        e = hipStreamCreateWithFlags(&ctx->stream_d2h, hipStreamNonBlocking);
+    }
+    if (e != hipSuccess) {
+        st = hip_status(e, "ctx_create");
+        ucg_builtin_dev_ctx_destroy(ctx);
+        return st;
+    }
+    *ctx_p = ctx;
+    return UCS_OK;
+}
+
+void ucg_builtin_dev_ctx_destroy(ucg_builtin_dev_ctx_t *ctx)
+{
+    if (ctx == nullptr) {
+        return;
+    }
+    if (ctx->device >= 0) {
+        (void)hipSetDevice(ctx->device);
+    }
+    if (ctx->stream) {
+        (void)hipStreamSynchronize(ctx->stream);
+    }
+    if (ctx->stream_d2h) {
+        (void)hipStreamSynchronize(ctx->stream_d2h);
+        (void)hipStreamDestroy(ctx->stream_d2h);
+    }
+    if (ctx->slot_ev) {
+        for (unsigned i = 0; i < ctx->nslots; i++) {
+            (void)hipEventDestroy(ctx->slot_ev[i]);
+        }
+        delete[] ctx->slot_ev;
+    }
+    delete[] ctx->slot_used;
+    if (ctx->h_ring) {
+        (void)hipHostFree(ctx->h_ring);
+    }
+    if (ctx->d_ring) {
+        (void)hipFree(ctx->d_ring);
+    }
+    if (ctx->d_ring2) {
+        (void)hipFree(ctx->d_ring2);
+    }
+    if (ctx->d_acc) {
+        (void)hipFree(ctx->d_acc);
+    }
+    if (ctx->stream && ctx->own_stream) {
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+void *ucg_builtin_dev_ctx_stream(ucg_builtin_dev_ctx_t *ctx)
+{
+    return ctx ? (void*)ctx->stream : nullptr;
+}
+
+ucs_status_t ucg_builtin_dev_sync(ucg_builtin_dev_ctx_t *ctx)
+{
+    if (ctx == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "sync", "ctx is NULL");
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    return UCS_OK;
+}
+
+static ucs_status_t check_args(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
+                               ucg_dev_dtype_t dt, const char *what)
+{
+    if (ctx == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, what, "ctx is NULL");
+    }
+    if (!ucg_builtin_dev_is_supported(dt, op)) {
+        return set_error(UCS_ERR_UNSUPPORTED, what,
+                         "dtype/op pair not defined (MPI: logical/bitwise ops "
+                         "need an integer type)");
+    }
+    return UCS_OK;
+}
+
+static ucs_status_t reduce_on(ucg_builtin_dev_ctx_t *ctx, hipStream_t st,
+                              ucg_dev_op_t op, ucg_dev_dtype_t dt, void *dst,
+                              const void *src, size_t count)
+{
+    if (count == 0) {
+        return UCS_OK;
+    }
+    if (((uintptr_t)dst | (uintptr_t)src) % kDtSize[dt]) {
+        return set_error(UCS_ERR_INVALID_PARAM, "reduce",
+                         "operands are not element-aligned");
+    }
+    const char *d = (const char*)dst, *s = (const char*)src;
+    const size_t bytes = count * kDtSize[dt];
+    if (d != s && d < s + bytes && s < d + bytes) {
+        return set_error(UCS_ERR_INVALID_PARAM, "reduce",
+                         "src and dst partially overlap");
+    }
+    HIP_TRY(g_reduce[dt][op](dst, src, count, st, launch_cfg().variant));
+    ctx->counters[0]++;
+    ctx->counters[1] += 3 * bytes;
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_reduce(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
+                                    ucg_dev_dtype_t dt, void *dst,
+                                    const void *src, size_t count)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "reduce");
+    if (st != UCS_OK) {
+        return st;
+    }
+    if (count && (dst == nullptr || src == nullptr)) {
+        return set_error(UCS_ERR_INVALID_PARAM, "reduce", "NULL buffer");
+    }
+    return reduce_on(ctx, ctx->stream, op, dt, dst, src, count);
+}
+
+ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
+                                          ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                          void *dst, const void *const *srcs,
+                                          unsigned nsrc, unsigned self,
+                                          size_t count)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "reduce_multi");
+    if (st != UCS_OK) {
+        return st;
+    }
+    if (nsrc == 0 || nsrc > (unsigned)kMaxMulti || (nsrc & (nsrc - 1)) ||
+        self >= nsrc || srcs == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "reduce_multi",
+                         "nsrc must be a power of two <= 16 and self < nsrc");
+    }
+    if (count == 0) {
+        return UCS_OK;
+    }
+    SrcList list;
+    for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
+        list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
+        if (i < nsrc && (srcs[i] == nullptr ||
+                         ((uintptr_t)srcs[i] % kDtSize[dt]))) {
+            return set_error(UCS_ERR_INVALID_PARAM, "reduce_multi",
+                             "NULL or misaligned source");
+        }
+    }
+    HIP_TRY(g_multi[dt][op](dst, list, nsrc, self, count, ctx->stream));
+    ctx->counters[0]++;
+    ctx->counters[1] += (uint64_t)(nsrc + 1) * count * kDtSize[dt];
+    return UCS_OK;
+}
+
+/* ---- host-resident whole-buffer combine (pipelined) --------------------- */
+ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
+                                          ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                          void *dst_host, const void *src_host,
+                                          size_t count)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "combine_host");
+    if (st != UCS_OK || count == 0) {
+        return st;
+    }
+    std::lock_guard<std::mutex> g(ctx->lock);
+    if ((st = set_device(ctx)) != UCS_OK || (st = ring_init(ctx)) != UCS_OK) {
+        return st;
+    }
+    const size_t sz    = kDtSize[dt];
+    const size_t chunk = (ctx->slot_bytes / sz) * sz;
+    const size_t bytes = count * sz;
+    for (size_t off = 0; off < bytes; off += chunk) {
+        const size_t n = (bytes - off < chunk) ? bytes - off : chunk;
+        unsigned k;
+        if ((st = slot_acquire(ctx, &k)) != UCS_OK) {
+            return st;
+        }
+        char *ds = ctx->d_ring + (size_t)k * ctx->slot_bytes;
+        char *dd = ctx->d_ring2 + (size_t)k * ctx->slot_bytes;
+        HIP_TRY(hipMemcpyAsync(ds, (const char*)src_host + off, n,
+                               hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(dd, (const char*)dst_host + off, n,
+                               hipMemcpyHostToDevice, ctx->stream));
+        if ((st = reduce_on(ctx, ctx->stream, op, dt, dd, ds, n / sz)) != UCS_OK) {
+            return st;
+        }
+        HIP_TRY(hipEventRecord(ctx->slot_ev[k], ctx->stream));
+        HIP_TRY(hipStreamWaitEvent(ctx->stream_d2h, ctx->slot_ev[k], 0));
+        HIP_TRY(hipMemcpyAsync((char*)dst_host + off, dd, n,
+                               hipMemcpyDeviceToHost, ctx->stream_d2h));
+        HIP_TRY(hipEventRecord(ctx->slot_ev[k], ctx->stream_d2h));
+        ctx->counters[2] += 2 * n;
+        ctx->counters[3] += n;
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    for (unsigned i = 0; i < ctx->nslots; i++) {
+        ctx->slot_used[i] = false;
+    }
+    return UCS_OK;
+}
+
+/* ---- per-step staging with fragment aggregation ------------------------- */
+static ucs_status_t run_flush(ucg_builtin_dev_ctx_t *ctx,
+                              ucg_builtin_dev_ctx::Run &r)
+{
+    if (!r.active) {
+        return UCS_OK;
+    }
+    r.active = false;
+    const size_t sz = kDtSize[r.dt];
+    char *ds = ctx->d_ring + (size_t)r.slot * ctx->slot_bytes;
+    HIP_TRY(hipMemcpyAsync(ds, ctx->h_ring + (size_t)r.slot * ctx->slot_bytes,
+                           r.used, hipMemcpyHostToDevice, ctx->stream));
+    ucs_status_t st = reduce_on(ctx, ctx->stream, (ucg_dev_op_t)r.op,
+                                (ucg_dev_dtype_t)r.dt, ctx->d_acc + r.off, ds,
+                                r.used / sz);
+    if (st != UCS_OK) {
+        return st;
+    }
+    HIP_TRY(hipEventRecord(ctx->slot_ev[r.slot], ctx->stream));
+    ctx->counters[2] += r.used;
+    return UCS_OK;
+}
+
+/* flush every pending run, oldest first: the device then applies each
+ * element's contributions in the order the fragments arrived */
+static ucs_status_t runs_flush_all(ucg_builtin_dev_ctx_t *ctx)
+{
+    for (;;) {
+        ucg_builtin_dev_ctx::Run *oldest = nullptr;
+        for (auto &r : ctx->runs) {
+            if (r.active && (oldest == nullptr || r.seq < oldest->seq)) {
+                oldest = &r;
+            }
+        }
+        if (oldest == nullptr) {
+            return UCS_OK;
+        }
+        ucs_status_t st = run_flush(ctx, *oldest);
+        if (st != UCS_OK) {
+            return st;
+        }
+    }
+}
+
+static bool overlaps(const ucg_builtin_dev_ctx::Run &r, size_t lo, size_t hi)
+{
+    return r.active && r.off < hi && lo < r.off + r.used;
+}
+
+ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
+                                         void *host_dst, size_t bytes)
+{
+    if (ctx == nullptr || (bytes && host_dst == nullptr)) {
+        return set_error(UCS_ERR_INVALID_PARAM, "stage_begin", "bad arguments");
+    }
+    std::lock_guard<std::mutex> g(ctx->lock);
+    ucs_status_t st;
+    if ((st = set_device(ctx)) != UCS_OK || (st = ring_init(ctx)) != UCS_OK ||
+        (st = runs_flush_all(ctx)) != UCS_OK) {
+        return st;
+    }
+    if (bytes > ctx->d_acc_cap) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        if (ctx->d_acc) {
+            HIP_TRY(hipFree(ctx->d_acc));
+            ctx->d_acc = nullptr;
+        }
+        HIP_TRY(hipMalloc((void**)&ctx->d_acc, bytes));
+        ctx->d_acc_cap = bytes;
+    }
+    ctx->host_dst  = host_dst;
+    ctx->stage_len = bytes;
+    if (bytes) {
+        HIP_TRY(hipMemcpyAsync(ctx->d_acc, host_dst, bytes,
+                               hipMemcpyHostToDevice, ctx->stream));
+        ctx->counters[2] += bytes;
+    }
+    return UCS_OK;
+}
+
+/*
+ * Fragment combine (ucg_builtin_mpi_reduce_fragment's replacement). The
+ * borrowed src is copied into a pinned ring slot at once; fragments that
+ * continue a pending run are appended to it so that one H2D copy and one
+ * kernel serve many AM-sized fragments. Interleaved senders (a fan-in step
+ * with ep_cnt > 1) each grow their own run. A run may only grow over a range
+ * that no later-started run already holds, so flushing runs oldest-first
+ * reproduces the per-element arrival order exactly (bit-exact fp results).
+ */
+ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
+                                     ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                     size_t dst_offset, const void *host_src,
+                                     size_t count)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "combine");
+    if (st != UCS_OK) {
+        return st;
+    }
+    std::lock_guard<std::mutex> g(ctx->lock);
+    const size_t sz = kDtSize[dt];
+    size_t bytes    = count * sz;
+    if (ctx->host_dst == nullptr || dst_offset + bytes > ctx->stage_len ||
+        dst_offset % sz) {
+        return set_error(UCS_ERR_OUT_OF_RANGE, "combine",
+                         "fragment outside the staged step buffer");
+    }
+    const char *src  = static_cast<const char*>(host_src);
+    const size_t cap = (ctx->slot_bytes / sz) * sz;
+    while (bytes > 0) {
+        ucg_builtin_dev_ctx::Run *run = nullptr;
+        for (auto &r : ctx->runs) {
+            if (r.active && r.op == (int)op && r.dt == (int)dt &&
+                r.off + r.used == dst_offset && r.used < cap) {
+                run = &r;
+                break;
+            }
+        }
+        const size_t lo = dst_offset;
+        const size_t hi = dst_offset + (run ? std::min(bytes, cap - run->used) :
+                                              std::min(bytes, cap));
+        /* growing a run over a range that a LATER run already holds would
+         * flush this contribution before an earlier-arrived one; a brand-new
+         * run is always flushed last, so it never clashes */
+        bool clash = false;
+        for (auto &r : ctx->runs) {
+            if (run != nullptr && &r != run && overlaps(r, lo, hi) &&
+                r.seq > run->seq) {
+                clash = true;
+            }
+        }
+        if (run == nullptr || clash) {
+            unsigned nact = 0;
+            for (auto &r : ctx->runs) {
+                nact += r.active;
+            }
+            if (clash || nact >= ctx->max_runs) {
+                if ((st = runs_flush_all(ctx)) != UCS_OK) {
+                    return st;
+                }
+            }
+            for (auto &r : ctx->runs) {
+                if (!r.active) {
+                    run = &r;
+                    break;
+                }
+            }
+            unsigned k;
+            if ((st = slot_acquire(ctx, &k)) != UCS_OK) {
+                return st;
+            }
+            run->active = true;
+            run->slot   = k;
+            run->used   = 0;
+            run->off    = dst_offset;
+            run->op     = op;
+            run->dt     = dt;
+            run->seq    = ctx->run_seq++;
+        }
+        const size_t room = cap - run->used;
+        const size_t n    = bytes < room ? bytes : room;
+        /* src is borrowed (released right after the callback returns,
+         * builtin/ops/builtin_comp_step.inl:443-449): copy it now */
+        memcpy(ctx->h_ring + (size_t)run->slot * ctx->slot_bytes + run->used,
+               src, n);
+        run->used  += n;
+        src        += n;
+        dst_offset += n;
+        bytes      -= n;
+        if (run->used == cap) {
+            /* a full run can only be flushed if nothing older is pending */
+            bool older = false;
+            for (auto &r : ctx->runs) {
+                older |= (r.active && r.seq < run->seq);
+            }
+            st = older ? runs_flush_all(ctx) : run_flush(ctx, *run);
+            if (st != UCS_OK) {
+                return st;
+            }
+        }
+    }
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
+{
+    if (ctx == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "stage_end", "ctx is NULL");
+    }
+    std::lock_guard<std::mutex> g(ctx->lock);
+    ucs_status_t st = runs_flush_all(ctx);
+    if (st != UCS_OK) {
+        return st;
+    }
+    if (ctx->host_dst && ctx->stage_len) {
+        HIP_TRY(hipMemcpyAsync(ctx->host_dst, ctx->d_acc, ctx->stage_len,
+                               hipMemcpyDeviceToHost, ctx->stream));
+        ctx->counters[3] += ctx->stage_len;
+    }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    for (unsigned i = 0; i < ctx->nslots; i++) {
+        ctx->slot_used[i] = false;
+    }
+    ctx->host_dst  = nullptr;
+    ctx->stage_len = 0;
+    return UCS_OK;
+}
+
+/* ---- memory helpers ------------------------------------------------------ */
+void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
+{
+    void *p = nullptr;
+    if (ctx) {
+        (void)hipSetDevice(ctx->device);
+    }
+    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+        hip_status(e, "hipMalloc");
+        return nullptr;
+    }
+    return p;
+}
+
+void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
+{
+    (void)ctx;
+    if (ptr) {
+        (void)hipFree(ptr);
+    }
+}
+
+void *ucg_builtin_dev_host_alloc(size_t bytes)
+{
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        hip_status(e, "hipHostMalloc");
+        return nullptr;
+    }
+    return p;
+}
+
+void ucg_builtin_dev_host_free(void *ptr)
+{
+    if (ptr) {
+        (void)hipHostFree(ptr);
+    }
+}
+
+ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
+                                    const void *src, size_t bytes)
+{
+    if (ctx == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "memcpy", "ctx is NULL");
+    }
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_fill(ucg_builtin_dev_ctx_t *ctx, ucg_dev_dtype_t dt,
+                                  ucg_dev_dist_t dist, uint64_t seed, void *dst,
+                                  size_t count)
+{
+    if (ctx == nullptr || (int)dt < 0 || dt >= UCG_DEV_DT_LAST || (int)dist < 0 ||
+        dist >= UCG_DEV_DIST_LAST || (count && dst == nullptr)) {
+        return set_error(UCS_ERR_INVALID_PARAM, "fill", "bad arguments");
+    }
+    if (count == 0) {
+        return UCS_OK;
+    }
+    /* host-side key derivation, same as ucg_oracle_fill */
+    uint64_t z = seed + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    const uint64_t key = z ^ (z >> 31);
+    g_fill[dt](dst, (int)dist, key, count, ctx->stream);
+    HIP_TRY(hipGetLastError());
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_profile_reduce(ucg_builtin_dev_ctx_t *ctx,
+                                            ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                            void *dst, const void *src,
+                                            size_t count, unsigned iters,
+                                            double *avg_us)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "profile_reduce");
+    if (st != UCS_OK) {
+        return st;
+    }
+    if (iters == 0 || avg_us == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "profile_reduce", "bad arguments");
+    }
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, ctx->stream));
+    for (unsigned i = 0; i < iters && st == UCS_OK; i++) {
+        st = reduce_on(ctx, ctx->stream, op, dt, dst, src, count);
+    }
+    HIP_TRY(hipEventRecord(e1, ctx->stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_us = 1000.0 * ms / iters;
+    return st;
+}
+
+void ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx, uint64_t out[4])
+{
+    for (int i = 0; i < 4; i++) {
+        out[i] = ctx ? ctx->counters[i].load() : 0;
+    }
+}
+
+} /* extern "C" */

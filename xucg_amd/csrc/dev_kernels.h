@@ -1,0 +1,338 @@
+/*
+ * dev_kernels.h - CDNA4 (gfx950) kernels for the UCG combine path.
+ *
+ *   k_reduce        dst = src (op) dst, 16-B non-temporal vector loads of
+ *                   both operands, one tile of U vectors per lane, grid
+ *                   sized to the data; the unaligned head and the ragged
+ *                   tail (< 16 B each) are done by the first lanes of the
+ *                   grid with lane-masked scalar accesses.
+ *   k_reduce_scalar same contract when src and dst disagree mod 16 B.
+ *   k_reduce_multi  one-shot N-operand combine in the recursive-doubling
+ *                   association (builtin/plan/builtin_recursive.c:158-169).
+ *   k_fill          counter-based synthetic generator.
+ *
+ * Element-wise, HBM-bound: 3 x N x sizeof(T) algorithmic bytes per combine,
+ * no reuse, so no LDS staging and no MFMA; the levers are 16-B accesses,
+ * enough bytes in flight per CU and launch geometry.
+ */
+#ifndef UCG_DEV_KERNELS_H_
+#define UCG_DEV_KERNELS_H_
+
+#include "combine_ops.h"
+
+namespace ucgdev {
+
+constexpr int kBlock = 256;           /* 4 waves of 64 lanes */
+constexpr int kMaxMulti = 16;         /* max operands of k_reduce_multi */
+constexpr int kMultiU   = 2;          /* vectors per lane in k_reduce_multi */
+constexpr int kReduceU  = 4;          /* vectors per lane in k_reduce */
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int NT>
+__device__ __forceinline__ u32x4 ld16(const u32x4 *p)
+{
+    if (NT) {
+        return __builtin_nontemporal_load(p);
+    }
+    return *p;
+}
+
+template <int NT>
+__device__ __forceinline__ void st16(u32x4 *p, u32x4 v)
+{
+    if (NT) {
+        __builtin_nontemporal_store(v, p);
+    } else {
+        *p = v;
+    }
+}
+
+/* apply the functor to the 16/sizeof(T) lanes of a 16-B vector */
+template <typename T, int OP>
+__device__ __forceinline__ u32x4 vapply(u32x4 s, u32x4 d)
+{
+    constexpr int V = 16 / sizeof(T);
+    T a[V], b[V];
+    __builtin_memcpy(a, &s, 16);
+    __builtin_memcpy(b, &d, 16);
+#pragma unroll
+    for (int k = 0; k < V; k++) {
+        b[k] = Comb<T, OP>::apply(a[k], b[k]);
+    }
+    u32x4 o;
+    __builtin_memcpy(&o, b, 16);
+    return o;
+}
+
+/*
+ * The streaming combine. One tile of U 16-B vectors per lane (lane stride
+ * kBlock), no loop: the grid is sized to the data, so the hardware dispatcher
+ * streams fresh workgroups onto the CUs and every wave issues its 2U loads
+ * back to back before its first use. Loads and stores carry the non-temporal
+ * hint: nothing is re-read, and measured on MI355X this geometry moved the
+ * 2 x 256 MiB fp32 combine from 56% (grid-stride loop, temporal) to 79% of
+ * 8 TB/s (profiles/). The ragged head (until dst is 16-B aligned)
+ * and tail (< 16 B) are done by the first lanes of the grid.
+ */
+template <typename T, int OP, int U, int NT>
+__global__ void __launch_bounds__(kBlock)
+k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
+{
+    constexpr int V   = 16 / sizeof(T);
+    const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+
+    /* ragged edges: < V elements each, one lane per element */
+    if (gtid < head) {
+        dst[gtid] = Comb<T, OP>::apply(src[gtid], dst[gtid]);
+    }
+    if (gtid < tail) {
+        const size_t j = head + nvec * V + gtid;
+        dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
+    }
+
+    const u32x4 *s4   = reinterpret_cast<const u32x4*>(src + head);
+    u32x4 *d4         = reinterpret_cast<u32x4*>(dst + head);
+    const size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * kBlock;
+        if (i < nvec) {
+            a[u] = ld16<NT>(s4 + i);
+            b[u] = ld16<NT>(d4 + i);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * kBlock;
+        if (i < nvec) {
+            st16<NT>(d4 + i, vapply<T, OP>(a[u], b[u]));
+        }
+    }
+}
+
+template <typename T, int OP>
+__global__ void __launch_bounds__(kBlock)
+k_reduce_scalar(T *dst, const T *src, size_t count)
+{
+    constexpr int U   = 4;
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+    size_t i          = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    for (; i + (U - 1) * nthr < count; i += U * nthr) {
+        T a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            a[u] = src[i + u * nthr];
+            b[u] = dst[i + u * nthr];
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            dst[i + u * nthr] = Comb<T, OP>::apply(a[u], b[u]);
+        }
+    }
+    for (; i < count; i += nthr) {
+        dst[i] = Comb<T, OP>::apply(src[i], dst[i]);
+    }
+}
+
+/* ---- recursive-doubling association ------------------------------------ */
+struct SrcList {
+    const void *p[kMaxMulti];
+};
+
+/* val[m] holds member (self ^ m). Level j (h = 2^(j-1)) computes, for every m
+ * with its low j bits clear, V(self^m, j) = V(self^m^h, j-1) (op) V(self^m,
+ * j-1): the incoming (src) operand is the partner's accumulator. */
+template <int N, typename E, typename F>
+__device__ __forceinline__ E rd_tree(E (&val)[N], F f)
+{
+#pragma unroll
+    for (int h = 1; h < N; h <<= 1) {
+#pragma unroll
+        for (int m = 0; m < N; m += 2 * h) {
+            val[m] = f(val[m + h], val[m]);
+        }
+    }
+    return val[0];
+}
+
+template <typename T, int OP, int N>
+__global__ void __launch_bounds__(kBlock)
+k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
+               size_t tail)
+{
+    constexpr int V    = 16 / sizeof(T);
+    const size_t gtid  = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<T, OP>(a, b); };
+
+    if (gtid < head || gtid < tail) {
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            size_t j;
+            if (part == 0) {
+                if (gtid >= head) continue;
+                j = gtid;
+            } else {
+                if (gtid >= tail) continue;
+                j = head + nvec * V + gtid;
+            }
+            T val[N];
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                val[m] = static_cast<const T*>(srcs.p[self ^ m])[j];
+            }
+            dst[j] = rd_tree<N>(val, fs);
+        }
+    }
+
+    u32x4 *d4 = reinterpret_cast<u32x4*>(dst + head);
+    const size_t base = (size_t)blockIdx.x * (kBlock * kMultiU) + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kMultiU; u++) {
+        const size_t i = base + (size_t)u * kBlock;
+        if (i < nvec) {
+            u32x4 val[N];
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                val[m] = ld16<1>(reinterpret_cast<const u32x4*>(
+                             static_cast<const T*>(srcs.p[self ^ m]) + head) + i);
+            }
+            st16<1>(d4 + i, rd_tree<N>(val, fv));
+        }
+    }
+}
+
+template <typename T, int OP, int N>
+__global__ void __launch_bounds__(kBlock)
+k_reduce_multi_scalar(T *dst, SrcList srcs, unsigned self, size_t count)
+{
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+    auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < count;
+         i += nthr) {
+        T val[N];
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            val[m] = static_cast<const T*>(srcs.p[self ^ m])[i];
+        }
+        dst[i] = rd_tree<N>(val, fs);
+    }
+}
+
+/* ---- synthetic generator (== ucg_oracle_fill) --------------------------- */
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x)
+{
+    uint64_t z = x + 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__constant__ uint32_t c_spec_f32[22] = {
+    0x00000000, 0x80000000, 0x3f800000, 0xbf800000, 0x3fc00000, 0x00000001,
+    0x007fffff, 0x00800000, 0x7f7fffff, 0xff7fffff, 0x7f800000, 0xff800000,
+    0x7fc00000, 0x7fc12345, 0xffc54321, 0x7f800001, 0xff812345, 0x4b800000,
+    0x33800000, 0x3dcccccd, 0x80000001, 0x40400000};
+__constant__ uint64_t c_spec_f64[22] = {
+    0x0000000000000000ull, 0x8000000000000000ull, 0x3ff0000000000000ull,
+    0xbff0000000000000ull, 0x3ff8000000000000ull, 0x0000000000000001ull,
+    0x000fffffffffffffull, 0x0010000000000000ull, 0x7fefffffffffffffull,
+    0xffefffffffffffffull, 0x7ff0000000000000ull, 0xfff0000000000000ull,
+    0x7ff8000000000000ull, 0x7ff8000000012345ull, 0xfff8000000054321ull,
+    0x7ff0000000000001ull, 0xfff0000000012345ull, 0x4340000000000000ull,
+    0x3ca0000000000000ull, 0x3fb999999999999aull, 0x8000000000000001ull,
+    0x4008000000000000ull};
+__constant__ uint16_t c_spec_f16[22] = {
+    0x0000, 0x8000, 0x3c00, 0xbc00, 0x3e00, 0x0001, 0x03ff, 0x0400, 0x7bff,
+    0xfbff, 0x7c00, 0xfc00, 0x7e00, 0x7e45, 0xfe21, 0x7c01, 0xfc23, 0x6800,
+    0x1000, 0x2e66, 0x8001, 0x4200};
+__constant__ uint16_t c_spec_bf16[22] = {
+    0x0000, 0x8000, 0x3f80, 0xbf80, 0x3fc0, 0x0001, 0x007f, 0x0080, 0x7f7f,
+    0xff7f, 0x7f80, 0xff80, 0x7fc0, 0x7fc5, 0xffc3, 0x7f81, 0xff85, 0x4380,
+    0x3b80, 0x3dcd, 0x8001, 0x4040};
+
+__device__ __forceinline__ uint64_t spec_int(unsigned bits, unsigned idx)
+{
+    const uint64_t m  = (bits == 64) ? ~0ull : ((1ull << bits) - 1);
+    const uint64_t mx = m >> 1;
+    switch (idx) {
+    case 0:  return 0;
+    case 1:  return 1;
+    case 2:  return m;
+    case 3:  return 2;
+    case 4:  return mx;
+    case 5:  return mx + 1;
+    case 6:  return mx - 1;
+    case 7:  return mx + 2;
+    case 8:  return 0x5555555555555555ull & m;
+    case 9:  return 0xaaaaaaaaaaaaaaaaull & m;
+    case 10: return 3;
+    case 11: return m - 6;
+    case 12: return 0x0f0f0f0f0f0f0f0full & m;
+    case 13: return 0xf0f0f0f0f0f0f0f0ull & m;
+    case 14: return 0x100 & m;
+    default: return m - 0xff;
+    }
+}
+
+template <int DT>
+__device__ __forceinline__ uint64_t gen_bits(int dist, uint64_t h)
+{
+    const uint64_t sign = h >> 63;
+    if (dist == UCG_DEV_DIST_SPECIAL) {
+        if (DT == UCG_DEV_DT_FLOAT32)  return c_spec_f32[h % 22];
+        if (DT == UCG_DEV_DT_FLOAT64)  return c_spec_f64[h % 22];
+        if (DT == UCG_DEV_DT_FLOAT16)  return c_spec_f16[h % 22];
+        if (DT == UCG_DEV_DT_BFLOAT16) return c_spec_bf16[h % 22];
+        return spec_int(8 * sizeof(typename DtType<DT>::T), (unsigned)(h % 16));
+    }
+    if (dist == UCG_DEV_DIST_EXACT) {
+        const int64_t v = (int64_t)(h % 2049u) - 1024;
+        if (DT == UCG_DEV_DT_FLOAT16)  return f2h_rne((float)v);
+        if (DT == UCG_DEV_DT_BFLOAT16) return f2b_rne((float)v);
+        if (DT == UCG_DEV_DT_FLOAT32)  return __float_as_uint((float)v);
+        if (DT == UCG_DEV_DT_FLOAT64)  return (uint64_t)__double_as_longlong((double)v);
+        return (uint64_t)v;
+    }
+    if (DT == UCG_DEV_DT_FLOAT16) {
+        const uint64_t e = ((h >> 10) & 0xff) % 17;
+        return (sign << 15) | ((e + 7) << 10) | (h & 0x3ff);
+    }
+    if (DT == UCG_DEV_DT_BFLOAT16) {
+        const uint64_t e = ((h >> 7) & 0xff) % 17;
+        return (sign << 15) | ((e + 119) << 7) | (h & 0x7f);
+    }
+    if (DT == UCG_DEV_DT_FLOAT32) {
+        const uint64_t e = ((h >> 23) & 0xff) % 17;
+        return (sign << 31) | ((e + 119) << 23) | (h & 0x7fffff);
+    }
+    if (DT == UCG_DEV_DT_FLOAT64) {
+        const uint64_t e = ((h >> 52) & 0x7ff) % 17;
+        return (sign << 63) | ((e + 1015) << 52) | (h & 0xfffffffffffffull);
+    }
+    return h;
+}
+
+template <int DT>
+__global__ void __launch_bounds__(kBlock)
+k_fill(void *dst, int dist, uint64_t key, size_t count)
+{
+    typedef typename DtType<DT>::T T;
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < count;
+         i += nthr) {
+        const uint64_t b = gen_bits<DT>(dist, splitmix64(key ^ (uint64_t)i));
+        switch (sizeof(T)) {
+        case 1:  static_cast<uint8_t*>(dst)[i]  = (uint8_t)b;  break;
+        case 2:  static_cast<uint16_t*>(dst)[i] = (uint16_t)b; break;
+        case 4:  static_cast<uint32_t*>(dst)[i] = (uint32_t)b; break;
+        default: static_cast<uint64_t*>(dst)[i] = b;           break;
+        }
+    }
+}
+
+} /* namespace ucgdev */
+
+#endif

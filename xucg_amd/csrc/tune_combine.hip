@@ -1,0 +1,357 @@
+/*
+ * tune_combine.hip - standalone A/B harness for the fp32 SUM combine kernel
+ * geometry on MI355X (not part of the product libraries).
+ *
+ *   hipcc -O3 --offload-arch=gfx950 -I../../include tune_combine.hip -o tune
+ *   ./tune [count_log2=26] [rounds=5]
+ *
+ * Every variant runs on the same buffers, interleaved over `rounds` rounds
+ * (cdna_hip_programming.md rule 24); prints min/median us and GB/s on the
+ * 3N-byte algorithmic basis. Results are checked against the baseline
+ * variant's output bit for bit.
+ */
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "dev_kernels.h"
+
+using namespace ucgdev;
+
+#define CHECK(x)                                                               \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess) {                                                \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,          \
+                    hipGetErrorString(e_));                                    \
+            exit(1);                                                           \
+        }                                                                      \
+    } while (0)
+
+/* variant A: grid-stride loop, U vectors per lane per iteration (the first
+ * product kernel, kept here as the A/B reference) */
+template <int U, int NT>
+__global__ void __launch_bounds__(256)
+k_gridstride(float *dst, const float *src, size_t nvec)
+{
+    const size_t nthr = (size_t)gridDim.x * 256;
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (size_t)(U - 1) * nthr < nvec; i += (size_t)U * nthr) {
+        u32x4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            a[u] = ld16<NT>(s4 + i + u * nthr);
+            b[u] = ld16<NT>(d4 + i + u * nthr);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            st16<NT>(d4 + i + u * nthr, vapply<float, 0>(a[u], b[u]));
+        }
+    }
+    for (; i < nvec; i += nthr) {
+        st16<NT>(d4 + i, vapply<float, 0>(ld16<NT>(s4 + i), ld16<NT>(d4 + i)));
+    }
+}
+
+/* variant E: oneshot with separate temporal choice for loads and stores,
+ * optional XCD-contiguous block remap */
+template <int U, int NTL, int NTS, int XCD>
+__global__ void __launch_bounds__(256)
+k_oneshot2(float *dst, const float *src, size_t nvec)
+{
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    size_t blk = blockIdx.x;
+    if (XCD) {
+        const size_t nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = blk % 8;
+        blk = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + blk / 8;
+    }
+    const size_t base = blk * 256 * U + threadIdx.x;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + u * 256;
+        if (i < nvec) {
+            a[u] = ld16<NTL>(s4 + i);
+            b[u] = ld16<NTL>(d4 + i);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + u * 256;
+        if (i < nvec) {
+            st16<NTS>(d4 + i, vapply<float, 0>(a[u], b[u]));
+        }
+    }
+}
+
+/* variant B: each block owns one contiguous chunk of vectors */
+template <int U, int NT, int BS>
+__global__ void __launch_bounds__(BS)
+k_chunked(float *dst, const float *src, size_t nvec, size_t per_block)
+{
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    size_t beg = (size_t)blockIdx.x * per_block;
+    size_t end = beg + per_block < nvec ? beg + per_block : nvec;
+    size_t i   = beg + threadIdx.x;
+    for (; i + (U - 1) * BS < end; i += U * BS) {
+        u32x4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            a[u] = ld16<NT>(s4 + i + u * BS);
+            b[u] = ld16<NT>(d4 + i + u * BS);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            st16<NT>(d4 + i + u * BS, vapply<float, 0>(a[u], b[u]));
+        }
+    }
+    for (; i < end; i += BS) {
+        st16<NT>(d4 + i, vapply<float, 0>(ld16<NT>(s4 + i), ld16<NT>(d4 + i)));
+    }
+}
+
+/* variant C: no loop, one tile of U vectors per thread, huge grid */
+template <int U, int NT, int BS>
+__global__ void __launch_bounds__(BS)
+k_oneshot(float *dst, const float *src, size_t nvec)
+{
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + u * BS;
+        if (i < nvec) {
+            a[u] = ld16<NT>(s4 + i);
+            b[u] = ld16<NT>(d4 + i);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + u * BS;
+        if (i < nvec) {
+            st16<NT>(d4 + i, vapply<float, 0>(a[u], b[u]));
+        }
+    }
+}
+
+/* variant D: loads of both operands with sc0/sc1/nt bits via the buffer
+ * intrinsic (aux), product loop structure */
+template <int U, int AUXL, int AUXS, int BS>
+__global__ void __launch_bounds__(BS)
+k_buffer(float *dst, const float *src, size_t nvec)
+{
+    /* nvec * 16 <= 2^32 assumed by the harness sizes */
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, 0, (int)0xFFFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)dst, 0, (int)0xFFFFFFFF, 0x00020000);
+    const size_t nthr = (size_t)gridDim.x * BS;
+    size_t i = (size_t)blockIdx.x * BS + threadIdx.x;
+    for (; i + (U - 1) * nthr < nvec; i += U * nthr) {
+        u32x4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const unsigned off = (unsigned)((i + u * nthr) * 16);
+            a[u] = __builtin_bit_cast(u32x4,
+                       __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUXL));
+            b[u] = __builtin_bit_cast(u32x4,
+                       __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, AUXL));
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const unsigned off = (unsigned)((i + u * nthr) * 16);
+            __builtin_amdgcn_raw_buffer_store_b128(
+                __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int,
+                                   vapply<float, 0>(a[u], b[u])),
+                rd, off, 0, AUXS);
+        }
+    }
+    for (; i < nvec; i += nthr) {
+        const unsigned off = (unsigned)(i * 16);
+        u32x4 a = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, AUXL));
+        u32x4 b = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, off, 0, AUXL));
+        __builtin_amdgcn_raw_buffer_store_b128(vapply<float, 0>(a, b), rd, off, 0, AUXS);
+    }
+}
+
+struct Variant {
+    std::string name;
+    std::function<void(float*, const float*, size_t, hipStream_t)> run;
+    std::vector<float> us;
+};
+
+int main(int argc, char **argv)
+{
+    const int lg     = argc > 1 ? atoi(argv[1]) : 26;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+    const int iters  = 20;
+    const size_t n = (size_t)1 << lg, nvec = n / 4;
+    float *src, *dst, *ref;
+    CHECK(hipMalloc(&src, n * 4));
+    CHECK(hipMalloc(&dst, n * 4));
+    CHECK(hipMalloc(&ref, n * 4));
+    hipStream_t st;
+    CHECK(hipStreamCreate(&st));
+
+    std::vector<Variant> vs;
+    /* product kernel first: everything is checked against its output */
+    vs.push_back({"product k_reduce<f32,SUM,4,NT1>", [=](float *d, const float *s, size_t nv, hipStream_t q) {
+        unsigned g = (unsigned)((nv + 1023) / 1024);
+        hipLaunchKernelGGL((k_reduce<float, 0, 4, 1>), dim3(g), dim3(256), 0, q, d, s, (size_t)0, nv, (size_t)0);
+    }, {}});
+    auto grid_stride = [&](int U, int NT, int maxb) {
+        char buf[128];
+        snprintf(buf, sizeof(buf), "gridstride U%d NT%d blocks%d", U, NT, maxb);
+        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)std::min<size_t>((nv + 256 * U - 1) / (256 * U), maxb);
+            if (U == 4 && NT == 0) hipLaunchKernelGGL((k_gridstride<4, 0>), dim3(g), dim3(256), 0, q, d, s, nv);
+            if (U == 2 && NT == 1) hipLaunchKernelGGL((k_gridstride<2, 1>), dim3(g), dim3(256), 0, q, d, s, nv);
+        }, {}});
+    };
+    grid_stride(4, 0, 2048);
+    grid_stride(2, 1, 4096);
+    auto oneshot2 = [&](int U, int NTL, int NTS, int XCD) {
+        char buf[128];
+        snprintf(buf, sizeof(buf), "oneshot2 U%d NTL%d NTS%d XCD%d", U, NTL, NTS, XCD);
+        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)((nv + 256 * U - 1) / (256 * U));
+#define O2(A, B, C, D) if (U == A && NTL == B && NTS == C && XCD == D) hipLaunchKernelGGL((k_oneshot2<A, B, C, D>), dim3(g), dim3(256), 0, q, d, s, nv)
+            O2(4, 1, 1, 0); O2(4, 1, 0, 0); O2(4, 0, 1, 0); O2(4, 1, 1, 1);
+            O2(2, 1, 1, 0); O2(1, 1, 1, 0); O2(3, 1, 1, 0); O2(6, 1, 1, 0);
+            O2(2, 1, 1, 1);
+#undef O2
+        }, {}});
+    };
+    oneshot2(4, 1, 1, 0);
+    oneshot2(4, 1, 0, 0);
+    oneshot2(4, 0, 1, 0);
+    oneshot2(4, 1, 1, 1);
+    oneshot2(2, 1, 1, 0);
+    oneshot2(2, 1, 1, 1);
+    oneshot2(1, 1, 1, 0);
+    oneshot2(3, 1, 1, 0);
+    oneshot2(6, 1, 1, 0);
+
+    auto chunked = [&](int U, int NT, int blocks) {
+        char buf[128];
+        snprintf(buf, sizeof(buf), "chunked U%d NT%d blocks%d", U, NT, blocks);
+        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+            size_t per = (nv + blocks - 1) / blocks;
+            per = (per + 255) / 256 * 256;
+            unsigned g = (unsigned)((nv + per - 1) / per);
+#define CK(UU, NN) hipLaunchKernelGGL((k_chunked<UU, NN, 256>), dim3(g), dim3(256), 0, q, d, s, nv, per)
+            if (U == 4 && NT == 0) CK(4, 0);
+            if (U == 8 && NT == 0) CK(8, 0);
+            if (U == 4 && NT == 1) CK(4, 1);
+#undef CK
+        }, {}});
+    };
+    chunked(4, 0, 2048);
+    chunked(4, 0, 1024);
+    chunked(8, 0, 1024);
+    chunked(4, 1, 2048);
+
+    auto oneshot = [&](int U, int NT, int BS) {
+        char buf[128];
+        snprintf(buf, sizeof(buf), "oneshot U%d NT%d bs%d", U, NT, BS);
+        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)((nv + (size_t)BS * U - 1) / ((size_t)BS * U));
+#define OS(UU, NN, BB) hipLaunchKernelGGL((k_oneshot<UU, NN, BB>), dim3(g), dim3(BB), 0, q, d, s, nv)
+            if (U == 4 && NT == 0 && BS == 256) OS(4, 0, 256);
+            if (U == 2 && NT == 0 && BS == 256) OS(2, 0, 256);
+            if (U == 8 && NT == 0 && BS == 256) OS(8, 0, 256);
+            if (U == 4 && NT == 1 && BS == 256) OS(4, 1, 256);
+            if (U == 4 && NT == 0 && BS == 512) OS(4, 0, 512);
+            if (U == 2 && NT == 0 && BS == 1024) OS(2, 0, 1024);
+#undef OS
+        }, {}});
+    };
+    oneshot(4, 0, 256);
+    oneshot(2, 0, 256);
+    oneshot(8, 0, 256);
+    oneshot(4, 1, 256);
+    oneshot(4, 0, 512);
+    oneshot(2, 0, 1024);
+
+    if (nvec * 16 <= 0xFFFFFFFFull) {
+        auto buffer = [&](const char *nm, int aux_l, int aux_s, int maxb) {
+            char buf[128];
+            snprintf(buf, sizeof(buf), "buffer %s blocks%d", nm, maxb);
+            vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+                unsigned g = (unsigned)std::min<size_t>((nv + 1023) / 1024, maxb);
+#define BF(L, S) hipLaunchKernelGGL((k_buffer<4, L, S, 256>), dim3(g), dim3(256), 0, q, d, s, nv)
+                if (aux_l == 0 && aux_s == 0) BF(0, 0);
+                if (aux_l == 2 && aux_s == 2) BF(2, 2);
+                if (aux_l == 0 && aux_s == 2) BF(0, 2);
+                if (aux_l == 2 && aux_s == 0) BF(2, 0);
+#undef BF
+            }, {}});
+        };
+        buffer("plain", 0, 0, 2048);
+        buffer("nt-both", 2, 2, 2048);
+        buffer("nt-store", 0, 2, 2048);
+        buffer("nt-load", 2, 0, 2048);
+    }
+
+    /* init */
+    hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, st,
+                       (void*)src, 0, 1ull, n);
+    hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, st,
+                       (void*)ref, 0, 2ull, n);
+    CHECK(hipStreamSynchronize(st));
+
+    /* correctness: each variant once from the same start vs variant 0 */
+    std::vector<uint32_t> want(n), got(n);
+    for (size_t v = 0; v < vs.size(); v++) {
+        CHECK(hipMemcpy(dst, ref, n * 4, hipMemcpyDeviceToDevice));
+        vs[v].run(dst, src, nvec, st);
+        CHECK(hipGetLastError());
+        CHECK(hipStreamSynchronize(st));
+        CHECK(hipMemcpy(v == 0 ? want.data() : got.data(), dst, n * 4,
+                        hipMemcpyDeviceToHost));
+        if (v && memcmp(want.data(), got.data(), n * 4)) {
+            printf("MISMATCH %s\n", vs[v].name.c_str());
+        }
+    }
+
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    for (int r = 0; r < rounds; r++) {
+        for (auto &v : vs) {
+            v.run(dst, src, nvec, st);  /* warm */
+            CHECK(hipEventRecord(e0, st));
+            for (int i = 0; i < iters; i++) {
+                v.run(dst, src, nvec, st);
+            }
+            CHECK(hipEventRecord(e1, st));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            v.us.push_back(1000.f * ms / iters);
+        }
+    }
+    const double bytes = 3.0 * n * 4;
+    printf("n=2^%d (%.0f MiB per operand), %d rounds x %d iters\n", lg,
+           n * 4 / 1048576.0, rounds, iters);
+    for (auto &v : vs) {
+        std::sort(v.us.begin(), v.us.end());
+        double med = v.us[v.us.size() / 2], mn = v.us[0];
+        printf("%-36s min %8.1f us  med %8.1f us  %7.0f GB/s (%.1f%% of 8 TB/s)\n",
+               v.name.c_str(), mn, med, bytes / (med * 1e-6) / 1e9,
+               100.0 * bytes / (med * 1e-6) / 8e12);
+    }
+    return 0;
+}

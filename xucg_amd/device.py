@@ -1,0 +1,202 @@
+"""Python handle over the C-ABI device combine (include/ucg_builtin_dev.h).
+
+`DevContext` is the per-group device context of UCG's builtin planner
+(`struct ucg_builtin_group_ctx`, reference builtin/builtin.c:66-90). Its
+methods map one-to-one onto the C entry points; buffers are passed as raw
+device pointers (ints), `DevBuffer` objects, or torch tensors (`data_ptr()`).
+Torch is not required by this module.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, dt_index, op_index, dist_index, DTYPE_SIZE
+
+NP_STORAGE = {"int8": np.int8, "uint8": np.uint8, "int16": np.int16,
+              "uint16": np.uint16, "int32": np.int32, "uint32": np.uint32,
+              "int64": np.int64, "uint64": np.uint64, "float16": np.float16,
+              "bfloat16": np.uint16, "float32": np.float32,
+              "float64": np.float64}
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if isinstance(x, (DevBuffer, HostBuffer)):
+        return x.ptr
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if isinstance(x, np.ndarray):
+        return x.ctypes.data
+    raise TypeError(f"cannot take a device pointer of {type(x)}")
+
+
+def dtype_size(dt):
+    return DTYPE_SIZE[dt_index(dt)]
+
+
+def is_supported(dt, op):
+    return bool(_lib.dev().ucg_builtin_dev_is_supported(dt_index(dt), op_index(op)))
+
+
+def device_count():
+    return _lib.dev().ucg_builtin_dev_device_count()
+
+
+class DevBuffer:
+    """A hipMalloc'ed buffer owned by a DevContext."""
+
+    def __init__(self, ctx, nbytes):
+        self.ctx = ctx
+        self.nbytes = nbytes
+        self.ptr = _lib.dev().ucg_builtin_dev_malloc(ctx.handle, nbytes)
+        if not self.ptr:
+            raise MemoryError(f"hipMalloc({nbytes}) failed: {_lib.last_error()}")
+
+    def offset(self, nbytes):
+        return self.ptr + nbytes
+
+    def upload(self, arr, offset=0):
+        arr = np.ascontiguousarray(arr)
+        assert offset + arr.nbytes <= self.nbytes
+        check(_lib.dev().ucg_builtin_dev_memcpy(self.ctx.handle, self.ptr + offset,
+                                                arr.ctypes.data, arr.nbytes), "memcpy H2D")
+
+    def download(self, dtype, count, offset=0):
+        out = np.empty(count, dtype=dtype)
+        assert offset + out.nbytes <= self.nbytes
+        check(_lib.dev().ucg_builtin_dev_memcpy(self.ctx.handle, out.ctypes.data,
+                                                self.ptr + offset, out.nbytes), "memcpy D2H")
+        return out
+
+    def free(self):
+        if self.ptr:
+            _lib.dev().ucg_builtin_dev_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class HostBuffer:
+    """Pinned (hipHostMalloc) host memory viewed as a numpy array."""
+
+    def __init__(self, nbytes):
+        self.nbytes = nbytes
+        self.ptr = _lib.dev().ucg_builtin_dev_host_alloc(nbytes)
+        if not self.ptr:
+            raise MemoryError(f"hipHostMalloc({nbytes}) failed: {_lib.last_error()}")
+
+    def view(self, dtype, count=None):
+        dtype = np.dtype(dtype)
+        count = self.nbytes // dtype.itemsize if count is None else count
+        buf = (ctypes.c_char * (count * dtype.itemsize)).from_address(self.ptr)
+        return np.frombuffer(buf, dtype=dtype, count=count)
+
+    def free(self):
+        if self.ptr:
+            _lib.dev().ucg_builtin_dev_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class DevContext:
+    """Per-group device context: one HIP stream, a pinned staging ring and the
+    per-step device accumulator."""
+
+    def __init__(self, device=-1, stream=None, stage_bytes=0, stage_slots=0):
+        L = _lib.dev()
+        p = _lib.DevCtxParams(device, stream or None, stage_bytes, stage_slots)
+        h = ctypes.c_void_p()
+        check(L.ucg_builtin_dev_ctx_create(ctypes.byref(p), ctypes.byref(h)),
+              "ucg_builtin_dev_ctx_create")
+        self.handle = h.value
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self):
+        if getattr(self, "handle", None):
+            _lib.dev().ucg_builtin_dev_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return _lib.dev().ucg_builtin_dev_ctx_stream(self.handle)
+
+    def sync(self):
+        check(_lib.dev().ucg_builtin_dev_sync(self.handle), "ucg_builtin_dev_sync")
+
+    # -- memory -----------------------------------------------------------
+    def alloc(self, nbytes):
+        return DevBuffer(self, nbytes)
+
+    def fill(self, dt, dist, seed, buf, count):
+        check(_lib.dev().ucg_builtin_dev_fill(self.handle, dt_index(dt), dist_index(dist),
+                                              seed, _ptr(buf), count), "ucg_builtin_dev_fill")
+
+    # -- combine ----------------------------------------------------------
+    def reduce(self, op, dt, dst, src, count):
+        """dst[i] = src[i] (op) dst[i] on device pointers (async)."""
+        return _lib.dev().ucg_builtin_dev_reduce(self.handle, op_index(op), dt_index(dt),
+                                                 _ptr(dst), _ptr(src), count)
+
+    def reduce_checked(self, op, dt, dst, src, count):
+        check(self.reduce(op, dt, dst, src, count), "ucg_builtin_dev_reduce")
+
+    def reduce_multi(self, op, dt, dst, srcs, self_index, count):
+        arr = (ctypes.c_void_p * len(srcs))(*[_ptr(s) for s in srcs])
+        return _lib.dev().ucg_builtin_dev_reduce_multi(self.handle, op_index(op),
+                                                       dt_index(dt), _ptr(dst), arr,
+                                                       len(srcs), self_index, count)
+
+    def combine_host(self, op, dt, dst_host, src_host, count):
+        return _lib.dev().ucg_builtin_dev_combine_host(self.handle, op_index(op),
+                                                       dt_index(dt), _ptr(dst_host),
+                                                       _ptr(src_host), count)
+
+    def stage_begin(self, host_dst, nbytes):
+        return _lib.dev().ucg_builtin_dev_stage_begin(self.handle, _ptr(host_dst), nbytes)
+
+    def combine(self, op, dt, dst_offset, host_src, count):
+        return _lib.dev().ucg_builtin_dev_combine(self.handle, op_index(op), dt_index(dt),
+                                                  dst_offset, _ptr(host_src), count)
+
+    def stage_end(self):
+        return _lib.dev().ucg_builtin_dev_stage_end(self.handle)
+
+    # -- profiling --------------------------------------------------------
+    def profile_reduce(self, op, dt, dst, src, count, iters):
+        us = ctypes.c_double()
+        check(_lib.dev().ucg_builtin_dev_profile_reduce(self.handle, op_index(op),
+                                                        dt_index(dt), _ptr(dst), _ptr(src),
+                                                        count, iters, ctypes.byref(us)),
+              "ucg_builtin_dev_profile_reduce")
+        return us.value
+
+    def counters(self):
+        out = (ctypes.c_uint64 * 4)()
+        _lib.dev().ucg_builtin_dev_counters(self.handle, out)
+        return {"launches": out[0], "combined_bytes": out[1], "h2d_bytes": out[2],
+                "d2h_bytes": out[3]}

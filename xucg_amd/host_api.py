@@ -1,0 +1,52 @@
+"""ctypes signatures of libucg_builtin.so (include/ucg_builtin_combine.h)."""
+import ctypes
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_int = ctypes.c_int
+_u = ctypes.c_uint
+_u64 = ctypes.c_uint64
+
+REDUCE_CB = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint, _vp)
+OP_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp)
+CONVERT_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_size_t))
+IS_INT_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int))
+DT_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp)
+
+
+class ReduceParams(ctypes.Structure):
+    """ucg_builtin_reduce_params_t (mirror of api/ucg.h:129-160)."""
+    _fields_ = [("reduce_cb_f", REDUCE_CB), ("is_sum_f", OP_FN),
+                ("is_loc_expected_f", OP_FN), ("is_commutative_f", OP_FN),
+                ("convert", CONVERT_FN), ("is_integer_f", IS_INT_FN),
+                ("is_floating_point_f", DT_FN)]
+
+
+class CombineConfig(ctypes.Structure):
+    _fields_ = [("dev_enable", ctypes.c_int), ("dev_min_bytes", _sz),
+                ("stage_bytes", _sz), ("stage_slots", ctypes.c_uint),
+                ("device", ctypes.c_int)]
+
+
+HOST_API = {
+    "ucg_builtin_combine_config_read": (None, [ctypes.POINTER(CombineConfig)]),
+    "ucg_builtin_combine_create": (_int, [ctypes.POINTER(ReduceParams),
+                                          ctypes.POINTER(CombineConfig),
+                                          ctypes.POINTER(_vp)]),
+    "ucg_builtin_combine_destroy": (None, [_vp]),
+    "ucg_builtin_combine_set_classifier": (None, [_vp, OP_FN, DT_FN]),
+    "ucg_builtin_combine_classify": (_int, [_vp, _vp, _vp, ctypes.POINTER(_int),
+                                            ctypes.POINTER(_int)]),
+    "ucg_builtin_combine_has_device": (_int, [_vp]),
+    "ucg_builtin_combine_dev_ctx": (_vp, [_vp]),
+    "ucg_builtin_combine_reduce": (_int, [_vp, _vp, _vp, _vp, _int, _vp]),
+    "ucg_builtin_combine_step_begin": (_int, [_vp, _vp, _vp, _vp, _sz]),
+    "ucg_builtin_combine_fragment": (_int, [_vp, _sz, _vp, _sz]),
+    "ucg_builtin_combine_step_end": (_int, [_vp]),
+    "ucg_builtin_combine_stats": (None, [_vp, ctypes.POINTER(_u64)]),
+    "ucg_builtin_step_fragment_length": (_sz, [_sz, _sz]),
+    "ucg_builtin_step_fragments_total": (_u64, [_sz, _sz, _u]),
+    "ucg_builtin_dev_chunk_bytes": (_sz, [_sz, _sz, _sz]),
+    "ucg_builtin_recursive_steps": (_u, [_u64, _u]),
+    "ucg_builtin_recursive_peer": (_u64, [_u64, _u, _u, _u]),
+}
