@@ -218,7 +218,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(n),
-                "kernel": "ucgdev::k_reduce<float, SUM, 4, 0>",
+                "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64>",
                 "kernel_avg_us": round(avg_us, 3),
                 "algorithmic_bytes_per_launch": bytes_per_step,
             },

@@ -22,7 +22,7 @@ fatal() { # rc -> 0 if the step may be followed by another GPU step
 
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
     echo "== pytest -m gpu" | tee -a "$OUT/steps.log"
-    timeout -k 10 900 python -m pytest tests -q -m gpu -x > "$OUT/pytest_gpu.log" 2>&1
+    timeout -k 10 900 python -m pytest tests -q -m gpu > "$OUT/pytest_gpu.log" 2>&1
     rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/steps.log"; tail -5 "$OUT/pytest_gpu.log"
     fatal $rc
 fi
@@ -36,7 +36,7 @@ if [ "$WHAT" = all ] || [ "$WHAT" = prof ]; then
     echo "== rocprofv3 kernel trace" | tee -a "$OUT/steps.log"
     cd /tmp
     timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
-        -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 \
+        -d "$OUT/prof" -o bench -- python3 "$ROOT/bench.py" \
         --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
     rc=$?; echo "rocprof rc=$rc" | tee -a "$OUT/steps.log"
     cd "$ROOT"

@@ -1,0 +1,200 @@
+"""The host C layer (libucg_builtin.so): dispatch, classification, staging
+and the control-path rules. CPU tests exercise the reduce_cb_f fallback; GPU
+tests (marked) exercise the device path through the same entry points."""
+import numpy as np
+import pytest
+
+import xucg_amd
+from xucg_amd import host
+from oracle import oracle as O
+
+from mock_mpi import (MockMPI, OPS, DTYPES, OP_MINLOC, DT_DOUBLE_INT,
+                      op_classifier, dt_classifier)
+
+
+def host_only_combine(mpi, **kw):
+    cfg = host.make_config(dev_enable=0)
+    return host.BuiltinCombine(mpi.callbacks(), cfg, **kw)
+
+
+def test_config_from_environment(monkeypatch):
+    monkeypatch.setenv("UCX_BUILTIN_DEV_COMBINE", "n")
+    monkeypatch.setenv("UCX_BUILTIN_DEV_MIN_BYTES", "64k")
+    monkeypatch.setenv("UCX_BUILTIN_DEV_STAGE_BYTES", "2m")
+    monkeypatch.setenv("UCX_BUILTIN_DEV_STAGE_SLOTS", "6")
+    monkeypatch.setenv("UCX_BUILTIN_DEV_DEVICE", "3")
+    c = host.read_config()
+    assert (c.dev_enable, c.dev_min_bytes, c.stage_bytes, c.stage_slots, c.device) == \
+        (0, 64 << 10, 2 << 20, 6, 3)
+    monkeypatch.delenv("UCX_BUILTIN_DEV_COMBINE")
+    monkeypatch.delenv("UCX_BUILTIN_DEV_MIN_BYTES")
+    c = host.read_config()
+    assert c.dev_enable == 1 and c.dev_min_bytes == 1 << 20
+
+
+def test_classification_through_api_callbacks():
+    mpi = MockMPI()
+    cmb = host_only_combine(mpi)
+    dev = {n: i for i, n in enumerate(O.DTYPES)}
+    # without the private classifier only SUM is identifiable (is_sum_f)
+    assert cmb.classify(OPS["sum"], DTYPES["int32"]) == (0, dev["int32"])
+    assert cmb.classify(OPS["sum"], DTYPES["uint64"]) == (0, dev["uint64"])
+    assert cmb.classify(OPS["sum"], DTYPES["float64"]) == (0, dev["float64"])
+    # api/ cannot tell fp16 from bf16: a 2-byte float is taken as fp16
+    assert cmb.classify(OPS["sum"], DTYPES["bfloat16"]) == (0, dev["float16"])
+    assert cmb.classify(OPS["max"], DTYPES["int32"]) is None
+    assert cmb.classify(OPS["sum"], DT_DOUBLE_INT) is None
+    cmb.close()
+
+
+def test_private_classifier_widens_the_device_set():
+    mpi = MockMPI()
+    cmb = host_only_combine(mpi, op_classifier=op_classifier, dt_classifier=dt_classifier)
+    assert cmb.classify(OPS["max"], DTYPES["int32"]) == (2, 4)
+    assert cmb.classify(OPS["bxor"], DTYPES["uint8"]) == (9, 1)
+    assert cmb.classify(OPS["sum"], DTYPES["bfloat16"]) == (0, 9)
+    assert cmb.classify(OPS["band"], DTYPES["float32"]) is None   # MPI-invalid
+    assert cmb.classify(OP_MINLOC, DTYPES["float64"]) is None
+    cmb.close()
+
+
+@pytest.mark.parametrize("dt,op", [("float32", "sum"), ("int64", "prod"),
+                                   ("float16", "max"), ("uint8", "bxor")])
+def test_host_fallback_is_the_callback(dt, op):
+    mpi = MockMPI()
+    cmb = host_only_combine(mpi)
+    src = O.fill(dt, "round", 1, 1001)
+    dst = O.fill(dt, "round", 2, 1001)
+    want = O.reduce(op, dt, src, dst)
+    assert cmb.reduce(OPS[op], src, dst, 1001, DTYPES[dt]) == 0
+    assert (O.bits(dst) == O.bits(want)).all()
+    assert mpi.calls == [(OPS[op], 1001, DTYPES[dt])]
+    assert cmb.stats()["host_calls"] == 1 and cmb.stats()["dev_calls"] == 0
+    assert cmb.reduce(OPS[op], src, dst, 0, DTYPES[dt]) == 0     # no-op
+    assert len(mpi.calls) == 1
+    cmb.close()
+
+
+def test_callback_errors_are_propagated():
+    mpi = MockMPI()
+    cmb = host_only_combine(mpi)
+    a = np.zeros(8, np.float32)
+    mpi.fail_next = True
+    assert cmb.reduce(OPS["sum"], a, a.copy(), 8, DTYPES["float32"]) == xucg_amd._lib.UCS_ERR_IO_ERROR
+    assert cmb.stats()["cb_errors"] == 1
+    cmb.close()
+
+
+def test_fragmented_step_on_host_follows_the_fragment_rule():
+    """ucg_builtin_mpi_reduce_fragment: count = length / dtype_length for each
+    AM-short fragment (builtin_comp_step.inl:112-120)."""
+    mpi = MockMPI()
+    cmb = host_only_combine(mpi)
+    n = 4096 // 8 + 3
+    acc = O.fill("float64", "round", 5, n)
+    src = O.fill("float64", "round", 6, n)
+    want = O.reduce("sum", "float64", src, acc)
+    frag = host.fragment_length(256, 8)
+    assert frag == 248
+    assert cmb.step_begin(OPS["sum"], DTYPES["float64"], acc, acc.nbytes) == 0
+    assert cmb.step_begin(OPS["sum"], DTYPES["float64"], acc, acc.nbytes) == -15  # BUSY
+    raw = src.view(np.uint8)
+    for off in range(0, acc.nbytes, frag):
+        ln = min(frag, acc.nbytes - off)
+        assert cmb.fragment(off, raw[off:off + ln].copy(), ln) == 0
+    assert cmb.fragment(acc.nbytes - 8, raw[:16].copy(), 16) == xucg_amd._lib.UCS_ERR_OUT_OF_RANGE
+    assert cmb.step_end() == 0
+    assert (O.bits(acc) == O.bits(want)).all()
+    counts = [c for _, c, _ in mpi.calls]
+    assert counts == [31] * (len(counts) - 1) + [(acc.nbytes % frag) // 8]
+    assert len(counts) == host.fragments_total(acc.nbytes, frag, 1)
+    cmb.close()
+
+
+def test_control_rules_match_the_oracle():
+    for ms in (64, 256, 2048, 8192, 65536):
+        for dl in (1, 2, 4, 8, 12, 16):
+            assert host.fragment_length(ms, dl) == O.frag_length(ms, dl)
+            for ln in (1, 100, 4096, 1 << 20):
+                fl = host.fragment_length(ms, dl)
+                assert host.fragments_total(ln, fl, 3) == O.fragments_total(ln, fl, 3)
+    assert host.fragment_length(8, 4) == 0
+    # chunk sizing: whole fragments per slot, capped by the step
+    assert host.dev_chunk_bytes(1 << 30, 248, 8 << 20) == (8 << 20) // 248 * 248
+    assert host.dev_chunk_bytes(1000, 248, 8 << 20) == 1000
+    # recursive K-ing (builtin_recursive.c:76-88, 158-169)
+    assert host.recursive_steps(8, 2) == 3
+    assert host.recursive_steps(4, 2) == 2
+    assert host.recursive_steps(6, 2) == 0
+    assert host.recursive_steps(27, 3) == 3
+    assert host.recursive_steps(1, 2) == 0
+    for size in (2, 4, 8, 16):
+        for my in range(size):
+            for step in range(1, host.recursive_steps(size) + 1):
+                assert host.recursive_peer(my, step) == O.recursive_peer(my, step)
+
+
+def test_recursive_factor3_peers_partition_the_group():
+    size, factor = 27, 3
+    for step in range(1, host.recursive_steps(size, factor) + 1):
+        for my in range(size):
+            peers = {host.recursive_peer(my, step, factor, k) for k in range(1, factor)}
+            group = peers | {my}
+            assert len(group) == factor
+            # every member of the group computes the same group
+            for p in peers:
+                assert {host.recursive_peer(p, step, factor, k) for k in range(1, factor)} | {p} == group
+
+
+# --------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,op", [("float32", "sum"), ("float64", "sum"),
+                                   ("int32", "max"), ("bfloat16", "prod")])
+def test_dispatcher_sends_large_calls_to_the_device(dt, op):
+    mpi = MockMPI()
+    cfg = host.make_config(dev_enable=1, dev_min_bytes=1 << 16, stage_bytes=1 << 20)
+    cmb = host.BuiltinCombine(mpi.callbacks(), cfg, op_classifier=op_classifier,
+                              dt_classifier=dt_classifier)
+    assert cmb.has_device
+    n = (1 << 20) + 7
+    src = O.fill(dt, "round", 1, n)
+    dst = O.fill(dt, "round", 2, n)
+    want = O.reduce(op, dt, src, dst)
+    assert cmb.reduce(OPS[op], src, dst, n, DTYPES[dt]) == 0, xucg_amd._lib.last_error()
+    assert (O.bits(dst) == O.bits(want)).all()
+    st = cmb.stats()
+    assert st["dev_calls"] == 1 and st["host_calls"] == 0 and not mpi.calls
+    # small calls and unclassified ops stay on the host callback
+    small_s, small_d = src[:100].copy(), dst[:100].copy()
+    w2 = O.reduce(op, dt, small_s, small_d)
+    assert cmb.reduce(OPS[op], small_s, small_d, 100, DTYPES[dt]) == 0
+    assert (O.bits(small_d) == O.bits(w2)).all()
+    assert cmb.stats()["host_calls"] == 1
+    cmb.close()
+
+
+@pytest.mark.gpu
+def test_staged_step_on_device_matches_host_fallback():
+    n = (1 << 20) + 3
+    frag = host.fragment_length(8192, 4)
+    src = O.fill("float32", "round", 3, n)
+    results = []
+    for dev in (1, 0):
+        mpi = MockMPI()
+        cfg = host.make_config(dev_enable=dev, dev_min_bytes=1 << 16, stage_bytes=1 << 20)
+        cmb = host.BuiltinCombine(mpi.callbacks(), cfg)
+        acc = O.fill("float32", "round", 4, n)
+        assert cmb.step_begin(OPS["sum"], DTYPES["float32"], acc, acc.nbytes) == 0
+        raw = src.view(np.uint8)
+        for off in range(0, acc.nbytes, frag):
+            ln = min(frag, acc.nbytes - off)
+            assert cmb.fragment(off, raw[off:off + ln], ln) == 0
+        assert cmb.step_end() == 0, xucg_amd._lib.last_error()
+        st = cmb.stats()
+        if dev:
+            assert st["dev_steps"] == 1 and st["host_calls"] == 0
+        else:
+            assert st["dev_steps"] == 0 and st["host_calls"] > 100
+        results.append(acc)
+        cmb.close()
+    assert (O.bits(results[0]) == O.bits(results[1])).all()

@@ -167,7 +167,12 @@ template <int OP> struct Comb<f16_t, OP> {
             o.b = (b < a) ? d.b : s.b;
             return o;
         }
-        const float r = (OP == UCG_DEV_OP_SUM) ? (a + b) : (a * b);
+        float r = (OP == UCG_DEV_OP_SUM) ? (a + b) : (a * b);
+        /* keep the fp32 result in a register: without this barrier hipcc
+         * (ROCm 7.2) folds fptrunc(fmul(fpext a, fpext b)) into
+         * v_fma_mixlo_f16 a, b, +0, i.e. fma(a, b, +0), which turns an exact
+         * -0 product into +0 (caught by tests/golden: (+0) x (-0)) */
+        __asm__ volatile("" : "+v"(r));
         if (__builtin_expect(isnan32(r), 0)) {
             o.b = nan16(s.b, d.b, isnan32(a), isnan32(b), 0x0200u, 0xfe00u);
         } else {

@@ -111,13 +111,13 @@ static unsigned grid_for(size_t work_items, size_t per_block, int cap)
 typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
                                   hipStream_t st, int variant);
 
-template <typename T, int OP, int U, int NT>
+template <typename T, int OP, int U, int NT, int BS>
 static void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
                        hipStream_t st)
 {
     /* one tile of U vectors per lane: grid sized to the data (no cap) */
-    const unsigned grid = grid_for(nvec, (size_t)kBlock * U, 0x7fffffff);
-    hipLaunchKernelGGL((k_reduce<T, OP, U, NT>), dim3(grid), dim3(kBlock), 0, st,
+    const unsigned grid = grid_for(nvec, (size_t)BS * U, 0x7fffffff);
+    hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS>), dim3(grid), dim3(BS), 0, st,
                        d, s, head, nvec, tail);
 }
 
@@ -150,13 +150,15 @@ static hipError_t launch_reduce(void *dst, const void *src, size_t count,
     if (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM && variant >= 0) {
         /* tuning variants of the headline kernel (UCX_BUILTIN_DEV_VARIANT) */
         switch (variant) {
-        case 1: launch_vec<T, OP, 2, 1>(d, s, head, nvec, tail, st); break;
-        case 2: launch_vec<T, OP, 4, 0>(d, s, head, nvec, tail, st); break;
-        case 3: launch_vec<T, OP, 2, 0>(d, s, head, nvec, tail, st); break;
-        default: launch_vec<T, OP, kReduceU, 1>(d, s, head, nvec, tail, st); break;
+        case 1: launch_vec<T, OP, 4, 1, 256>(d, s, head, nvec, tail, st); break;
+        case 2: launch_vec<T, OP, 1, 1, 256>(d, s, head, nvec, tail, st); break;
+        case 3: launch_vec<T, OP, 1, 0, 64>(d, s, head, nvec, tail, st); break;
+        default:
+            launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
+            break;
         }
     } else {
-        launch_vec<T, OP, kReduceU, 1>(d, s, head, nvec, tail, st);
+        launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
     }
     return hipGetLastError();
 }
@@ -214,8 +216,8 @@ static hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         head = count;
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
-    const unsigned grid = grid_for(nvec, (size_t)kBlock * kMultiU, 0x7fffffff);
-    hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kBlock), 0,
+    const unsigned grid = grid_for(nvec, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
+    hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
                        st, d, srcs, self, head, nvec, tail);
     return hipGetLastError();
 }

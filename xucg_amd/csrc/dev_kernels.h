@@ -24,8 +24,13 @@ namespace ucgdev {
 
 constexpr int kBlock = 256;           /* 4 waves of 64 lanes */
 constexpr int kMaxMulti = 16;         /* max operands of k_reduce_multi */
-constexpr int kMultiU   = 2;          /* vectors per lane in k_reduce_multi */
-constexpr int kReduceU  = 4;          /* vectors per lane in k_reduce */
+/* streaming-kernel geometry, measured on MI355X (profiles/r01/tune_*.txt):
+ * one wave per workgroup and one 16-B vector per lane per operand reached
+ * 85.5% of 8 TB/s on the 1 GiB fp32 combine, vs 80% for 256-lane groups
+ * with 4 vectors per lane and 55% for a grid-stride loop */
+constexpr int kReduceBlock = 64;      /* lanes per workgroup: one wave */
+constexpr int kReduceU     = 1;       /* 16-B vectors per lane per operand */
+constexpr int kMultiU      = 1;       /* same for k_reduce_multi */
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -71,16 +76,16 @@ __device__ __forceinline__ u32x4 vapply(u32x4 s, u32x4 d)
  * streams fresh workgroups onto the CUs and every wave issues its 2U loads
  * back to back before its first use. Loads and stores carry the non-temporal
  * hint: nothing is re-read, and measured on MI355X this geometry moved the
- * 2 x 256 MiB fp32 combine from 56% (grid-stride loop, temporal) to 79% of
- * 8 TB/s (profiles/). The ragged head (until dst is 16-B aligned)
+ * 2 x 256 MiB fp32 combine from 56% (grid-stride loop, temporal) to 85% of
+ * 8 TB/s with one-wave workgroups and U = 1 (profiles/r01). The ragged head (until dst is 16-B aligned)
  * and tail (< 16 B) are done by the first lanes of the grid.
  */
-template <typename T, int OP, int U, int NT>
-__global__ void __launch_bounds__(kBlock)
+template <typename T, int OP, int U, int NT, int BS>
+__global__ void __launch_bounds__(BS)
 k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 {
     constexpr int V   = 16 / sizeof(T);
-    const size_t gtid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t gtid = (size_t)blockIdx.x * BS + threadIdx.x;
 
     /* ragged edges: < V elements each, one lane per element */
     if (gtid < head) {
@@ -93,11 +98,11 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 
     const u32x4 *s4   = reinterpret_cast<const u32x4*>(src + head);
     u32x4 *d4         = reinterpret_cast<u32x4*>(dst + head);
-    const size_t base = (size_t)blockIdx.x * (kBlock * U) + threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * (BS * U) + threadIdx.x;
     u32x4 a[U], b[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const size_t i = base + (size_t)u * kBlock;
+        const size_t i = base + (size_t)u * BS;
         if (i < nvec) {
             a[u] = ld16<NT>(s4 + i);
             b[u] = ld16<NT>(d4 + i);
@@ -105,7 +110,7 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const size_t i = base + (size_t)u * kBlock;
+        const size_t i = base + (size_t)u * BS;
         if (i < nvec) {
             st16<NT>(d4 + i, vapply<T, OP>(a[u], b[u]));
         }
@@ -158,12 +163,12 @@ __device__ __forceinline__ E rd_tree(E (&val)[N], F f)
 }
 
 template <typename T, int OP, int N>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                size_t tail)
 {
     constexpr int V    = 16 / sizeof(T);
-    const size_t gtid  = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
     auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };
     auto fv = [](u32x4 a, u32x4 b) { return vapply<T, OP>(a, b); };
 
@@ -188,10 +193,10 @@ k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
     }
 
     u32x4 *d4 = reinterpret_cast<u32x4*>(dst + head);
-    const size_t base = (size_t)blockIdx.x * (kBlock * kMultiU) + threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * (kReduceBlock * kMultiU) + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < kMultiU; u++) {
-        const size_t i = base + (size_t)u * kBlock;
+        const size_t i = base + (size_t)u * kReduceBlock;
         if (i < nvec) {
             u32x4 val[N];
 #pragma unroll

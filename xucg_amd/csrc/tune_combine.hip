@@ -93,6 +93,68 @@ k_oneshot2(float *dst, const float *src, size_t nvec)
     }
 }
 
+/* variant F: oneshot, block size BS, U vectors per lane; CONTIG=1 gives each
+ * lane U consecutive 16-B vectors (32/64 B contiguous per lane); DFIRST
+ * loads dst before src */
+template <int U, int BS, int CONTIG, int DFIRST>
+__global__ void __launch_bounds__(BS)
+k_oneshot3(float *dst, const float *src, size_t nvec)
+{
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    const size_t blk = (size_t)blockIdx.x * BS * U;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = CONTIG ? blk + threadIdx.x * U + u : blk + threadIdx.x + u * BS;
+        if (i < nvec) {
+            if (DFIRST) {
+                b[u] = ld16<1>(d4 + i);
+                a[u] = ld16<1>(s4 + i);
+            } else {
+                a[u] = ld16<1>(s4 + i);
+                b[u] = ld16<1>(d4 + i);
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = CONTIG ? blk + threadIdx.x * U + u : blk + threadIdx.x + u * BS;
+        if (i < nvec) {
+            st16<1>(d4 + i, vapply<float, 0>(a[u], b[u]));
+        }
+    }
+}
+
+/* variant G: oneshot with buffer loads/stores and explicit cache-policy aux
+ * bits (gfx950: bit0 sc0, bit1 nt, bit4 sc1); byte offsets < 4 GiB */
+template <int U, int AUXL, int AUXS, int BS = 256>
+__global__ void __launch_bounds__(BS)
+k_oneshot_buf(float *dst, const float *src, size_t nvec)
+{
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)src, 0, (int)0xFFFFFFFF, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)dst, 0, (int)0xFFFFFFFF, 0x00020000);
+    const size_t base = (size_t)blockIdx.x * BS * U + threadIdx.x;
+    u32x4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + u * BS;
+        if (i < nvec) {
+            a[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(i * 16), 0, AUXL));
+            b[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rd, (unsigned)(i * 16), 0, AUXL));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + u * BS;
+        if (i < nvec) {
+            __builtin_amdgcn_raw_buffer_store_b128(vapply<float, 0>(a[u], b[u]), rd, (unsigned)(i * 16), 0, AUXS);
+        }
+    }
+}
+
 /* variant B: each block owns one contiguous chunk of vectors */
 template <int U, int NT, int BS>
 __global__ void __launch_bounds__(BS)
@@ -207,9 +269,13 @@ int main(int argc, char **argv)
 
     std::vector<Variant> vs;
     /* product kernel first: everything is checked against its output */
-    vs.push_back({"product k_reduce<f32,SUM,4,NT1>", [=](float *d, const float *s, size_t nv, hipStream_t q) {
+    vs.push_back({"product k_reduce<f32,SUM,1,NT1,bs64>", [=](float *d, const float *s, size_t nv, hipStream_t q) {
+        unsigned g = (unsigned)((nv + kReduceBlock * kReduceU - 1) / (kReduceBlock * kReduceU));
+        hipLaunchKernelGGL((k_reduce<float, 0, kReduceU, 1, kReduceBlock>), dim3(g), dim3(kReduceBlock), 0, q, d, s, (size_t)0, nv, (size_t)0);
+    }, {}});
+    vs.push_back({"previous k_reduce<f32,SUM,4,NT1,bs256>", [=](float *d, const float *s, size_t nv, hipStream_t q) {
         unsigned g = (unsigned)((nv + 1023) / 1024);
-        hipLaunchKernelGGL((k_reduce<float, 0, 4, 1>), dim3(g), dim3(256), 0, q, d, s, (size_t)0, nv, (size_t)0);
+        hipLaunchKernelGGL((k_reduce<float, 0, 4, 1, 256>), dim3(g), dim3(256), 0, q, d, s, (size_t)0, nv, (size_t)0);
     }, {}});
     auto grid_stride = [&](int U, int NT, int maxb) {
         char buf[128];
@@ -221,7 +287,6 @@ int main(int argc, char **argv)
         }, {}});
     };
     grid_stride(4, 0, 2048);
-    grid_stride(2, 1, 4096);
     auto oneshot2 = [&](int U, int NTL, int NTS, int XCD) {
         char buf[128];
         snprintf(buf, sizeof(buf), "oneshot2 U%d NTL%d NTS%d XCD%d", U, NTL, NTS, XCD);
@@ -234,75 +299,41 @@ int main(int argc, char **argv)
 #undef O2
         }, {}});
     };
-    oneshot2(4, 1, 1, 0);
-    oneshot2(4, 1, 0, 0);
-    oneshot2(4, 0, 1, 0);
-    oneshot2(4, 1, 1, 1);
-    oneshot2(2, 1, 1, 0);
-    oneshot2(2, 1, 1, 1);
     oneshot2(1, 1, 1, 0);
-    oneshot2(3, 1, 1, 0);
-    oneshot2(6, 1, 1, 0);
 
-    auto chunked = [&](int U, int NT, int blocks) {
+    auto os3 = [&](int U, int BS, int CONTIG, int DFIRST) {
         char buf[128];
-        snprintf(buf, sizeof(buf), "chunked U%d NT%d blocks%d", U, NT, blocks);
-        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
-            size_t per = (nv + blocks - 1) / blocks;
-            per = (per + 255) / 256 * 256;
-            unsigned g = (unsigned)((nv + per - 1) / per);
-#define CK(UU, NN) hipLaunchKernelGGL((k_chunked<UU, NN, 256>), dim3(g), dim3(256), 0, q, d, s, nv, per)
-            if (U == 4 && NT == 0) CK(4, 0);
-            if (U == 8 && NT == 0) CK(8, 0);
-            if (U == 4 && NT == 1) CK(4, 1);
-#undef CK
-        }, {}});
-    };
-    chunked(4, 0, 2048);
-    chunked(4, 0, 1024);
-    chunked(8, 0, 1024);
-    chunked(4, 1, 2048);
-
-    auto oneshot = [&](int U, int NT, int BS) {
-        char buf[128];
-        snprintf(buf, sizeof(buf), "oneshot U%d NT%d bs%d", U, NT, BS);
+        snprintf(buf, sizeof(buf), "oneshot3 U%d bs%d contig%d dfirst%d", U, BS, CONTIG, DFIRST);
         vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
             unsigned g = (unsigned)((nv + (size_t)BS * U - 1) / ((size_t)BS * U));
-#define OS(UU, NN, BB) hipLaunchKernelGGL((k_oneshot<UU, NN, BB>), dim3(g), dim3(BB), 0, q, d, s, nv)
-            if (U == 4 && NT == 0 && BS == 256) OS(4, 0, 256);
-            if (U == 2 && NT == 0 && BS == 256) OS(2, 0, 256);
-            if (U == 8 && NT == 0 && BS == 256) OS(8, 0, 256);
-            if (U == 4 && NT == 1 && BS == 256) OS(4, 1, 256);
-            if (U == 4 && NT == 0 && BS == 512) OS(4, 0, 512);
-            if (U == 2 && NT == 0 && BS == 1024) OS(2, 0, 1024);
-#undef OS
+#define O3(A, B, C, D) if (U == A && BS == B && CONTIG == C && DFIRST == D) hipLaunchKernelGGL((k_oneshot3<A, B, C, D>), dim3(g), dim3(B), 0, q, d, s, nv)
+            O3(1, 64, 0, 0); O3(2, 64, 0, 0); O3(4, 64, 0, 0); O3(1, 64, 0, 1);
+            O3(2, 128, 0, 0); O3(1, 128, 0, 0);
+#undef O3
         }, {}});
     };
-    oneshot(4, 0, 256);
-    oneshot(2, 0, 256);
-    oneshot(8, 0, 256);
-    oneshot(4, 1, 256);
-    oneshot(4, 0, 512);
-    oneshot(2, 0, 1024);
-
+    os3(1, 64, 0, 0);
+    os3(2, 64, 0, 0);
+    os3(4, 64, 0, 0);
+    os3(1, 64, 0, 1);
+    os3(2, 128, 0, 0);
+    os3(1, 128, 0, 0);
     if (nvec * 16 <= 0xFFFFFFFFull) {
-        auto buffer = [&](const char *nm, int aux_l, int aux_s, int maxb) {
+        auto osb = [&](int U, int AL, int AS, int BS) {
             char buf[128];
-            snprintf(buf, sizeof(buf), "buffer %s blocks%d", nm, maxb);
+            snprintf(buf, sizeof(buf), "oneshot_buf U%d auxL%d auxS%d bs%d", U, AL, AS, BS);
             vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
-                unsigned g = (unsigned)std::min<size_t>((nv + 1023) / 1024, maxb);
-#define BF(L, S) hipLaunchKernelGGL((k_buffer<4, L, S, 256>), dim3(g), dim3(256), 0, q, d, s, nv)
-                if (aux_l == 0 && aux_s == 0) BF(0, 0);
-                if (aux_l == 2 && aux_s == 2) BF(2, 2);
-                if (aux_l == 0 && aux_s == 2) BF(0, 2);
-                if (aux_l == 2 && aux_s == 0) BF(2, 0);
-#undef BF
+                unsigned g = (unsigned)((nv + (size_t)BS * U - 1) / ((size_t)BS * U));
+#define OB(A, B, C, D) if (U == A && AL == B && AS == C && BS == D) hipLaunchKernelGGL((k_oneshot_buf<A, B, C, D>), dim3(g), dim3(D), 0, q, d, s, nv)
+                OB(1, 2, 2, 64); OB(1, 18, 2, 64); OB(1, 3, 2, 64); OB(2, 18, 2, 64); OB(1, 18, 18, 64);
+#undef OB
             }, {}});
         };
-        buffer("plain", 0, 0, 2048);
-        buffer("nt-both", 2, 2, 2048);
-        buffer("nt-store", 0, 2, 2048);
-        buffer("nt-load", 2, 0, 2048);
+        osb(1, 2, 2, 64);
+        osb(1, 18, 2, 64);
+        osb(1, 3, 2, 64);
+        osb(2, 18, 2, 64);
+        osb(1, 18, 18, 64);
     }
 
     /* init */
