@@ -109,7 +109,7 @@ typedef enum ucg_dev_dtype {
 } ucg_dev_dtype_t;
 
 /* Reduction operators (MPI predefined ops without MINLOC/MAXLOC, which the
- * reference rejects: builtin/ops/builtin_control.c:881-884). */
+ * reference rejects: builtin/ops/builtin_control.c:884-887). */
 typedef enum ucg_dev_op {
     UCG_DEV_OP_SUM = 0,
     UCG_DEV_OP_PROD,
