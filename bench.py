@@ -92,6 +92,144 @@ def cpu_baseline(count, budget_s=10.0):
     }
 
 
+def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
+    """BASELINE configs 4 and 5 across the N GPUs of the node (N > 1 only).
+
+    C4: reduce-scatter + all-gather of a 4 GiB fp32 buffer
+        (a) RCCL reduce_scatter_tensor + all_gather_into_tensor (ring order)
+        (b) one-shot xGMI reduce-scatter: every GPU reads its 1/N shard from
+            all N peer-mapped buffers and combines them in the reference
+            plan's association (ucg_builtin_dev_reduce_multi), then RCCL
+            all-gather; parity vs (a) on exact-integer inputs (bit-exact)
+    C5: the reference recursive-doubling allreduce (builtin_recursive.c:
+        158-169) of 512 MiB fp64 per GPU: RCCL send/recv of the whole
+        accumulator + device combine per step; parity: bit-exact against a
+        local one-shot evaluation of the same association
+    busBW = (N-1)/N x S / t per collective. Every phase is
+    guarded; an error is recorded in the JSON instead of aborting the line."""
+    import torch
+    from xucg_amd import group as G
+
+    dev = torch.device(f"cuda:{local_rank}")
+    out = {}
+
+    def agreed(fn, name):
+        err = None
+        try:
+            res = fn()
+        except Exception as e:  # recorded, then agreed on by every rank
+            res, err = None, f"{type(e).__name__}: {e}"[:300]
+        flag = torch.tensor([1.0 if err else 0.0], device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if err or flag.item() > 0:
+            out[name] = {"error": err or "failed on another rank"}
+        else:
+            out[name] = res
+
+    def timed(fn, iters):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item() / iters
+
+    n4 = 1 << 30                      # 4 GiB fp32 (config 4)
+    shard = n4 // world
+    x = torch.empty(n4, dtype=torch.float32, device=dev)
+    ctx.fill("float32", "exact", 0x5EED4000 + rank, x, n4)
+    ctx.sync()
+    rs_out = torch.empty(shard, dtype=torch.float32, device=dev)
+    ag_out = torch.empty(n4, dtype=torch.float32, device=dev)
+    s_bytes = n4 * 4
+    bus = (world - 1) / world * s_bytes
+
+    def rccl():
+        for _ in range(warmup):
+            dist.reduce_scatter_tensor(rs_out, x)
+            dist.all_gather_into_tensor(ag_out, rs_out)
+        t_rs = timed(lambda: dist.reduce_scatter_tensor(rs_out, x), steps)
+        t_ag = timed(lambda: dist.all_gather_into_tensor(ag_out, rs_out), steps)
+        return {"bytes": s_bytes, "rs_ms": round(t_rs * 1e3, 3),
+                "ag_ms": round(t_ag * 1e3, 3),
+                "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
+                "ag_busbw_gbs": round(bus / t_ag / 1e9, 1)}
+    agreed(rccl, "c4_rccl_rs_ag_4gib_fp32")
+
+    def oneshot():
+        if world & (world - 1) or world > 16:
+            return {"skipped": "one-shot needs a power-of-two group <= 16"}
+        peers = G.PeerBuffers(ctx, x.data_ptr(), rank, world, dist)
+        mine = torch.empty(shard, dtype=torch.float32, device=dev)
+        try:
+            def rs():
+                G.oneshot_reduce_scatter(ctx, peers, mine.data_ptr(), n4, "float32",
+                                         "sum", rank, world)
+                torch.cuda.synchronize()  # readers done before anyone proceeds
+                dist.barrier()
+            for _ in range(warmup):
+                rs()
+            t_rs = timed(rs, steps)
+            dist.reduce_scatter_tensor(rs_out, x)
+            torch.cuda.synchronize()
+            same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
+            t_ag = timed(lambda: dist.all_gather_into_tensor(ag_out, mine), steps)
+        finally:
+            torch.cuda.synchronize()
+            dist.barrier()
+            peers.close()
+        return {"bytes": s_bytes, "rs_ms": round(t_rs * 1e3, 3),
+                "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
+                "rs_ag_ms": round((t_rs + t_ag) * 1e3, 3),
+                "bit_exact_vs_rccl_on_exact_inputs": same,
+                "association": "recursive doubling (builtin_recursive.c:158-169)"}
+    agreed(oneshot, "c4_oneshot_xgmi_rs_4gib_fp32")
+    del x, rs_out, ag_out
+    torch.cuda.empty_cache()
+
+    def recursive_doubling():
+        if world & (world - 1):
+            return {"skipped": "recursive doubling needs a power-of-two group"}
+        n5 = 1 << 26                  # 512 MiB fp64 per rank (config 5)
+        init = torch.empty(n5, dtype=torch.float64, device=dev)
+        ctx.fill("float64", "round", 0x5EED5000 + rank, init, n5)
+        acc = torch.empty_like(init)
+        tmp = torch.empty_like(init)
+        exchange = G.torch_exchange(dist)
+
+        def combine(a, t):
+            ctx.reduce_checked("sum", "float64", a, t, n5)
+
+        def once():
+            acc.copy_(init)           # ucg_builtin_init_reduce: recv <- send
+            G.recursive_doubling_allreduce(acc, tmp, rank, world, combine, exchange)
+        once()
+        torch.cuda.synchronize()
+        # parity: every member's input regenerated locally, one-shot tree
+        allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
+        for r in range(world):
+            ctx.fill("float64", "round", 0x5EED5000 + r, allx[r], n5)
+        ref = torch.empty_like(init)
+        _lib_check = ctx.reduce_multi("sum", "float64", ref, allx, rank, n5)
+        ctx.sync()
+        same = _lib_check == 0 and bool(torch.equal(acc.view(torch.int64),
+                                                    ref.view(torch.int64)))
+        del allx, ref
+        t = timed(once, steps)
+        steps_n = G.recursive_steps(world)
+        return {"bytes_per_rank": n5 * 8, "ms": round(t * 1e3, 3),
+                "steps": steps_n,
+                "algbw_gbs": round(n5 * 8 / t / 1e9, 1),
+                "link_gbs_per_step": round(n5 * 8 * steps_n / t / 1e9, 1),
+                "bit_exact_vs_oneshot_tree": same}
+    agreed(recursive_doubling, "c5_recursive_doubling_512mib_fp64")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,6 +238,10 @@ def main():
     ap.add_argument("--count", type=int, default=WORKLOAD_COUNT)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true")
+    ap.add_argument("--no-collective", action="store_true",
+                    help="N > 1: skip the RS+AG / recursive-doubling phases")
+    ap.add_argument("--collective-force", action="store_true",
+                    help="run the collective phases even at N = 1 (under torchrun)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -110,7 +252,7 @@ def main():
     import xucg_amd
 
     dist = None
-    if world > 1:
+    if world > 1 or args.collective_force:
         import datetime
         import torch.distributed as dist
         torch.cuda.set_device(local_rank)
@@ -122,7 +264,11 @@ def main():
             dist.barrier()
 
     n = args.count
-    ctx = xucg_amd.DevContext(device=local_rank)
+    # multi-GPU: launch on torch's current stream so RCCL and the combine are
+    # stream-ordered without host syncs
+    ctx = xucg_amd.DevContext(
+        device=local_rank,
+        stream=torch.cuda.current_stream(local_rank).cuda_stream if dist else None)
     src = ctx.alloc(n * 4)
     dst = ctx.alloc(n * 4)
     ctx.fill("float32", "round", 0x5EED0000 + 2 * rank, src, n)
@@ -187,6 +333,12 @@ def main():
         hs.free()
         hd.free()
 
+    collective = None
+    if (world > 1 and not args.no_collective) or args.collective_force:
+        src.free()
+        dst.free()
+        collective = collective_phases(ctx, dist, rank, world, local_rank)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
@@ -224,6 +376,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "extra": extra,
+            "collective": collective,
         }
         print(json.dumps(line), flush=True)
 

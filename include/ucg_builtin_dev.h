@@ -201,6 +201,18 @@ ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
                                      size_t count);
 ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx);
 
+/* ---- peer mapping (xGMI) for the one-shot multi-operand combine ----------*/
+/* An exported device buffer: the HIP IPC handle of its allocation plus the
+ * byte offset of the pointer inside that allocation. Opaque, fixed size. */
+#define UCG_BUILTIN_DEV_IPC_HANDLE_BYTES 80
+ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
+                                        const void *dev_ptr, void *handle);
+/* Map a peer's exported buffer into this process (lazy peer access). */
+ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
+                                        const void *handle, void **dev_ptr);
+ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx,
+                                         void *dev_ptr);
+
 /* ---- memory helpers --------------------------------------------------------*/
 void        *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
 void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);

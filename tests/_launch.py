@@ -1,0 +1,44 @@
+"""Launch N worker processes (one per rank) as children and collect exit codes.
+
+Workers are started with subprocess (fork + exec in the child), never by
+replacing this process; every worker gets a hard time limit and is killed by
+its exact PID when it overruns."""
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch(worker, world, args=(), timeout=240):
+    port = free_port()
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
+    env["MASTER_ADDR"] = "127.0.0.1"
+    env["MASTER_PORT"] = str(port)
+    env["WORLD_SIZE"] = str(world)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    procs = []
+    for r in range(world):
+        e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", worker),
+                                       *map(str, args)], env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs, codes = [], []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+            out += "\n<killed: timeout>"
+        outs.append(out)
+        codes.append(p.returncode)
+    return codes, outs

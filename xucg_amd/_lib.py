@@ -32,6 +32,7 @@ UCS_ERR_NOT_IMPLEMENTED = -8
 UCS_ERR_NO_DEVICE = -14
 UCS_ERR_OUT_OF_RANGE = -19
 UCS_ERR_UNSUPPORTED = -22
+IPC_HANDLE_BYTES = 80  # UCG_BUILTIN_DEV_IPC_HANDLE_BYTES
 
 # every exported C-ABI function: name -> (restype, argtypes)
 _vp = ctypes.c_void_p
@@ -65,6 +66,9 @@ DEV_API = {
     "ucg_builtin_dev_stage_begin": (_st, [_vp, _vp, _sz]),
     "ucg_builtin_dev_combine": (_st, [_vp, _int, _int, _sz, _vp, _sz]),
     "ucg_builtin_dev_stage_end": (_st, [_vp]),
+    "ucg_builtin_dev_ipc_export": (_st, [_vp, _vp, _vp]),
+    "ucg_builtin_dev_ipc_import": (_st, [_vp, _vp, ctypes.POINTER(_vp)]),
+    "ucg_builtin_dev_ipc_release": (_st, [_vp, _vp]),
     "ucg_builtin_dev_malloc": (_vp, [_vp, _sz]),
     "ucg_builtin_dev_free": (None, [_vp, _vp]),
     "ucg_builtin_dev_host_alloc": (_vp, [_sz]),

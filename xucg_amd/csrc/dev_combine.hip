@@ -869,6 +869,72 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
     return UCS_OK;
 }
 
+/* ---- peer mapping ------------------------------------------------------- */
+struct ipc_blob {
+    hipIpcMemHandle_t handle;
+    uint64_t          offset;
+    uint64_t          magic;
+};
+static_assert(sizeof(ipc_blob) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES,
+              "IPC blob does not fit the ABI size");
+static const uint64_t kIpcMagic = 0x5543475f49504331ull; /* "UCG_IPC1" */
+
+ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
+                                        const void *dev_ptr, void *handle)
+{
+    if (ctx == nullptr || dev_ptr == nullptr || handle == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_export", "bad arguments");
+    }
+    ucs_status_t st = set_device(ctx);
+    if (st != UCS_OK) {
+        return st;
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr));
+    ipc_blob b;
+    memset(&b, 0, sizeof(b));
+    HIP_TRY(hipIpcGetMemHandle(&b.handle, (void*)base));
+    b.offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
+    b.magic  = kIpcMagic;
+    memset(handle, 0, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    memcpy(handle, &b, sizeof(b));
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
+                                        const void *handle, void **dev_ptr)
+{
+    if (ctx == nullptr || handle == nullptr || dev_ptr == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import", "bad arguments");
+    }
+    ipc_blob b;
+    memcpy(&b, handle, sizeof(b));
+    if (b.magic != kIpcMagic) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import", "not an exported handle");
+    }
+    ucs_status_t st = set_device(ctx);
+    if (st != UCS_OK) {
+        return st;
+    }
+    void *base = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&base, b.handle, hipIpcMemLazyEnablePeerAccess));
+    *dev_ptr = (char*)base + b.offset;
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx, void *dev_ptr)
+{
+    if (ctx == nullptr || dev_ptr == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_release", "bad arguments");
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr));
+    HIP_TRY(hipIpcCloseMemHandle((void*)base));
+    return UCS_OK;
+}
+
 /* ---- memory helpers ------------------------------------------------------ */
 void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
 {

@@ -186,6 +186,26 @@ class DevContext:
     def stage_end(self):
         return _lib.dev().ucg_builtin_dev_stage_end(self.handle)
 
+    # -- peer mapping -----------------------------------------------------
+    def ipc_export(self, buf):
+        """Opaque bytes naming `buf` for another process (xGMI peer)."""
+        h = (ctypes.c_char * _lib.IPC_HANDLE_BYTES)()
+        check(_lib.dev().ucg_builtin_dev_ipc_export(self.handle, _ptr(buf), h),
+              "ucg_builtin_dev_ipc_export")
+        return bytes(h)
+
+    def ipc_import(self, blob):
+        """Map a peer buffer exported by ipc_export(); returns a device pointer."""
+        h = (ctypes.c_char * _lib.IPC_HANDLE_BYTES).from_buffer_copy(blob)
+        p = ctypes.c_void_p()
+        check(_lib.dev().ucg_builtin_dev_ipc_import(self.handle, h, ctypes.byref(p)),
+              "ucg_builtin_dev_ipc_import")
+        return p.value
+
+    def ipc_release(self, ptr):
+        check(_lib.dev().ucg_builtin_dev_ipc_release(self.handle, ptr),
+              "ucg_builtin_dev_ipc_release")
+
     # -- profiling --------------------------------------------------------
     def profile_reduce(self, op, dt, dst, src, count, iters):
         us = ctypes.c_double()

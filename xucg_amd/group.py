@@ -1,0 +1,127 @@
+"""Multi-rank execution of the combine path: one process per GPU.
+
+torch.distributed is the plumbing (RCCL over xGMI on the GPU box, gloo for
+CPU tests); every combine runs through the C-ABI device shim. Three ways to
+allreduce a buffer across 2^k members, all built on the same combine:
+
+  recursive_doubling_allreduce  the reference plan itself
+                                (builtin/plan/builtin_recursive.c:158-169):
+                                at step k exchange the whole accumulator with
+                                member my ^ 2^(k-1), then acc = incoming (op)
+                                acc. Bit-exact with the reference.
+  oneshot_reduce_scatter        every member owns a contiguous shard and reads
+                                that shard from all members at once (peer
+                                mapped, xGMI), evaluating the same per-element
+                                association as the plan in registers
+                                (ucg_builtin_dev_reduce_multi); followed by an
+                                all-gather. Bit-exact with the plan's result
+                                on the shard owner.
+  RCCL reduce_scatter + all_gather  the vendor baseline (ring association:
+                                within the fp tolerance of SURVEY.md 8c only).
+"""
+import numpy as np
+
+from . import _lib
+
+SHARD_ALIGN_BYTES = 256
+
+
+def shard_bounds(count, elem_size, world, rank, align_bytes=SHARD_ALIGN_BYTES):
+    """[lo, hi) element range of `rank`'s shard: equal shards
+    rounded down to `align_bytes`, the remainder to the last rank."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    align = align_bytes // elem_size if align_bytes % elem_size == 0 else 1
+    per = (count // world) // align * align
+    lo = per * rank
+    hi = count if rank == world - 1 else per * (rank + 1)
+    return lo, hi
+
+
+def recursive_steps(world, factor=2):
+    """Number of recursive steps, 0 when world is not a power of factor
+    (builtin/plan/builtin_recursive.c:76-88)."""
+    return _lib.host().ucg_builtin_recursive_steps(world, factor)
+
+
+def recursive_peer(rank, step, factor=2, peer_idx=1):
+    return _lib.host().ucg_builtin_recursive_peer(rank, step, factor, peer_idx)
+
+
+def recursive_doubling_allreduce(acc, tmp, rank, world, combine, exchange):
+    """The reference recursive-doubling plan.
+
+    acc      this member's contribution on entry, the allreduce on exit
+             (ucg_builtin_init_reduce seeds recv <- send, builtin_control.c:43-47)
+    tmp      receive buffer of the same size
+    combine  combine(dst=acc, src=tmp): dst = src (op) dst
+    exchange exchange(send=acc, recv=tmp, peer): full-vector swap
+    """
+    if world == 1:
+        return
+    steps = recursive_steps(world)
+    if steps == 0:
+        raise ValueError("recursive doubling needs a power-of-two group "
+                         "(builtin_recursive.c:78-88 returns UNSUPPORTED)")
+    for step in range(1, steps + 1):
+        peer = recursive_peer(rank, step)
+        exchange(acc, tmp, peer)
+        combine(acc, tmp)
+
+
+def torch_exchange(dist, group=None):
+    """exchange() over torch.distributed point-to-point (RCCL or gloo)."""
+    def exchange(send, recv, peer):
+        ops = [dist.P2POp(dist.isend, send, peer, group),
+               dist.P2POp(dist.irecv, recv, peer, group)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+    return exchange
+
+
+class PeerBuffers:
+    """Every member's buffer mapped into this process (IPC over xGMI).
+
+    ptrs[r] is a device pointer to member r's buffer (the local one for
+    r == rank). Collective: every member must construct it together."""
+
+    def __init__(self, ctx, local_ptr, rank, world, dist, group=None):
+        self.ctx = ctx
+        self.rank = rank
+        blob = ctx.ipc_export(local_ptr)
+        blobs = [None] * world
+        dist.all_gather_object(blobs, blob, group=group)
+        self.ptrs = []
+        self._imported = []
+        for r, b in enumerate(blobs):
+            if r == rank:
+                self.ptrs.append(local_ptr)
+            else:
+                p = ctx.ipc_import(b)
+                self._imported.append(p)
+                self.ptrs.append(p)
+
+    def close(self):
+        for p in self._imported:
+            self.ctx.ipc_release(p)
+        self._imported = []
+
+
+def oneshot_reduce_scatter(ctx, peers, out_ptr, count, dt, op, rank, world):
+    """out[0:hi-lo] = V(rank, log2 world) over shard [lo, hi) of every member's
+    buffer, read in place through `peers` (no staging copy). The caller must
+    have all members' inputs complete before, and keep them until all members
+    finished (barrier on both sides)."""
+    size = _lib.DTYPE_SIZE[_lib.dt_index(dt)]
+    lo, hi = shard_bounds(count, size, world, rank)
+    srcs = [p + lo * size for p in peers.ptrs]
+    _lib.check(ctx.reduce_multi(op, dt, out_ptr, srcs, rank, hi - lo),
+               "ucg_builtin_dev_reduce_multi")
+    return lo, hi
+
+
+def oracle_shard(op, dt, inputs, rank, world, oracle):
+    """Expected one-shot shard for tests: the plan's result on the owner."""
+    size = np.dtype(inputs[0].dtype).itemsize
+    lo, hi = shard_bounds(inputs[0].size, size, world, rank)
+    return lo, hi, oracle.reduce_multi(op, dt, [x[lo:hi] for x in inputs], rank)
