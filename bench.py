@@ -92,6 +92,36 @@ def cpu_baseline(count, budget_s=10.0):
     }
 
 
+def c1_loopback(ranks=4, iters=20000):
+    """BASELINE config 1 on this host's CPUs: 4 processes allreduce 4 KiB fp32
+    through the builtin operation engine over the shared-memory transport
+    (tests/c/c1_allreduce.c; host combine, no GPU). Latency per allreduce."""
+    import subprocess
+    import uuid
+    exe = os.path.join(ROOT, "tests", "c", "_build", "c1_allreduce")
+    res = {}
+    for max_short in (256, 8192):
+        name = f"ucg_bench_c1_{os.getpid()}_{uuid.uuid4().hex[:6]}"
+        procs = []
+        for r in range(ranks):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(ranks))
+            procs.append(subprocess.Popen([exe, name, str(iters), str(max_short)], env=env,
+                                          stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                          text=True))
+        outs = []
+        for p in procs:
+            try:
+                outs.append(p.communicate(timeout=120)[0])
+            except subprocess.TimeoutExpired:
+                p.kill()
+                outs.append(p.communicate()[0] + " <timeout>")
+        try:
+            res[f"max_short_{max_short}"] = json.loads(outs[0].strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            res[f"max_short_{max_short}"] = {"error": outs[0][-300:]}
+    return res
+
+
 def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     """BASELINE configs 4 and 5 across the N GPUs of the node (N > 1 only).
 
@@ -342,6 +372,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
+        extra["c1_loopback_allreduce_4kib_fp32"] = c1_loopback()
 
     if rank == 0:
         line = {

@@ -83,6 +83,11 @@ void         ucg_builtin_combine_set_classifier(ucg_builtin_combine_t *cmb,
 int          ucg_builtin_combine_classify(ucg_builtin_combine_t *cmb,
                                           void *reduce_op, void *datatype,
                                           ucg_dev_op_t *op, ucg_dev_dtype_t *dt);
+/* Contiguous element length of an opaque datatype (datatype.convert +
+ * ucp_contig_dt_length, builtin/ops/builtin_control.c:1091-1093); 0 if not
+ * contiguous. NULL is one byte (api/ucg.h:354-356). */
+size_t       ucg_builtin_combine_dtype_length(ucg_builtin_combine_t *cmb,
+                                              void *datatype);
 /* 1 when a device context is attached (a GPU was found and enabled). */
 int          ucg_builtin_combine_has_device(ucg_builtin_combine_t *cmb);
 ucg_builtin_dev_ctx_t *ucg_builtin_combine_dev_ctx(ucg_builtin_combine_t *cmb);

@@ -84,7 +84,9 @@ typedef enum {
     UCS_ERR_NOT_IMPLEMENTED =  -8,
     UCS_ERR_NO_DEVICE       = -14,
     UCS_ERR_BUSY            = -15,
+    UCS_ERR_CANCELED        = -16,
     UCS_ERR_OUT_OF_RANGE    = -19,
+    UCS_ERR_TIMED_OUT       = -20,
     UCS_ERR_UNSUPPORTED     = -22
 } ucs_status_t;
 #endif

@@ -1,0 +1,112 @@
+/*
+ * ucg_builtin_ops.h - the builtin planner's operation engine around the
+ * combine, and a minimal host transport so a multi-process allreduce runs
+ * without UCX.
+ *
+ * Reference anchors (paths relative to the reference tree):
+ *   transport      uct_ep_am_short()/uct_iface_progress() as used by
+ *                  builtin/ops/builtin_data.c:37-137 and builtin/builtin.c:
+ *                  318-340; the AM data is borrowed for the callback only.
+ *   wire header    ucg_builtin_header_t, builtin/ops/builtin_ops.h:53-60:
+ *                  {u16 group_id; u8 coll_id; u8 step_idx; u32 remote_offset}
+ *   slots          UCG_BUILTIN_MAX_CONCURRENT_OPS = 16, slot = coll_id % 16,
+ *                  builtin/ops/builtin_ops.h:388, builtin/builtin.c:153-155
+ *   AM handler     direct combine when local_id matches, else stash,
+ *                  builtin/builtin.c:133-219
+ *   step execute   send every fragment to every peer, then drain stashed
+ *                  messages, builtin/ops/builtin_data.c:584-668 and
+ *                  builtin/ops/builtin_comp_step.inl:403-462
+ *   completion     pending = ep_cnt x fragments, next step or finish,
+ *                  builtin/ops/builtin_comp_step.inl:8-95,342-401
+ *   plan           recursive doubling, builtin/plan/builtin_recursive.c:20-228
+ *   fragments      builtin/ops/builtin_control.c:434,462-465
+ *   seeding        ucg_builtin_init_reduce, builtin/ops/builtin_control.c:43-47
+ *
+ * Every combine goes through ucg_builtin_combine_step_begin/_fragment/
+ * _step_end (include/ucg_builtin_combine.h): steps large enough and of a
+ * classified type run on the device, the rest call the user's reduce_cb_f.
+ */
+#ifndef UCG_BUILTIN_OPS_H_
+#define UCG_BUILTIN_OPS_H_
+
+#include "ucg_builtin_combine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UCG_BUILTIN_OPS_MAX_CONCURRENT 16   /* builtin_ops.h:388 */
+#define UCG_BUILTIN_OPS_MAX_MEMBERS    64
+
+/* ---- f2: shared-memory active-message transport ------------------------ */
+typedef struct ucg_builtin_shm_iface ucg_builtin_shm_iface_t;
+
+/* Called for every delivered message: data = 8-B header + payload,
+ * `length` includes the header. The data is valid during the call only. */
+typedef ucs_status_t (*ucg_builtin_am_cb_f)(void *arg, void *data, size_t length);
+
+/* Collective over the `members` processes of one host: every member opens
+ * the same `name` (a POSIX shm object, unlinked by member 0 on close).
+ * max_short is the largest AM including the 8-B header (UCT cap.am.max_short;
+ * the reference's BUILTIN_SHORT_MAX_TX_SIZE default is 256). */
+ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
+                                        unsigned my_index, size_t max_short,
+                                        unsigned ring_cells,
+                                        ucg_builtin_shm_iface_t **iface_p);
+void         ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *iface);
+size_t       ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *iface);
+/* uct_ep_am_short: UCS_ERR_NO_RESOURCE when the peer's ring is full */
+ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *iface,
+                                      unsigned peer, uint64_t header,
+                                      const void *payload, size_t length);
+/* uct_iface_progress: deliver pending messages; returns how many */
+unsigned     ucg_builtin_shm_progress(ucg_builtin_shm_iface_t *iface,
+                                      ucg_builtin_am_cb_f cb, void *arg);
+/* Blocking barrier of all members (set-up / tear-down only). */
+void         ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *iface);
+
+/* ---- f1: group and collective engine ------------------------------------ */
+typedef struct ucg_builtin_lgroup ucg_builtin_lgroup_t;
+typedef struct ucg_builtin_lcoll  ucg_builtin_lcoll_t;
+
+/* group_id must be non-zero (builtin_control.c:645); `combine` is the
+ * per-group combine state and stays owned by the caller. */
+ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
+                                       uint16_t group_id, unsigned member_count,
+                                       unsigned my_index,
+                                       ucg_builtin_combine_t *combine,
+                                       ucg_builtin_lgroup_t **group_p);
+void         ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *group);
+/* Progress the transport and any pending resends of this group's ops. */
+unsigned     ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *group);
+
+/* MPI_Allreduce (modifiers AGGREGATE|BROADCAST, api/ucg_mpi.h:53-54) on the
+ * recursive-doubling plan: member_count must be a power of two (otherwise
+ * UCS_ERR_UNSUPPORTED, as builtin_recursive.c:78-88 for inter-node groups).
+ * sbuf == rbuf means in place. The op is reusable (persistent). */
+ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *group,
+                                         const void *sbuf, void *rbuf,
+                                         int count, void *dtype, void *op,
+                                         ucg_builtin_lcoll_t **coll_p);
+/* ucg_collective_start: UCS_OK if complete, UCS_INPROGRESS, or an error */
+ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *coll);
+/* 1 when the last start completed; its status in *status */
+int          ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *coll,
+                                    ucs_status_t *status);
+/* Progress until complete (or error); returns the final status. */
+ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *coll);
+void         ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *coll);
+/* The plan as the builtin planner's print (builtin/builtin.c:750-901):
+ * steps, peers, fragment length and count. Returns bytes written. */
+size_t       ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *coll, char *buf,
+                                        size_t max);
+/* [0] messages sent, [1] messages received directly, [2] stashed,
+ * [3] resends after UCS_ERR_NO_RESOURCE */
+void         ucg_builtin_lgroup_stats(ucg_builtin_lgroup_t *group,
+                                      uint64_t out[4]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -18,6 +18,11 @@ def free_port():
 
 
 def launch(worker, world, args=(), timeout=240):
+    return launch_exe(os.path.join(ROOT, "tests", worker), world, args, timeout,
+                      python=True)
+
+
+def launch_exe(exe, world, args=(), timeout=240, python=False):
     port = free_port()
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
@@ -28,8 +33,8 @@ def launch(worker, world, args=(), timeout=240):
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", worker),
-                                       *map(str, args)], env=e, stdout=subprocess.PIPE,
+        cmd = ([sys.executable] if python else []) + [exe, *map(str, args)]
+        procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     outs, codes = [], []
     for p in procs:

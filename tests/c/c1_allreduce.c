@@ -1,0 +1,125 @@
+/*
+ * c1_allreduce.c - BASELINE config 1: an N-process loopback allreduce of
+ * 4 KiB fp32 SUM through the builtin operation engine (libucg_builtin.so)
+ * over the shared-memory transport, combine on the host callback.
+ *
+ *   RANK=r WORLD_SIZE=n c1_allreduce <shm-name> [iters] [max_short] [count]
+ *
+ * The "MPI library" behind reduce_cb_f is a plain C loop with MPI's operand
+ * order (inoutvec[i] = invec[i] + inoutvec[i]); inputs are exact integers so
+ * its NaN handling never matters. The result of every member is checked bit
+ * for bit against the oracle's simulation of the reference plan
+ * (oracle/combine_ref.c, test infrastructure). Member 0 prints one JSON line.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "ucg_builtin_ops.h"
+#include "combine_ref.h"
+
+static int mini_reduce(void *op, char *src, char *dst, unsigned count, void *dt)
+{
+    const float *s = (const float*)src;
+    float *d = (float*)dst;
+    unsigned i;
+    (void)op;
+    (void)dt;
+    for (i = 0; i < count; i++) {
+        d[i] = s[i] + d[i];
+    }
+    return 0;
+}
+
+static int is_sum(void *op) { (void)op; return 1; }
+static int no(void *op) { (void)op; return 0; }
+static int yes(void *op) { (void)op; return 1; }
+static int convert(void *dt, uintptr_t *u) { (void)dt; *u = 4u << 3; return 0; }
+static int is_int(void *dt, int *s) { (void)dt; *s = 0; return 0; }
+static int is_fp(void *dt) { (void)dt; return 1; }
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+int main(int argc, char **argv)
+{
+    const char *name = argc > 1 ? argv[1] : "ucg_c1";
+    int iters        = argc > 2 ? atoi(argv[2]) : 10000;
+    size_t max_short = argc > 3 ? (size_t)atol(argv[3]) : 256;
+    int count        = argc > 4 ? atoi(argv[4]) : 1024;
+    unsigned rank    = (unsigned)atoi(getenv("RANK") ? getenv("RANK") : "0");
+    unsigned world   = (unsigned)atoi(getenv("WORLD_SIZE") ? getenv("WORLD_SIZE") : "1");
+    ucg_builtin_reduce_params_t rp = {mini_reduce, is_sum, no, yes, convert,
+                                      is_int, is_fp};
+    ucg_builtin_combine_config_t cfg = {0, 1u << 20, 8u << 20, 4, -1};
+    ucg_builtin_combine_t *cmb;
+    ucg_builtin_shm_iface_t *iface;
+    ucg_builtin_lgroup_t *g;
+    ucg_builtin_lcoll_t *c;
+    float **inputs, *out, *want;
+    unsigned r;
+    int i, ok;
+    double t0, us;
+
+    if (ucg_builtin_combine_create(&rp, &cfg, &cmb) != UCS_OK ||
+        ucg_builtin_shm_iface_open(name, world, rank, max_short, 64, &iface) != UCS_OK ||
+        ucg_builtin_lgroup_create(iface, 1, world, rank, cmb, &g) != UCS_OK) {
+        fprintf(stderr, "rank %u: set-up failed\n", rank);
+        return 1;
+    }
+    inputs = calloc(world, sizeof(*inputs));
+    for (r = 0; r < world; r++) {
+        inputs[r] = malloc(count * sizeof(float));
+        ucg_oracle_fill(ORA_F32, ORA_DIST_EXACT, 0xC1000 + r, inputs[r], count);
+    }
+    out  = calloc(count, sizeof(float));
+    want = calloc(count, sizeof(float));
+    ucg_oracle_reduce_multi(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
+                            world, rank, count);
+    if (ucg_builtin_lcoll_allreduce(g, inputs[rank], out, count, (void*)1,
+                                    (void*)1, &c) != UCS_OK) {
+        fprintf(stderr, "rank %u: allreduce create failed\n", rank);
+        return 1;
+    }
+    for (i = 0; i < 100; i++) {        /* warm-up */
+        if (ucg_builtin_lcoll_start(c) == UCS_INPROGRESS) {
+            ucg_builtin_lcoll_wait(c);
+        }
+    }
+    ucg_builtin_shm_barrier(iface);
+    t0 = now_s();
+    for (i = 0; i < iters; i++) {
+        ucs_status_t st = ucg_builtin_lcoll_start(c);
+        if (st == UCS_INPROGRESS) {
+            st = ucg_builtin_lcoll_wait(c);
+        }
+        if (st != UCS_OK) {
+            fprintf(stderr, "rank %u: allreduce failed %d\n", rank, st);
+            return 1;
+        }
+    }
+    us = (now_s() - t0) / iters * 1e6;
+    ok = memcmp(out, want, count * sizeof(float)) == 0;
+    ucg_builtin_shm_barrier(iface);
+    if (rank == 0) {
+        uint64_t st[4];
+        ucg_builtin_lgroup_stats(g, st);
+        printf("{\"config\": \"C1: %u-rank loopback allreduce, %d fp32 SUM\", "
+               "\"ranks\": %u, \"bytes\": %zu, \"max_short\": %zu, "
+               "\"latency_us\": %.3f, \"iters\": %d, \"bit_exact\": %s, "
+               "\"messages_sent\": %llu, \"stashed\": %llu}\n",
+               world, count, world, count * sizeof(float), max_short, us, iters,
+               ok ? "true" : "false", (unsigned long long)st[0],
+               (unsigned long long)st[2]);
+    }
+    ucg_builtin_lcoll_destroy(c);
+    ucg_builtin_lgroup_destroy(g);
+    ucg_builtin_shm_iface_close(iface);
+    ucg_builtin_combine_destroy(cmb);
+    return ok ? 0 : 3;
+}

@@ -30,7 +30,10 @@ UCS_ERR_NO_MEMORY = -4
 UCS_ERR_INVALID_PARAM = -5
 UCS_ERR_NOT_IMPLEMENTED = -8
 UCS_ERR_NO_DEVICE = -14
+UCS_ERR_BUSY = -15
+UCS_ERR_CANCELED = -16
 UCS_ERR_OUT_OF_RANGE = -19
+UCS_ERR_TIMED_OUT = -20
 UCS_ERR_UNSUPPORTED = -22
 IPC_HANDLE_BYTES = 80  # UCG_BUILTIN_DEV_IPC_HANDLE_BYTES
 

@@ -194,6 +194,11 @@ static size_t dtype_length(ucg_builtin_combine_t *cmb, void *datatype)
     return contig_dt_length(ucp_dt);
 }
 
+size_t ucg_builtin_combine_dtype_length(ucg_builtin_combine_t *cmb, void *datatype)
+{
+    return cmb ? dtype_length(cmb, datatype) : 0;
+}
+
 int ucg_builtin_combine_classify(ucg_builtin_combine_t *cmb, void *reduce_op,
                                  void *datatype, ucg_dev_op_t *op_out,
                                  ucg_dev_dtype_t *dt_out)

@@ -1,0 +1,753 @@
+/*
+ * builtin_ops.c - the builtin planner's operation engine around the combine
+ * and a minimal shared-memory AM transport (include/ucg_builtin_ops.h).
+ *
+ * This is a C restatement of the receive/step machinery of the reference's
+ * builtin/ops for the REDUCE_RECURSIVE method (see the header for file:line
+ * anchors), written against this build's combine dispatcher instead of a
+ * direct reduce_cb_f call. It is what lets the reference's allreduce plan run
+ * end to end between processes with no UCX underneath.
+ */
+#define _GNU_SOURCE
+#include "ucg_builtin_ops.h"
+
+#include <fcntl.h>
+#include <sched.h>
+#include <stdatomic.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+/* ======================================================================== */
+/* f2: shared-memory AM transport                                           */
+/* ======================================================================== */
+typedef struct {
+    _Alignas(64) _Atomic uint64_t head;   /* producer index */
+    _Alignas(64) _Atomic uint64_t tail;   /* consumer index */
+} ring_ctl_t;
+
+typedef struct {
+    uint32_t length;    /* payload bytes (without the header) */
+    uint32_t reserved;
+    uint64_t header;    /* followed by the payload: data = &header */
+} cell_t;
+
+#define SEG_CTL_BYTES 128
+#define UNEXP_GROUPS  64
+
+typedef struct stash {
+    struct stash *next;
+    uint64_t      header;
+    size_t        length;  /* payload bytes */
+    uint8_t       data[];
+} stash_t;
+
+struct ucg_builtin_shm_iface {
+    char      name[256];
+    unsigned  members;
+    unsigned  my;
+    size_t    max_short;
+    size_t    cell_size;
+    unsigned  cells;
+    size_t    ring_bytes;
+    size_t    seg_bytes;
+    char     *seg;
+    uint64_t  barrier_gen;
+    /* ops layer: groups by id and messages for groups not created yet
+     * (the reference's bctx->group_by_id / bctx->unexpected, builtin.c:
+     * 150-205) */
+    ucg_builtin_lgroup_t *groups[UNEXP_GROUPS];
+    stash_t  *unexpected;
+};
+
+static ring_ctl_t *ring_ctl(ucg_builtin_shm_iface_t *it, unsigned src, unsigned dst)
+{
+    return (ring_ctl_t*)(it->seg + SEG_CTL_BYTES +
+                         ((size_t)src * it->members + dst) * it->ring_bytes);
+}
+
+static cell_t *ring_cell(ucg_builtin_shm_iface_t *it, ring_ctl_t *r, uint64_t idx)
+{
+    return (cell_t*)((char*)r + sizeof(ring_ctl_t) + (idx % it->cells) * it->cell_size);
+}
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static double wait_timeout_s(void)
+{
+    const char *t = getenv("UCX_BUILTIN_WAIT_TIMEOUT");
+    return t ? atof(t) : 300.0;
+}
+
+ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
+                                        unsigned my_index, size_t max_short,
+                                        unsigned ring_cells,
+                                        ucg_builtin_shm_iface_t **iface_p)
+{
+    ucg_builtin_shm_iface_t *it;
+    int fd;
+    struct stat stt;
+
+    if (name == NULL || iface_p == NULL || members == 0 ||
+        members > UCG_BUILTIN_OPS_MAX_MEMBERS || my_index >= members ||
+        max_short <= 8 || max_short > (1u << 20) || ring_cells < 2) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    it = calloc(1, sizeof(*it));
+    if (it == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    snprintf(it->name, sizeof(it->name), "/%s", name[0] == '/' ? name + 1 : name);
+    it->members    = members;
+    it->my         = my_index;
+    it->max_short  = max_short;
+    it->cells      = ring_cells;
+    it->cell_size  = (sizeof(cell_t) + (max_short - 8) + 63) & ~(size_t)63;
+    it->ring_bytes = sizeof(ring_ctl_t) + (size_t)ring_cells * it->cell_size;
+    it->seg_bytes  = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
+
+    fd = shm_open(it->name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) {
+        free(it);
+        return UCS_ERR_IO_ERROR;
+    }
+    /* a fresh object is zero-filled: every ring starts empty (head = tail) */
+    if (fstat(fd, &stt) != 0 ||
+        ((size_t)stt.st_size < it->seg_bytes && ftruncate(fd, it->seg_bytes) != 0)) {
+        close(fd);
+        free(it);
+        return UCS_ERR_IO_ERROR;
+    }
+    it->seg = mmap(NULL, it->seg_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (it->seg == MAP_FAILED) {
+        free(it);
+        return UCS_ERR_NO_MEMORY;
+    }
+    ucg_builtin_shm_barrier(it);   /* everybody mapped before any send */
+    *iface_p = it;
+    return UCS_OK;
+}
+
+void ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *it)
+{
+    stash_t *m;
+    if (it == NULL) {
+        return;
+    }
+    ucg_builtin_shm_barrier(it);
+    munmap(it->seg, it->seg_bytes);
+    if (it->my == 0) {
+        shm_unlink(it->name);
+    }
+    while ((m = it->unexpected) != NULL) {
+        it->unexpected = m->next;
+        free(m);
+    }
+    free(it);
+}
+
+size_t ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *it)
+{
+    return it ? it->max_short : 0;
+}
+
+void ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
+{
+    _Atomic uint64_t *arrive = (_Atomic uint64_t*)it->seg;
+    uint64_t gen = ++it->barrier_gen;
+    double t0 = now_s(), lim = wait_timeout_s();
+    atomic_fetch_add_explicit(arrive, 1, memory_order_acq_rel);
+    while (atomic_load_explicit(arrive, memory_order_acquire) < gen * it->members) {
+        if (now_s() - t0 > lim) {
+            fprintf(stderr, "ucg_builtin_shm_barrier(%s): timed out after %.0f s\n",
+                    it->name, lim);
+            abort();
+        }
+        sched_yield();
+    }
+}
+
+ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *it, unsigned peer,
+                                      uint64_t header, const void *payload,
+                                      size_t length)
+{
+    ring_ctl_t *r;
+    uint64_t head, tail;
+    cell_t *c;
+
+    if (peer >= it->members || peer == it->my) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (length + 8 > it->max_short) {
+        return UCS_ERR_INVALID_PARAM;   /* UCS_ERR_MESSAGE_TRUNCATED in UCT */
+    }
+    r    = ring_ctl(it, it->my, peer);
+    head = atomic_load_explicit(&r->head, memory_order_relaxed);
+    tail = atomic_load_explicit(&r->tail, memory_order_acquire);
+    if (head - tail >= it->cells) {
+        return UCS_ERR_NO_RESOURCE;
+    }
+    c = ring_cell(it, r, head);
+    c->length = (uint32_t)length;
+    c->header = header;
+    if (length) {
+        memcpy(c + 1, payload, length);
+    }
+    atomic_store_explicit(&r->head, head + 1, memory_order_release);
+    return UCS_OK;
+}
+
+unsigned ucg_builtin_shm_progress(ucg_builtin_shm_iface_t *it,
+                                  ucg_builtin_am_cb_f cb, void *arg)
+{
+    unsigned src, n = 0;
+    for (src = 0; src < it->members; src++) {
+        ring_ctl_t *r;
+        uint64_t tail, head;
+        if (src == it->my) {
+            continue;
+        }
+        r    = ring_ctl(it, src, it->my);
+        tail = atomic_load_explicit(&r->tail, memory_order_relaxed);
+        head = atomic_load_explicit(&r->head, memory_order_acquire);
+        while (tail < head) {
+            cell_t *c = ring_cell(it, r, tail);
+            (void)cb(arg, &c->header, 8 + (size_t)c->length);
+            tail++;
+            /* the cell is free only after the callback returned */
+            atomic_store_explicit(&r->tail, tail, memory_order_release);
+            n++;
+        }
+    }
+    return n;
+}
+
+/* ======================================================================== */
+/* f1: the builtin operation engine                                         */
+/* ======================================================================== */
+
+/* builtin/ops/builtin_ops.h:45-60 */
+typedef union {
+    struct {
+        uint16_t group_id;
+        union {
+            struct {
+                uint8_t coll_id;
+                uint8_t step_idx;
+            };
+            uint16_t local_id;
+        };
+        uint32_t remote_offset;
+    };
+    uint64_t header;
+} ops_header_t;
+
+_Static_assert(sizeof(ops_header_t) == 8, "wire header is 8 bytes");
+
+#define OPS_MAX_STEPS 8
+
+typedef struct {
+    unsigned    peer;             /* one endpoint per step (factor 2) */
+    uint8_t     step_idx;         /* phase->step_index, 1-based */
+    const char *send_buffer;
+    size_t      frag_len;         /* 0: single message */
+    uint64_t    fragments_total;  /* ep_cnt x fragments */
+} op_step_t;
+
+typedef struct {
+    ucg_builtin_lcoll_t *req;     /* the op running in this slot */
+    uint16_t             expecting;
+    stash_t             *msgs;    /* slot->messages */
+} op_slot_t;
+
+struct ucg_builtin_lgroup {
+    ucg_builtin_shm_iface_t *iface;
+    uint16_t                 group_id;
+    unsigned                 size;
+    unsigned                 my;
+    ucg_builtin_combine_t   *cmb;
+    op_slot_t                slots[UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    uint8_t                  next_coll_id;
+    uint64_t                 stats[4];
+};
+
+struct ucg_builtin_lcoll {
+    ucg_builtin_lgroup_t *g;
+    const char  *sbuf;
+    char        *rbuf;
+    int          count;
+    void        *dtype;
+    void        *op;
+    size_t       dt_len;
+    size_t       length;
+    op_step_t    steps[OPS_MAX_STEPS];
+    unsigned     nsteps;
+    /* request state (builtin_ops.h:233-241) */
+    int          active;
+    int          done;
+    ucs_status_t status;
+    uint8_t      coll_id;
+    unsigned     cur;
+    uint64_t     pending;
+    int          step_open;
+    int          send_pending;
+    size_t       iter_offset;
+};
+
+static int  recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
+                    size_t length);
+static void step_execute(ucg_builtin_lcoll_t *c);
+
+static stash_t *stash_new(uint64_t header, const void *payload, size_t length)
+{
+    stash_t *m = malloc(sizeof(*m) + length);
+    if (m) {
+        m->next   = NULL;
+        m->header = header;
+        m->length = length;
+        memcpy(m->data, payload, length);
+    }
+    return m;
+}
+
+static void stash_append(stash_t **list, stash_t *m)
+{
+    while (*list) {
+        list = &(*list)->next;
+    }
+    *list = m;
+}
+
+/* finish the op: ucg_builtin_comp_last_step_cb, builtin_comp_step.inl:8-38 */
+static void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
+{
+    op_slot_t *slot = &c->g->slots[c->coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    if (c->step_open) {
+        ucs_status_t st = ucg_builtin_combine_step_end(c->g->cmb);
+        if (status == UCS_OK) {
+            status = st;
+        }
+        c->step_open = 0;
+    }
+    c->status       = status;
+    c->done         = 1;
+    c->active       = 0;
+    c->send_pending = 0;
+    slot->req       = NULL;
+    slot->expecting = 0;
+}
+
+/* ucg_builtin_step_check_pending, builtin_comp_step.inl:403-462 */
+static void check_pending(ucg_builtin_lcoll_t *c, uint16_t local_id)
+{
+    op_slot_t *slot = &c->g->slots[c->coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    slot->expecting = local_id;
+    for (;;) {
+        stash_t **pp = &slot->msgs, *m;
+        while (*pp) {
+            ops_header_t h;
+            h.header = (*pp)->header;
+            if (h.local_id == local_id) {
+                break;
+            }
+            pp = &(*pp)->next;
+        }
+        if ((m = *pp) == NULL) {
+            return;
+        }
+        *pp = m->next;   /* remove first: the next call may recurse here */
+        ops_header_t h;
+        h.header = m->header;
+        int step_done = recv_cb(c, h.remote_offset, m->data, m->length);
+        free(m);
+        if (step_done) {
+            return;      /* the next step (if any) drained its own messages */
+        }
+    }
+}
+
+/* ucg_builtin_step_execute (REDUCE_RECURSIVE: send, then receive),
+ * builtin_data.c:584-668 with ucg_builtin_step_am_short_max :83-137 */
+static void step_execute(ucg_builtin_lcoll_t *c)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    op_step_t *s = &c->steps[c->cur];
+    ops_header_t h;
+    ucs_status_t st;
+
+    if (!c->step_open) {
+        st = ucg_builtin_combine_step_begin(g->cmb, c->op, c->dtype, c->rbuf,
+                                            c->length);
+        if (st != UCS_OK) {
+            finish(c, st);
+            return;
+        }
+        c->step_open   = 1;
+        c->pending     = s->fragments_total;
+        c->iter_offset = 0;
+    }
+    h.header        = 0;
+    h.group_id      = g->group_id;
+    h.coll_id       = c->coll_id;
+    h.step_idx      = s->step_idx;
+    if (s->frag_len == 0) {
+        if (c->iter_offset == 0) {
+            h.remote_offset = 0;
+            st = ucg_builtin_shm_am_short(g->iface, s->peer, h.header,
+                                          s->send_buffer, c->length);
+            if (st == UCS_ERR_NO_RESOURCE) {
+                c->send_pending = 1;      /* ucg_builtin_req_enqueue_resend */
+                return;
+            }
+            if (st != UCS_OK) {
+                finish(c, st);
+                return;
+            }
+            g->stats[0]++;
+            c->iter_offset = c->length ? c->length : 1;
+        }
+    } else {
+        while (c->iter_offset < c->length) {
+            size_t n = c->length - c->iter_offset;
+            if (n > s->frag_len) {
+                n = s->frag_len;
+            }
+            h.remote_offset = (uint32_t)c->iter_offset;
+            st = ucg_builtin_shm_am_short(g->iface, s->peer, h.header,
+                                          s->send_buffer + c->iter_offset, n);
+            if (st == UCS_ERR_NO_RESOURCE) {
+                c->send_pending = 1;
+                return;
+            }
+            if (st != UCS_OK) {
+                finish(c, st);
+                return;
+            }
+            g->stats[0]++;
+            c->iter_offset += n;
+        }
+    }
+    c->send_pending = 0;
+    check_pending(c, h.local_id);
+}
+
+/* ucg_builtin_step_recv_cb -> handle_data (REDUCE) + handle_comp,
+ * builtin_comp_step.inl:184-232, 314-401; returns 1 when the step is done */
+static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
+                   size_t length)
+{
+    ucs_status_t st = ucg_builtin_combine_fragment(c->g->cmb, offset, data, length);
+    if (st != UCS_OK) {
+        finish(c, st);      /* recv_handle_error, :332-333 */
+        return 1;
+    }
+    if (--c->pending != 0) {
+        return 0;
+    }
+    /* the step is complete: the device mirror goes back to recv_buffer
+     * before the next step sends it (builtin_control.c:850-857) */
+    st = ucg_builtin_combine_step_end(c->g->cmb);
+    c->step_open = 0;
+    if (st != UCS_OK) {
+        finish(c, st);
+        return 1;
+    }
+    if (c->cur + 1 == c->nsteps) {
+        finish(c, UCS_OK);
+    } else {
+        c->cur++;
+        step_execute(c);  /* ucg_builtin_comp_step_cb, :60-95 */
+    }
+    return 1;
+}
+
+/* ucg_builtin_am_handler, builtin/builtin.c:133-219 */
+static ucs_status_t am_handler(void *arg, void *data, size_t length)
+{
+    ucg_builtin_shm_iface_t *it = arg;
+    ops_header_t h;
+    ucg_builtin_lgroup_t *g;
+    op_slot_t *slot;
+    stash_t *m;
+
+    memcpy(&h.header, data, 8);
+    g = it->groups[h.group_id % UNEXP_GROUPS];
+    if (g == NULL || g->group_id != h.group_id) {
+        m = stash_new(h.header, (char*)data + 8, length - 8);
+        if (m) {
+            stash_append(&it->unexpected, m);
+        }
+        return UCS_OK;
+    }
+    slot = &g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    if (slot->req && h.local_id == slot->expecting) {
+        g->stats[1]++;
+        (void)recv_cb(slot->req, h.remote_offset, (char*)data + 8, length - 8);
+        return UCS_OK;
+    }
+    g->stats[2]++;
+    m = stash_new(h.header, (char*)data + 8, length - 8);
+    if (m == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    stash_append(&slot->msgs, m);
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
+                                       uint16_t group_id, unsigned member_count,
+                                       unsigned my_index,
+                                       ucg_builtin_combine_t *combine,
+                                       ucg_builtin_lgroup_t **group_p)
+{
+    ucg_builtin_lgroup_t *g;
+    stash_t **pp;
+
+    if (iface == NULL || group_p == NULL || combine == NULL || group_id == 0 ||
+        member_count != iface->members || my_index != iface->my) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (iface->groups[group_id % UNEXP_GROUPS] != NULL) {
+        return UCS_ERR_BUSY;
+    }
+    g = calloc(1, sizeof(*g));
+    if (g == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    g->iface    = iface;
+    g->group_id = group_id;
+    g->size     = member_count;
+    g->my       = my_index;
+    g->cmb      = combine;
+    iface->groups[group_id % UNEXP_GROUPS] = g;
+    /* adopt messages that arrived before the group existed (builtin.c:
+     * 424-446) */
+    pp = &iface->unexpected;
+    while (*pp) {
+        ops_header_t h;
+        h.header = (*pp)->header;
+        if (h.group_id == group_id) {
+            stash_t *m = *pp;
+            *pp = m->next;
+            m->next = NULL;
+            stash_append(&g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT].msgs, m);
+        } else {
+            pp = &(*pp)->next;
+        }
+    }
+    *group_p = g;
+    return UCS_OK;
+}
+
+void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
+{
+    unsigned i;
+    if (g == NULL) {
+        return;
+    }
+    for (i = 0; i < UCG_BUILTIN_OPS_MAX_CONCURRENT; i++) {
+        stash_t *m;
+        while ((m = g->slots[i].msgs) != NULL) {
+            g->slots[i].msgs = m->next;
+            free(m);
+        }
+    }
+    g->iface->groups[g->group_id % UNEXP_GROUPS] = NULL;
+    free(g);
+}
+
+unsigned ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *g)
+{
+    unsigned n = ucg_builtin_shm_progress(g->iface, am_handler, g->iface), i;
+    /* resend queue (builtin.c:260-294, 329-337) */
+    for (i = 0; i < UCG_BUILTIN_OPS_MAX_CONCURRENT; i++) {
+        ucg_builtin_lcoll_t *c = g->slots[i].req;
+        if (c && c->send_pending) {
+            g->stats[3]++;
+            step_execute(c);
+            n++;
+        }
+    }
+    return n;
+}
+
+void ucg_builtin_lgroup_stats(ucg_builtin_lgroup_t *g, uint64_t out[4])
+{
+    int i;
+    for (i = 0; i < 4; i++) {
+        out[i] = g ? g->stats[i] : 0;
+    }
+}
+
+ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                         void *rbuf, int count, void *dtype,
+                                         void *op, ucg_builtin_lcoll_t **coll_p)
+{
+    ucg_builtin_lcoll_t *c;
+    unsigned steps, k;
+    size_t max_payload;
+
+    if (g == NULL || coll_p == NULL || rbuf == NULL || count < 0 ||
+        (count && sbuf == NULL)) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    steps = ucg_builtin_recursive_steps(g->size, 2);
+    if (g->size > 1 && steps == 0) {
+        return UCS_ERR_UNSUPPORTED;   /* needs the tree plan (next row, f3) */
+    }
+    if (steps > OPS_MAX_STEPS) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    c = calloc(1, sizeof(*c));
+    if (c == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    c->g      = g;
+    c->sbuf   = sbuf;
+    c->rbuf   = rbuf;
+    c->count  = count;
+    c->dtype  = dtype;
+    c->op     = op;
+    c->dt_len = ucg_builtin_combine_dtype_length(g->cmb, dtype);
+    if (c->dt_len == 0) {
+        free(c);
+        return UCS_ERR_INVALID_PARAM;
+    }
+    c->length   = (size_t)count * c->dt_len;
+    c->nsteps   = steps;
+    max_payload = ucg_builtin_shm_iface_max_short(g->iface) - 8;
+    if (c->length * g->size > 0xffffffffull) {
+        free(c);
+        return UCS_ERR_UNSUPPORTED;   /* 32-bit remote_offset, SURVEY 7 (ix) */
+    }
+    for (k = 0; k < steps; k++) {
+        op_step_t *s = &c->steps[k];
+        s->peer     = (unsigned)ucg_builtin_recursive_peer(g->my, k + 1, 2, 1);
+        s->step_idx = (uint8_t)(k + 1);
+        /* step 1 sends the send buffer, later steps the accumulator
+         * (builtin_control.c:660-671, 850-857) */
+        s->send_buffer = (k == 0) ? (const char*)sbuf : (const char*)rbuf;
+        if (c->length > max_payload) {
+            s->frag_len = ucg_builtin_step_fragment_length(
+                              ucg_builtin_shm_iface_max_short(g->iface), c->dt_len);
+            if (s->frag_len == 0) {
+                free(c);
+                return UCS_ERR_UNSUPPORTED;
+            }
+            s->fragments_total = ucg_builtin_step_fragments_total(c->length,
+                                                                  s->frag_len, 1);
+        } else {
+            s->frag_len        = 0;
+            s->fragments_total = 1;
+        }
+    }
+    c->done   = 1;
+    c->status = UCS_OK;
+    *coll_p   = c;
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *c)
+{
+    ucg_builtin_lgroup_t *g;
+    op_slot_t *slot;
+
+    if (c == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (c->active) {
+        return UCS_ERR_BUSY;
+    }
+    g = c->g;
+    c->coll_id = g->next_coll_id;
+    slot = &g->slots[c->coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    if (slot->req != NULL) {
+        return UCS_ERR_BUSY;    /* more than 16 ops outstanding */
+    }
+    g->next_coll_id++;          /* ucg_collective_trigger, base/ucg_group.c:485 */
+    /* ucg_builtin_init_reduce: recv <- send (in place: nothing to copy) */
+    if (c->rbuf != c->sbuf && c->length) {
+        memcpy(c->rbuf, c->sbuf, c->length);
+    }
+    c->done         = 0;
+    c->status       = UCS_INPROGRESS;
+    c->cur          = 0;
+    c->step_open    = 0;
+    c->send_pending = 0;
+    if (c->nsteps == 0 || c->length == 0) {
+        c->done   = 1;
+        c->status = UCS_OK;
+        return UCS_OK;
+    }
+    c->active = 1;
+    slot->req = c;
+    step_execute(c);
+    return c->done ? c->status : UCS_INPROGRESS;
+}
+
+int ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *c, ucs_status_t *status)
+{
+    if (c->done && status) {
+        *status = c->status;
+    }
+    return c->done;
+}
+
+ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
+{
+    double t0 = now_s(), lim = wait_timeout_s();
+    while (!c->done) {
+        if (ucg_builtin_lgroup_progress(c->g) == 0) {
+            if (now_s() - t0 > lim) {
+                finish(c, UCS_ERR_TIMED_OUT);
+                break;
+            }
+            sched_yield();
+        }
+    }
+    return c->status;
+}
+
+void ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *c)
+{
+    if (c && c->active) {
+        finish(c, UCS_ERR_CANCELED);
+    }
+    free(c);
+}
+
+size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
+{
+    size_t w = 0;
+    unsigned k;
+    if (c == NULL || buf == NULL || max == 0) {
+        return 0;
+    }
+#define PUT(...) do {                                                         \
+        int _r = snprintf(buf + w, w < max ? max - w : 0, __VA_ARGS__);       \
+        if (_r > 0) w += (size_t)_r;                                          \
+    } while (0)
+    PUT("Planner: builtin (recursive doubling), member %u of %u\n", c->g->my,
+        c->g->size);
+    PUT("Phases: %u\n", c->nsteps);
+    for (k = 0; k < c->nsteps; k++) {
+        const op_step_t *s = &c->steps[k];
+        PUT("Step #%u (step_idx %u): Reduce (R) with peer %u, send %s, "
+            "fragment length %zu, fragments total %llu, aggregation reduce\n",
+            k, (unsigned)s->step_idx, s->peer, k == 0 ? "send.buffer" : "recv.buffer",
+            s->frag_len ? s->frag_len : c->length,
+            (unsigned long long)s->fragments_total);
+    }
+#undef PUT
+    return w < max ? w : max - 1;
+}

@@ -49,4 +49,25 @@ HOST_API = {
     "ucg_builtin_dev_chunk_bytes": (_sz, [_sz, _sz, _sz]),
     "ucg_builtin_recursive_steps": (_u, [_u64, _u]),
     "ucg_builtin_recursive_peer": (_u64, [_u64, _u, _u, _u]),
+    "ucg_builtin_combine_dtype_length": (_sz, [_vp, _vp]),
+    # include/ucg_builtin_ops.h
+    "ucg_builtin_shm_iface_open": (_int, [ctypes.c_char_p, _u, _u, _sz, _u,
+                                          ctypes.POINTER(_vp)]),
+    "ucg_builtin_shm_iface_close": (None, [_vp]),
+    "ucg_builtin_shm_iface_max_short": (_sz, [_vp]),
+    "ucg_builtin_shm_am_short": (_int, [_vp, _u, _u64, _vp, _sz]),
+    "ucg_builtin_shm_progress": (_u, [_vp, _vp, _vp]),
+    "ucg_builtin_shm_barrier": (None, [_vp]),
+    "ucg_builtin_lgroup_create": (_int, [_vp, ctypes.c_uint16, _u, _u, _vp,
+                                         ctypes.POINTER(_vp)]),
+    "ucg_builtin_lgroup_destroy": (None, [_vp]),
+    "ucg_builtin_lgroup_progress": (_u, [_vp]),
+    "ucg_builtin_lgroup_stats": (None, [_vp, ctypes.POINTER(_u64)]),
+    "ucg_builtin_lcoll_allreduce": (_int, [_vp, _vp, _vp, _int, _vp, _vp,
+                                           ctypes.POINTER(_vp)]),
+    "ucg_builtin_lcoll_start": (_int, [_vp]),
+    "ucg_builtin_lcoll_test": (_int, [_vp, ctypes.POINTER(_int)]),
+    "ucg_builtin_lcoll_wait": (_int, [_vp]),
+    "ucg_builtin_lcoll_destroy": (None, [_vp]),
+    "ucg_builtin_lcoll_describe": (_sz, [_vp, ctypes.c_char_p, _sz]),
 }
