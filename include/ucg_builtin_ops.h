@@ -18,7 +18,12 @@
  *                  builtin/ops/builtin_comp_step.inl:403-462
  *   completion     pending = ep_cnt x fragments, next step or finish,
  *                  builtin/ops/builtin_comp_step.inl:8-95,342-401
- *   plan           recursive doubling, builtin/plan/builtin_recursive.c:20-228
+ *   plans          recursive doubling, builtin/plan/builtin_recursive.c:20-228;
+ *                  tree fan-in / fan-out (single host: flat, root = parent of
+ *                  all), builtin/plan/builtin_tree.c:86-380; the choice,
+ *                  builtin/builtin.c:95-121
+ *   aggregation    REDUCE for REDUCE_TERMINAL/RECURSIVE, WRITE for the
+ *                  fan-out receive, builtin/ops/builtin_control.c:960-972
  *   fragments      builtin/ops/builtin_control.c:434,462-465
  *   seeding        ucg_builtin_init_reduce, builtin/ops/builtin_control.c:43-47
  *
@@ -80,14 +85,23 @@ void         ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *group);
 /* Progress the transport and any pending resends of this group's ops. */
 unsigned     ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *group);
 
-/* MPI_Allreduce (modifiers AGGREGATE|BROADCAST, api/ucg_mpi.h:53-54) on the
- * recursive-doubling plan: member_count must be a power of two (otherwise
- * UCS_ERR_UNSUPPORTED, as builtin_recursive.c:78-88 for inter-node groups).
- * sbuf == rbuf means in place. The op is reusable (persistent). */
+/* MPI_Allreduce (modifiers AGGREGATE|BROADCAST, api/ucg_mpi.h:53-54):
+ * recursive doubling when member_count is a power of two, otherwise the tree
+ * fan-in to member 0 followed by its fan-out (ucg_builtin_choose_topology,
+ * builtin/builtin.c:112-121; UCX_BUILTIN_ALLREDUCE_PLAN=tree|recursive
+ * overrides, a knob of this build). sbuf == rbuf means in place. The op is
+ * reusable (persistent). */
 ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *group,
                                          const void *sbuf, void *rbuf,
                                          int count, void *dtype, void *op,
                                          ucg_builtin_lcoll_t **coll_p);
+/* MPI_Reduce (AGGREGATE|SINGLE_DESTINATION, api/ucg_mpi.h:41-42, 156): fan-in to
+ * `root`, whose rbuf receives the result; rbuf is not touched (may be NULL)
+ * on the other members. */
+ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *group,
+                                      const void *sbuf, void *rbuf,
+                                      int count, void *dtype, void *op,
+                                      unsigned root, ucg_builtin_lcoll_t **coll_p);
 /* ucg_collective_start: UCS_OK if complete, UCS_INPROGRESS, or an error */
 ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *coll);
 /* 1 when the last start completed; its status in *status */

@@ -324,6 +324,57 @@ uint64_t ucg_oracle_recursive_peer(uint64_t my, unsigned step)
     return base + ((my - base + step_size) % (step_size * 2));
 }
 
+int ucg_oracle_tree_reduce(int op, int dt, void *dst, const void *const *srcs,
+                           unsigned nsrc, unsigned root, const unsigned *order,
+                           size_t count)
+{
+    size_t sz = ucg_oracle_dtype_size(dt);
+    unsigned i, k = 0;
+    if (sz == 0 || nsrc == 0 || root >= nsrc || !ucg_oracle_is_supported(dt, op)) {
+        return -1;
+    }
+    memcpy(dst, srcs[root], count * sz);           /* init_reduce */
+    for (i = 0; i + 1 < nsrc; i++) {
+        unsigned child;
+        if (order) {
+            child = order[i];
+        } else {
+            child = (k == root) ? ++k : k;   /* ascending, skipping the root */
+            k++;
+        }
+        if (child >= nsrc || child == root) {
+            return -1;
+        }
+        ucg_oracle_reduce(op, dt, srcs[child], dst, count);
+    }
+    return 0;
+}
+
+int ucg_oracle_tree_intra(unsigned my, unsigned size, unsigned root,
+                          unsigned *up, unsigned *up_cnt,
+                          unsigned *down, unsigned *down_cnt)
+{
+    unsigned m;
+    *up_cnt = *down_cnt = 0;
+    if (my >= size || root >= size) {
+        return -1;
+    }
+    /* every other member is one "HOST" distance away: the first member
+     * before me at that distance is my parent, and only a member with no
+     * parent (master_phase NET) takes children - all members at the first
+     * distance it sees. Relabelled so the root plays member 0. */
+    if (my != root) {
+        up[(*up_cnt)++] = root;
+        return 0;
+    }
+    for (m = 0; m < size; m++) {
+        if (m != root) {
+            down[(*down_cnt)++] = m;
+        }
+    }
+    return 0;
+}
+
 int ucg_oracle_reduce_multi(int op, int dt, void *dst, const void *const *srcs,
                             unsigned nsrc, unsigned self, size_t count)
 {

@@ -56,6 +56,14 @@ def lib():
         L.ucg_oracle_reduce_multi.argtypes = [i, i, vp, ctypes.POINTER(vp),
                                               ctypes.c_uint, ctypes.c_uint, sz]
         L.ucg_oracle_reduce_multi.restype = i
+        L.ucg_oracle_tree_reduce.argtypes = [i, i, vp, ctypes.POINTER(vp), ctypes.c_uint,
+                                             ctypes.c_uint, ctypes.POINTER(ctypes.c_uint),
+                                             sz]
+        L.ucg_oracle_tree_reduce.restype = i
+        pu = ctypes.POINTER(ctypes.c_uint)
+        L.ucg_oracle_tree_intra.argtypes = [ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                            pu, pu, pu, pu]
+        L.ucg_oracle_tree_intra.restype = i
         L.ucg_oracle_fill.argtypes = [i, i, u64, vp, sz]
         L.ucg_oracle_fill.restype = None
         L.ucg_oracle_is_supported.argtypes = [i, i]
@@ -139,6 +147,30 @@ def reduce_multi(op, dt, srcs, self_index):
     if rc != 0:
         raise ValueError("reduce_multi failed")
     return out
+
+
+def tree_reduce(op, dt, srcs, root=0, order=None):
+    """Tree fan-in result at the root: children reduced in `order`
+    (default ascending member index)."""
+    srcs = [np.ascontiguousarray(s, dtype=storage(dt)) for s in srcs]
+    out = np.empty_like(srcs[0])
+    arr = (ctypes.c_void_p * len(srcs))(*[s.ctypes.data for s in srcs])
+    ordp = None
+    if order is not None:
+        ordp = (ctypes.c_uint * len(order))(*order)
+    rc = lib().ucg_oracle_tree_reduce(op_index(op), dt_index(dt), out.ctypes.data,
+                                      arr, len(srcs), root, ordp, out.size)
+    if rc != 0:
+        raise ValueError("tree_reduce failed")
+    return out
+
+
+def tree_intra(my, size, root=0):
+    up, down = (ctypes.c_uint * 64)(), (ctypes.c_uint * 64)()
+    nu, nd = ctypes.c_uint(), ctypes.c_uint()
+    lib().ucg_oracle_tree_intra(my, size, root, up, ctypes.byref(nu), down,
+                                ctypes.byref(nd))
+    return list(up[:nu.value]), list(down[:nd.value])
 
 
 def special_table(dt):

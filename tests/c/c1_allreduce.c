@@ -7,7 +7,8 @@
  *
  * The "MPI library" behind reduce_cb_f is a plain C loop with MPI's operand
  * order (inoutvec[i] = invec[i] + inoutvec[i]); inputs are exact integers so
- * its NaN handling never matters. The result of every member is checked bit
+ * its NaN handling never matters, nor does the tree plan's arrival order
+ * (non-power-of-two worlds). The result of every member is checked bit
  * for bit against the oracle's simulation of the reference plan
  * (oracle/combine_ref.c, test infrastructure). Member 0 prints one JSON line.
  */
@@ -79,8 +80,13 @@ int main(int argc, char **argv)
     }
     out  = calloc(count, sizeof(float));
     want = calloc(count, sizeof(float));
-    ucg_oracle_reduce_multi(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
-                            world, rank, count);
+    if ((world & (world - 1)) == 0 && !getenv("UCX_BUILTIN_ALLREDUCE_PLAN")) {
+        ucg_oracle_reduce_multi(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
+                                world, rank, count);
+    } else {   /* tree plan; exact inputs make the arrival order irrelevant */
+        ucg_oracle_tree_reduce(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
+                               world, 0, NULL, count);
+    }
     if (ucg_builtin_lcoll_allreduce(g, inputs[rank], out, count, (void*)1,
                                     (void*)1, &c) != UCS_OK) {
         fprintf(stderr, "rank %u: allreduce create failed\n", rank);

@@ -29,18 +29,19 @@ def test_allreduce_multiprocess_host(world, max_short, cells):
         print(outs[0])
 
 
-@pytest.mark.parametrize("max_short", [256, 8192])
-def test_c1_harness_bit_exact(max_short):
-    """BASELINE config 1 from plain C: 4 processes, 4 KiB fp32 SUM."""
+@pytest.mark.parametrize("max_short,world", [(256, 4), (8192, 4), (256, 3)])
+def test_c1_harness_bit_exact(max_short, world):
+    """BASELINE config 1 from plain C: 4 processes, 4 KiB fp32 SUM (and the
+    tree plan at 3 processes)."""
     import json
     import subprocess
     exe = os.path.join(os.path.dirname(__file__), "c", "_build", "c1_allreduce")
     if not os.path.exists(exe):
         subprocess.run(["make", "-s", "-C", os.path.dirname(exe) + "/.."], check=True)
-    codes, outs = launch_exe(exe, 4, (shm_name(), 2000, max_short))
-    assert codes == [0] * 4, "\n".join(outs)
+    codes, outs = launch_exe(exe, world, (shm_name(), 2000, max_short))
+    assert codes == [0] * world, "\n".join(outs)
     line = json.loads(outs[0].strip().splitlines()[-1])
-    assert line["bit_exact"] and line["ranks"] == 4 and line["bytes"] == 4096
+    assert line["bit_exact"] and line["ranks"] == world and line["bytes"] == 4096
 
 
 def test_plan_description_and_unsupported_sizes():
@@ -66,3 +67,68 @@ def test_allreduce_multiprocess_device_staging(world):
     codes, outs = launch("_worker_ops.py", world, args=(shm_name(), "dev", 256, 20),
                          timeout=300)
     assert codes == [0] * world, "\n".join(outs)
+
+
+def _digests(outs):
+    per_rank = []
+    for out in outs:
+        per_rank.append(sorted(line for line in out.splitlines() if line.startswith("digest")))
+    return per_rank
+
+
+@pytest.mark.parametrize("world,max_short,cells,plan", [
+    (3, 256, 64, None), (5, 64, 64, None), (6, 8192, 64, None), (7, 256, 2, None),
+    (4, 256, 64, "tree"), (2, 64, 64, "tree")])
+def test_tree_multiprocess_host(world, max_short, cells, plan, monkeypatch):
+    """Tree fan-in / fan-out (builtin_tree.c:86-380): MPI_Reduce to several
+    roots and the non-power-of-two MPI_Allreduce; plan='tree' forces the tree
+    on a power-of-two group (UCX_BUILTIN_ALLREDUCE_PLAN)."""
+    if plan:
+        monkeypatch.setenv("UCX_BUILTIN_ALLREDUCE_PLAN", plan)
+    codes, outs = launch("_worker_tree.py", world, args=(shm_name(), "host", max_short, cells),
+                         timeout=240)
+    assert codes == [0] * world, "\n".join(outs)
+    d = _digests(outs)
+    assert all(x == d[0] for x in d) and d[0], d     # every member holds the root's bits
+    assert "REDUCE_TERMINAL" in outs[0] and "SEND_TERMINAL" in outs[0]
+    assert ("SEND_TERMINAL, send send.buffer to 0" if world == 2 else "SEND_TO_SM_ROOT") in outs[1]
+    assert "RECV_TERMINAL, receive from 0" in outs[1] and "aggregation write" in outs[1]
+
+
+def test_tree_intra_restatement():
+    """The oracle's ucg_builtin_tree_add_intra for one host (all members at
+    DISTANCE_HOST): the root is every other member's only parent. The engine's
+    plans are checked against it member by member in _worker_tree.py."""
+    up, down = O.tree_intra(0, 5)
+    assert up == [] and down == [1, 2, 3, 4]
+    up, down = O.tree_intra(3, 5, root=1)
+    assert up == [1] and down == []
+
+
+def test_allreduce_rejects_bad_reduce_root():
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    iface = ops.ShmIface(shm_name(), 1, 0, max_short=256)
+    g = ops.Group(iface, 3, 1, 0, cmb)
+    x = np.arange(16, dtype=np.int32)
+    y = np.zeros_like(x)
+    assert g.reduce(x, y, 16, DTYPES["int32"], OPS["sum"], root=1).status == -5
+    c = g.reduce(x, y, 16, DTYPES["int32"], OPS["sum"], root=0)
+    assert c.status == 0 and c.run() == 0 and (y == x).all()
+    assert "reduce" in c.describe()
+    c.close()
+    g.close()
+    iface.close()
+    cmb.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [3, 5])
+def test_tree_multiprocess_device_staging(world):
+    """Tree root's fan-in staged on the GPU: children's fragments at the same
+    offsets become separate runs applied in arrival order."""
+    codes, outs = launch("_worker_tree.py", world, args=(shm_name(), "dev", 256),
+                         timeout=300)
+    assert codes == [0] * world, "\n".join(outs)
+    d = _digests(outs)
+    assert all(x == d[0] for x in d), d

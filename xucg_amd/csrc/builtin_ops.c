@@ -256,12 +256,35 @@ _Static_assert(sizeof(ops_header_t) == 8, "wire header is 8 bytes");
 
 #define OPS_MAX_STEPS 8
 
+/* the plan methods this engine runs (builtin/plan/builtin_plan.h), and the
+ * aggregation each receive applies (builtin_control.c:960-972) */
+typedef enum {
+    M_REDUCE_RECURSIVE,   /* send to the partner, then receive and reduce */
+    M_REDUCE_TERMINAL,    /* tree root: receive from every child and reduce */
+    M_SEND_TO_SM_ROOT,    /* tree leaf, fan-in (ppn > 2) */
+    M_SEND_TERMINAL,      /* tree leaf fan-in at ppn == 2, root fan-out */
+    M_RECV_TERMINAL       /* tree leaf, fan-out: receive the result */
+} op_method_t;
+
+typedef enum { AGG_NOP, AGG_REDUCE, AGG_WRITE } op_aggregation_t;
+
+static const char *const method_name[] = {
+    "REDUCE_RECURSIVE", "REDUCE_TERMINAL", "SEND_TO_SM_ROOT", "SEND_TERMINAL",
+    "RECV_TERMINAL"
+};
+
 typedef struct {
-    unsigned    peer;             /* one endpoint per step (factor 2) */
+    uint8_t     method;           /* op_method_t */
+    uint8_t     aggregation;      /* op_aggregation_t */
     uint8_t     step_idx;         /* phase->step_index, 1-based */
-    const char *send_buffer;
+    unsigned    send_cnt;         /* endpoints sent to, in this order */
+    unsigned    send_peers[UCG_BUILTIN_OPS_MAX_MEMBERS];
+    unsigned    recv_cnt;         /* endpoints received from */
+    unsigned    recv_peers[UCG_BUILTIN_OPS_MAX_MEMBERS];  /* describe only */
+    int         send_recv_buffer; /* 0: send.buffer, 1: recv.buffer */
     size_t      frag_len;         /* 0: single message */
-    uint64_t    fragments_total;  /* ep_cnt x fragments */
+    uint64_t    frags;            /* messages per endpoint */
+    uint64_t    fragments_total;  /* recv_cnt x frags */
 } op_step_t;
 
 typedef struct {
@@ -290,6 +313,10 @@ struct ucg_builtin_lcoll {
     void        *op;
     size_t       dt_len;
     size_t       length;
+    const char  *plan;            /* "recursive doubling" / "tree" */
+    int          kind;            /* 0 allreduce, 1 reduce */
+    unsigned     root;
+    int          init_reduce;     /* ucg_builtin_init_reduce on start */
     op_step_t    steps[OPS_MAX_STEPS];
     unsigned     nsteps;
     /* request state (builtin_ops.h:233-241) */
@@ -299,8 +326,10 @@ struct ucg_builtin_lcoll {
     uint8_t      coll_id;
     unsigned     cur;
     uint64_t     pending;
-    int          step_open;
+    int          step_started;
+    int          step_open;       /* a combine step is open */
     int          send_pending;
+    unsigned     iter_ep;
     size_t       iter_offset;
 };
 
@@ -343,6 +372,7 @@ static void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
     c->done         = 1;
     c->active       = 0;
     c->send_pending = 0;
+    c->step_started = 0;
     slot->req       = NULL;
     slot->expecting = 0;
 }
@@ -376,77 +406,126 @@ static void check_pending(ucg_builtin_lcoll_t *c, uint16_t local_id)
     }
 }
 
-/* ucg_builtin_step_execute (REDUCE_RECURSIVE: send, then receive),
- * builtin_data.c:584-668 with ucg_builtin_step_am_short_max :83-137 */
-static void step_execute(ucg_builtin_lcoll_t *c)
+/* ucg_builtin_comp_step_cb / ucg_builtin_comp_last_step_cb,
+ * builtin_comp_step.inl:8-95: close the step's combine (the device mirror goes
+ * back to recv_buffer before the next step sends it, builtin_control.c:
+ * 850-857), then move on */
+static void step_complete(ucg_builtin_lcoll_t *c)
 {
-    ucg_builtin_lgroup_t *g = c->g;
-    op_step_t *s = &c->steps[c->cur];
-    ops_header_t h;
-    ucs_status_t st;
-
-    if (!c->step_open) {
-        st = ucg_builtin_combine_step_begin(g->cmb, c->op, c->dtype, c->rbuf,
-                                            c->length);
+    if (c->step_open) {
+        ucs_status_t st = ucg_builtin_combine_step_end(c->g->cmb);
+        c->step_open = 0;
         if (st != UCS_OK) {
             finish(c, st);
             return;
         }
-        c->step_open   = 1;
-        c->pending     = s->fragments_total;
-        c->iter_offset = 0;
     }
-    h.header        = 0;
-    h.group_id      = g->group_id;
-    h.coll_id       = c->coll_id;
-    h.step_idx      = s->step_idx;
-    if (s->frag_len == 0) {
-        if (c->iter_offset == 0) {
-            h.remote_offset = 0;
-            st = ucg_builtin_shm_am_short(g->iface, s->peer, h.header,
-                                          s->send_buffer, c->length);
-            if (st == UCS_ERR_NO_RESOURCE) {
-                c->send_pending = 1;      /* ucg_builtin_req_enqueue_resend */
-                return;
-            }
-            if (st != UCS_OK) {
-                finish(c, st);
-                return;
-            }
-            g->stats[0]++;
-            c->iter_offset = c->length ? c->length : 1;
-        }
+    c->step_started = 0;
+    if (c->cur + 1 == c->nsteps) {
+        finish(c, UCS_OK);
     } else {
-        while (c->iter_offset < c->length) {
-            size_t n = c->length - c->iter_offset;
-            if (n > s->frag_len) {
-                n = s->frag_len;
-            }
-            h.remote_offset = (uint32_t)c->iter_offset;
-            st = ucg_builtin_shm_am_short(g->iface, s->peer, h.header,
-                                          s->send_buffer + c->iter_offset, n);
-            if (st == UCS_ERR_NO_RESOURCE) {
-                c->send_pending = 1;
-                return;
-            }
+        c->cur++;
+        step_execute(c);
+    }
+}
+
+/* ucg_builtin_step_execute, builtin_data.c:411-668: send every fragment to
+ * every endpoint of the step (endpoint-major, resumable at iter_ep /
+ * iter_offset after UCS_ERR_NO_RESOURCE, :470-517 and ucg_builtin_step_
+ * am_short_max :83-137), then either complete (no receive: comp_criteria
+ * SEND, builtin_control.c:1000-1002) or drain what is already stashed for
+ * this step (builtin_comp_step.inl:403-462) */
+static void step_execute(ucg_builtin_lcoll_t *c)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    op_step_t *s = &c->steps[c->cur];
+    const char *sbuf = s->send_recv_buffer ? c->rbuf : c->sbuf;
+    ops_header_t h;
+    ucs_status_t st;
+
+    if (!c->step_started) {
+        if (s->aggregation == AGG_REDUCE) {
+            st = ucg_builtin_combine_step_begin(g->cmb, c->op, c->dtype, c->rbuf,
+                                                c->length);
             if (st != UCS_OK) {
                 finish(c, st);
                 return;
             }
-            g->stats[0]++;
-            c->iter_offset += n;
+            c->step_open = 1;
         }
+        c->step_started = 1;
+        c->pending      = s->fragments_total;
+        c->iter_ep      = 0;
+        c->iter_offset  = 0;
+    }
+    h.header   = 0;
+    h.group_id = g->group_id;
+    h.coll_id  = c->coll_id;
+    h.step_idx = s->step_idx;
+    for (; c->iter_ep < s->send_cnt; c->iter_ep++) {
+        unsigned peer = s->send_peers[c->iter_ep];
+        if (s->frag_len == 0) {
+            if (c->iter_offset == 0) {
+                h.remote_offset = 0;
+                st = ucg_builtin_shm_am_short(g->iface, peer, h.header, sbuf,
+                                              c->length);
+                if (st == UCS_ERR_NO_RESOURCE) {
+                    c->send_pending = 1;  /* ucg_builtin_req_enqueue_resend */
+                    return;
+                }
+                if (st != UCS_OK) {
+                    finish(c, st);
+                    return;
+                }
+                g->stats[0]++;
+            }
+        } else {
+            while (c->iter_offset < c->length) {
+                size_t n = c->length - c->iter_offset;
+                if (n > s->frag_len) {
+                    n = s->frag_len;
+                }
+                h.remote_offset = (uint32_t)c->iter_offset;
+                st = ucg_builtin_shm_am_short(g->iface, peer, h.header,
+                                              sbuf + c->iter_offset, n);
+                if (st == UCS_ERR_NO_RESOURCE) {
+                    c->send_pending = 1;
+                    return;
+                }
+                if (st != UCS_OK) {
+                    finish(c, st);
+                    return;
+                }
+                g->stats[0]++;
+                c->iter_offset += n;
+            }
+        }
+        c->iter_offset = 0;   /* next endpoint starts from the first byte */
     }
     c->send_pending = 0;
+    if (s->recv_cnt == 0) {
+        step_complete(c);
+        return;
+    }
+    h.remote_offset = 0;
     check_pending(c, h.local_id);
 }
 
-/* ucg_builtin_step_recv_cb -> handle_data (REDUCE) + handle_comp,
+/* ucg_builtin_step_recv_cb -> recv_handle_chunk + handle_comp,
  * builtin_comp_step.inl:184-232, 314-401; returns 1 when the step is done */
 static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
                    size_t length)
 {
-    ucs_status_t st = ucg_builtin_combine_fragment(c->g->cmb, offset, data, length);
+    op_step_t *s = &c->steps[c->cur];
+    ucs_status_t st = UCS_OK;
+
+    if (offset + length > c->length) {
+        st = UCS_ERR_IO_ERROR;          /* a message outside recv.buffer */
+    } else if (s->aggregation == AGG_REDUCE) {
+        st = ucg_builtin_combine_fragment(c->g->cmb, offset, data, length);
+    } else if (s->aggregation == AGG_WRITE) {
+        memcpy(c->rbuf + offset, data, length);   /* :204-210 */
+    }
     if (st != UCS_OK) {
         finish(c, st);      /* recv_handle_error, :332-333 */
         return 1;
@@ -454,20 +533,7 @@ static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
     if (--c->pending != 0) {
         return 0;
     }
-    /* the step is complete: the device mirror goes back to recv_buffer
-     * before the next step sends it (builtin_control.c:850-857) */
-    st = ucg_builtin_combine_step_end(c->g->cmb);
-    c->step_open = 0;
-    if (st != UCS_OK) {
-        finish(c, st);
-        return 1;
-    }
-    if (c->cur + 1 == c->nsteps) {
-        finish(c, UCS_OK);
-    } else {
-        c->cur++;
-        step_execute(c);  /* ucg_builtin_comp_step_cb, :60-95 */
-    }
+    step_complete(c);
     return 1;
 }
 
@@ -589,24 +655,150 @@ void ucg_builtin_lgroup_stats(ucg_builtin_lgroup_t *g, uint64_t out[4])
     }
 }
 
-ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sbuf,
-                                         void *rbuf, int count, void *dtype,
-                                         void *op, ucg_builtin_lcoll_t **coll_p)
+/* Fragmentation of one step's message (builtin_control.c:434,462-465) */
+static ucs_status_t step_fragments(ucg_builtin_lcoll_t *c, op_step_t *s)
 {
-    ucg_builtin_lcoll_t *c;
-    unsigned steps, k;
-    size_t max_payload;
+    size_t max_short   = ucg_builtin_shm_iface_max_short(c->g->iface);
+    size_t max_payload = max_short - 8;
+    if (c->length > max_payload) {
+        s->frag_len = ucg_builtin_step_fragment_length(max_short, c->dt_len);
+        if (s->frag_len == 0) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+        s->frags = ucg_builtin_step_fragments_total(c->length, s->frag_len, 1);
+    } else {
+        s->frag_len = 0;
+        s->frags    = 1;
+    }
+    s->fragments_total = (uint64_t)s->recv_cnt * s->frags;
+    return UCS_OK;
+}
 
-    if (g == NULL || coll_p == NULL || rbuf == NULL || count < 0 ||
-        (count && sbuf == NULL)) {
-        return UCS_ERR_INVALID_PARAM;
-    }
-    steps = ucg_builtin_recursive_steps(g->size, 2);
-    if (g->size > 1 && steps == 0) {
-        return UCS_ERR_UNSUPPORTED;   /* needs the tree plan (next row, f3) */
-    }
+/* Recursive doubling, factor 2 (builtin_recursive.c:20-228): step k sends to
+ * and reduces from my ^ 2^(k-1); step 1 sends the send buffer, later steps
+ * the accumulator (builtin_control.c:825-857). */
+static ucs_status_t plan_recursive(ucg_builtin_lcoll_t *c)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    unsigned steps = ucg_builtin_recursive_steps(g->size, 2), k;
     if (steps > OPS_MAX_STEPS) {
         return UCS_ERR_UNSUPPORTED;
+    }
+    c->plan        = "recursive doubling";
+    c->nsteps      = steps;
+    c->init_reduce = 1;
+    for (k = 0; k < steps; k++) {
+        op_step_t *s  = &c->steps[k];
+        unsigned peer = (unsigned)ucg_builtin_recursive_peer(g->my, k + 1, 2, 1);
+        s->method           = M_REDUCE_RECURSIVE;
+        s->aggregation      = AGG_REDUCE;
+        s->step_idx         = (uint8_t)(k + 1);
+        s->send_cnt         = 1;
+        s->send_peers[0]    = peer;
+        s->recv_cnt         = 1;
+        s->recv_peers[0]    = peer;
+        s->send_recv_buffer = (k != 0);
+        if (step_fragments(c, s) != UCS_OK) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+    }
+    return UCS_OK;
+}
+
+/* Single-host tree (builtin_tree.c): every member of a shm iface is at
+ * UCG_GROUP_MEMBER_DISTANCE_HOST from every other, so ucg_builtin_tree_add_
+ * intra (:262-380) makes the root the parent of all other members (children
+ * in member order) and no member a waypoint; with ppn == member_count there
+ * is no inter-host phase (:486-495). ucg_builtin_tree_connect (:86-260,
+ * step_offset 1) then gives
+ *   fan-in,  step_idx 1: root REDUCE_TERMINAL from all children (init_reduce:
+ *            recv <- send first); each child SEND_TO_SM_ROOT (SEND_TERMINAL
+ *            when ppn == 2) of its send buffer to the root;
+ *   fan-out, step_idx 4 (allreduce only, BROADCAST modifier): root
+ *            SEND_TERMINAL of recv.buffer to all children; each child
+ *            RECV_TERMINAL into recv.buffer with WRITE aggregation.
+ * The root receives the children's messages in arrival order and reduces each
+ * one into recv.buffer as it comes (MULTIPLE_MESSAGES criteria,
+ * builtin_control.c:974-996): for a floating-point op the association follows
+ * arrival, as in the reference; every member ends with the root's bits.
+ * The reference builds root != 0 through ucg_builtin_topo_tree_set_root, which
+ * reads tree parameters out of a plan phase (builtin_tree.c:590-592); here the
+ * same flat tree is simply rooted at `root`. */
+static ucs_status_t plan_tree(ucg_builtin_lcoll_t *c, int fanout)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    unsigned ppn = g->size, m, nchild = 0;
+    unsigned children[UCG_BUILTIN_OPS_MAX_MEMBERS];
+    int is_root = (g->my == c->root);
+    op_step_t *s;
+
+    for (m = 0; m < g->size; m++) {
+        if (m != c->root) {
+            children[nchild++] = m;
+        }
+    }
+    c->plan   = "tree";
+    c->nsteps = 0;
+    /* fan-in */
+    s = &c->steps[c->nsteps++];
+    s->step_idx = 1;
+    if (is_root) {
+        s->method      = M_REDUCE_TERMINAL;
+        s->aggregation = AGG_REDUCE;
+        s->recv_cnt    = nchild;
+        memcpy(s->recv_peers, children, nchild * sizeof(unsigned));
+        s->send_cnt    = 0;
+        c->init_reduce = 1;
+    } else {
+        s->method        = (ppn == 2) ? M_SEND_TERMINAL : M_SEND_TO_SM_ROOT;
+        s->aggregation   = AGG_NOP;
+        s->send_cnt      = 1;
+        s->send_peers[0] = c->root;
+        s->recv_cnt      = 0;
+    }
+    s->send_recv_buffer = 0;
+    if (step_fragments(c, s) != UCS_OK) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    if (!fanout) {
+        return UCS_OK;
+    }
+    /* fan-out */
+    s = &c->steps[c->nsteps++];
+    s->step_idx = 4;
+    if (is_root) {
+        s->method      = M_SEND_TERMINAL;
+        s->aggregation = AGG_NOP;
+        s->send_cnt    = nchild;
+        memcpy(s->send_peers, children, nchild * sizeof(unsigned));
+        s->recv_cnt    = 0;
+    } else {
+        s->method        = M_RECV_TERMINAL;
+        s->aggregation   = AGG_WRITE;
+        s->send_cnt      = 0;
+        s->recv_cnt      = 1;
+        s->recv_peers[0] = c->root;
+    }
+    s->send_recv_buffer = 1;
+    return step_fragments(c, s);
+}
+
+static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
+                              void *rbuf, int count, void *dtype, void *op,
+                              ucg_builtin_lcoll_t **coll_p)
+{
+    ucg_builtin_lcoll_t *c;
+    size_t dt_len;
+
+    if (g == NULL || coll_p == NULL || count < 0 || (count && sbuf == NULL)) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    dt_len = ucg_builtin_combine_dtype_length(g->cmb, dtype);
+    if (dt_len == 0) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if ((size_t)count * dt_len * g->size > 0xffffffffull) {
+        return UCS_ERR_UNSUPPORTED;   /* 32-bit remote_offset, SURVEY 7 (ix) */
     }
     c = calloc(1, sizeof(*c));
     if (c == NULL) {
@@ -618,42 +810,85 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
     c->count  = count;
     c->dtype  = dtype;
     c->op     = op;
-    c->dt_len = ucg_builtin_combine_dtype_length(g->cmb, dtype);
-    if (c->dt_len == 0) {
-        free(c);
-        return UCS_ERR_INVALID_PARAM;
-    }
-    c->length   = (size_t)count * c->dt_len;
-    c->nsteps   = steps;
-    max_payload = ucg_builtin_shm_iface_max_short(g->iface) - 8;
-    if (c->length * g->size > 0xffffffffull) {
-        free(c);
-        return UCS_ERR_UNSUPPORTED;   /* 32-bit remote_offset, SURVEY 7 (ix) */
-    }
-    for (k = 0; k < steps; k++) {
-        op_step_t *s = &c->steps[k];
-        s->peer     = (unsigned)ucg_builtin_recursive_peer(g->my, k + 1, 2, 1);
-        s->step_idx = (uint8_t)(k + 1);
-        /* step 1 sends the send buffer, later steps the accumulator
-         * (builtin_control.c:660-671, 850-857) */
-        s->send_buffer = (k == 0) ? (const char*)sbuf : (const char*)rbuf;
-        if (c->length > max_payload) {
-            s->frag_len = ucg_builtin_step_fragment_length(
-                              ucg_builtin_shm_iface_max_short(g->iface), c->dt_len);
-            if (s->frag_len == 0) {
-                free(c);
-                return UCS_ERR_UNSUPPORTED;
-            }
-            s->fragments_total = ucg_builtin_step_fragments_total(c->length,
-                                                                  s->frag_len, 1);
-        } else {
-            s->frag_len        = 0;
-            s->fragments_total = 1;
-        }
-    }
+    c->dt_len = dt_len;
+    c->length = (size_t)count * dt_len;
     c->done   = 1;
     c->status = UCS_OK;
     *coll_p   = c;
+    return UCS_OK;
+}
+
+/* UCX_BUILTIN_ALLREDUCE_PLAN=auto|tree|recursive (this build's knob; the
+ * reference always takes ucg_builtin_choose_topology's choice) */
+static int allreduce_use_tree(unsigned size)
+{
+    const char *p = getenv("UCX_BUILTIN_ALLREDUCE_PLAN");
+    if (p && strcmp(p, "tree") == 0) {
+        return 1;
+    }
+    if (p && strcmp(p, "recursive") == 0) {
+        return 0;
+    }
+    return (size & (size - 1)) != 0;   /* builtin.c:112-121 */
+}
+
+ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                         void *rbuf, int count, void *dtype,
+                                         void *op, ucg_builtin_lcoll_t **coll_p)
+{
+    ucg_builtin_lcoll_t *c;
+    ucs_status_t st;
+
+    if (rbuf == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    st = lcoll_new(g, sbuf, rbuf, count, dtype, op, &c);
+    if (st != UCS_OK) {
+        return st;
+    }
+    c->kind = 0;
+    if (g->size == 1) {
+        c->plan        = "none";
+        c->init_reduce = 1;
+        st = UCS_OK;
+    } else if (allreduce_use_tree(g->size)) {
+        st = plan_tree(c, 1);
+    } else {
+        st = plan_recursive(c);
+    }
+    if (st != UCS_OK) {
+        free(c);
+        return st;
+    }
+    *coll_p = c;
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                      void *rbuf, int count, void *dtype,
+                                      void *op, unsigned root,
+                                      ucg_builtin_lcoll_t **coll_p)
+{
+    ucg_builtin_lcoll_t *c;
+    ucs_status_t st;
+
+    if (g == NULL || root >= g->size || (g->my == root && rbuf == NULL)) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    st = lcoll_new(g, sbuf, rbuf, count, dtype, op, &c);
+    if (st != UCS_OK) {
+        return st;
+    }
+    c->kind = 1;
+    c->root = root;
+    if (g->size == 1) {
+        c->plan        = "none";
+        c->init_reduce = 1;
+    } else if ((st = plan_tree(c, 0)) != UCS_OK) {
+        free(c);
+        return st;
+    }
+    *coll_p = c;
     return UCS_OK;
 }
 
@@ -675,14 +910,16 @@ ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *c)
         return UCS_ERR_BUSY;    /* more than 16 ops outstanding */
     }
     g->next_coll_id++;          /* ucg_collective_trigger, base/ucg_group.c:485 */
-    /* ucg_builtin_init_reduce: recv <- send (in place: nothing to copy) */
-    if (c->rbuf != c->sbuf && c->length) {
+    /* ucg_builtin_init_reduce: recv <- send (in place: nothing to copy);
+     * tree leaves have no init (builtin_control.c:755-767) */
+    if (c->init_reduce && c->rbuf != c->sbuf && c->length) {
         memcpy(c->rbuf, c->sbuf, c->length);
     }
     c->done         = 0;
     c->status       = UCS_INPROGRESS;
     c->cur          = 0;
     c->step_open    = 0;
+    c->step_started = 0;
     c->send_pending = 0;
     if (c->nsteps == 0 || c->length == 0) {
         c->done   = 1;
@@ -737,16 +974,35 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
         int _r = snprintf(buf + w, w < max ? max - w : 0, __VA_ARGS__);       \
         if (_r > 0) w += (size_t)_r;                                          \
     } while (0)
-    PUT("Planner: builtin (recursive doubling), member %u of %u\n", c->g->my,
-        c->g->size);
-    PUT("Phases: %u\n", c->nsteps);
+    PUT("Planner: builtin (%s), %s, member %u of %u", c->plan,
+        c->kind ? "reduce" : "allreduce", c->g->my, c->g->size);
+    if (c->kind) {
+        PUT(", root %u", c->root);
+    }
+    PUT("\nPhases: %u\n", c->nsteps);
     for (k = 0; k < c->nsteps; k++) {
         const op_step_t *s = &c->steps[k];
-        PUT("Step #%u (step_idx %u): Reduce (R) with peer %u, send %s, "
-            "fragment length %zu, fragments total %llu, aggregation reduce\n",
-            k, (unsigned)s->step_idx, s->peer, k == 0 ? "send.buffer" : "recv.buffer",
-            s->frag_len ? s->frag_len : c->length,
-            (unsigned long long)s->fragments_total);
+        unsigned e;
+        PUT("Step #%u (step_idx %u): %s", k, (unsigned)s->step_idx,
+            method_name[s->method]);
+        if (s->send_cnt) {
+            PUT(", send %s to", s->send_recv_buffer ? "recv.buffer" : "send.buffer");
+            for (e = 0; e < s->send_cnt; e++) {
+                PUT(" %u", s->send_peers[e]);
+            }
+        }
+        if (s->recv_cnt) {
+            PUT(", receive from");
+            for (e = 0; e < s->recv_cnt; e++) {
+                PUT(" %u", s->recv_peers[e]);
+            }
+        }
+        PUT(", fragment length %zu, fragments per endpoint %llu, "
+            "fragments total %llu, aggregation %s\n",
+            s->frag_len ? s->frag_len : c->length, (unsigned long long)s->frags,
+            (unsigned long long)s->fragments_total,
+            s->aggregation == AGG_REDUCE ? "reduce" :
+            s->aggregation == AGG_WRITE ? "write" : "nop");
     }
 #undef PUT
     return w < max ? w : max - 1;

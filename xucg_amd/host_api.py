@@ -65,6 +65,8 @@ HOST_API = {
     "ucg_builtin_lgroup_stats": (None, [_vp, ctypes.POINTER(_u64)]),
     "ucg_builtin_lcoll_allreduce": (_int, [_vp, _vp, _vp, _int, _vp, _vp,
                                            ctypes.POINTER(_vp)]),
+    "ucg_builtin_lcoll_reduce": (_int, [_vp, _vp, _vp, _int, _vp, _vp, _u,
+                                        ctypes.POINTER(_vp)]),
     "ucg_builtin_lcoll_start": (_int, [_vp]),
     "ucg_builtin_lcoll_test": (_int, [_vp, ctypes.POINTER(_int)]),
     "ucg_builtin_lcoll_wait": (_int, [_vp]),

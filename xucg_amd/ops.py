@@ -48,6 +48,9 @@ class Group:
     def allreduce(self, sbuf, rbuf, count, dtype, op):
         return Allreduce(self, sbuf, rbuf, count, dtype, op)
 
+    def reduce(self, sbuf, rbuf, count, dtype, op, root=0):
+        return Reduce(self, sbuf, rbuf, count, dtype, op, root)
+
     def close(self):
         if getattr(self, "handle", None):
             _lib.host().ucg_builtin_lgroup_destroy(self.handle)
@@ -62,15 +65,9 @@ def _addr(x):
     return x.ptr
 
 
-class Allreduce:
-    """A persistent allreduce on the builtin recursive-doubling plan."""
-
-    def __init__(self, group, sbuf, rbuf, count, dtype, op):
-        self.group = group
-        h = ctypes.c_void_p()
-        self.status = _lib.host().ucg_builtin_lcoll_allreduce(
-            group.handle, _addr(sbuf), _addr(rbuf), count, dtype, op, ctypes.byref(h))
-        self.handle = h.value if self.status == 0 else None
+class _Collective:
+    """A persistent collective of the builtin planner (status != 0: the
+    create call failed and `handle` is None)."""
 
     def start(self):
         return _lib.host().ucg_builtin_lcoll_start(self.handle)
@@ -93,3 +90,26 @@ class Allreduce:
         if self.handle:
             _lib.host().ucg_builtin_lcoll_destroy(self.handle)
             self.handle = None
+
+
+class Allreduce(_Collective):
+    """MPI_Allreduce: recursive doubling (power-of-two groups) or tree."""
+
+    def __init__(self, group, sbuf, rbuf, count, dtype, op):
+        self.group = group
+        h = ctypes.c_void_p()
+        self.status = _lib.host().ucg_builtin_lcoll_allreduce(
+            group.handle, _addr(sbuf), _addr(rbuf), count, dtype, op, ctypes.byref(h))
+        self.handle = h.value if self.status == 0 else None
+
+
+class Reduce(_Collective):
+    """MPI_Reduce: tree fan-in to `root` (rbuf may be None off the root)."""
+
+    def __init__(self, group, sbuf, rbuf, count, dtype, op, root=0):
+        self.group = group
+        h = ctypes.c_void_p()
+        self.status = _lib.host().ucg_builtin_lcoll_reduce(
+            group.handle, _addr(sbuf), 0 if rbuf is None else _addr(rbuf), count,
+            dtype, op, root, ctypes.byref(h))
+        self.handle = h.value if self.status == 0 else None
