@@ -97,6 +97,13 @@ ucg_builtin_dev_ctx_t *ucg_builtin_combine_dev_ctx(ucg_builtin_combine_t *cmb);
  * to the device (H2D -> kernel -> D2H); everything else, and every op or
  * type the device cannot classify, calls reduce_cb_f. The callback's return
  * value is propagated here (the reference discards it). */
+/* The atomic-packer condition of ucg_builtin_step_select_packers
+ * (builtin/ops/builtin_control.c:535-575): an unsigned integer datatype and
+ * is_sum_f(op). Returns the element length (1, 2, 4 or 8), else 0. */
+size_t       ucg_builtin_combine_atomic_sum_length(ucg_builtin_combine_t *cmb,
+                                                   void *reduce_op,
+                                                   void *datatype);
+
 ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
                                         void *reduce_op, void *src, void *dst,
                                         int dcount, void *datatype);

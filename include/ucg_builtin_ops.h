@@ -67,6 +67,22 @@ ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *iface,
 /* uct_iface_progress: deliver pending messages; returns how many */
 unsigned     ucg_builtin_shm_progress(ucg_builtin_shm_iface_t *iface,
                                       ucg_builtin_am_cb_f cb, void *arg);
+/* Incast: the bcopy-into-the-root's-buffer send of the UCX collectives
+ * extension that the reference's SM-root packers target (builtin/ops/
+ * builtin_pack.c:50-72, 100-148; selected for SEND_TO_SM_ROOT with an
+ * AGGREGATE modifier, builtin_control.c:535-602). All `expected` children
+ * of `root` send the same header; the first to arrive packs with
+ * reducing == 0 (copy), the rest with reducing == 1 (combine into dest) -
+ * or, when `concurrent`, every child packs with reducing == 1 into a zeroed
+ * cell outside the cell lock (atomic packers). The root's progress delivers
+ * the cell as ONE message once all children packed. UCS_ERR_NO_RESOURCE
+ * when the cell is busy with another message (retry later). */
+typedef void (*ucg_builtin_pack_cb_f)(void *arg, void *dest, int reducing);
+ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *iface,
+                                       unsigned root, uint64_t header,
+                                       unsigned expected, size_t length,
+                                       ucg_builtin_pack_cb_f pack, void *arg,
+                                       int concurrent);
 /* Blocking barrier of all members (set-up / tear-down only). */
 void         ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *iface);
 

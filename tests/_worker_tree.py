@@ -35,6 +35,10 @@ INT_CASES = [  # (dtype, op, count)
     ("uint32", "land", 64),
     ("int8", "lor", 1),
     ("uint64", "band", 2048),
+    ("uint8", "sum", 4099),          # unsigned SUM: the atomic packers with incast
+    ("uint16", "sum", 513),
+    ("uint32", "sum", 1000),
+    ("uint64", "sum", 77),
 ]
 FP_EXACT = [("float32", "sum", 1024), ("float64", "sum", 1500)]
 # (dtype, op, count, rtol): fp16/bf16 partial sums of "exact" inputs can round
@@ -129,6 +133,10 @@ def main():
     c = group.allreduce(x, np.zeros_like(x), 1024, DTYPES["float32"], OPS["sum"])
     text = c.describe()
     print("describe:\n" + text, flush=True)
+    c.close()
+    u = np.zeros(64, np.uint32)
+    c = group.allreduce(u, np.zeros_like(u), 64, DTYPES["uint32"], OPS["sum"])
+    print("describe uint32 sum:\n" + c.describe(), flush=True)
     c.close()
     if "(tree)" in text:
         up, down = O.tree_intra(rank, world, 0)

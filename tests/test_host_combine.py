@@ -198,3 +198,18 @@ def test_staged_step_on_device_matches_host_fallback():
         results.append(acc)
         cmb.close()
     assert (O.bits(results[0]) == O.bits(results[1])).all()
+
+
+def test_atomic_packer_condition():
+    """ucg_builtin_step_select_packers (builtin_control.c:535-575): the atomic
+    packers apply to unsigned integer SUM only, element length 1/2/4/8."""
+    from xucg_amd import _lib
+    from mock_mpi import MockMPI, OPS, DTYPES
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    f = _lib.host().ucg_builtin_combine_atomic_sum_length
+    for dt in DTYPES:
+        want = O.storage(dt)().itemsize if dt.startswith("uint") else 0
+        assert f(cmb.handle, OPS["sum"], DTYPES[dt]) == want, dt
+        assert f(cmb.handle, OPS["max"], DTYPES[dt]) == 0, dt
+    cmb.close()

@@ -122,6 +122,23 @@ def test_allreduce_rejects_bad_reduce_root():
     cmb.close()
 
 
+@pytest.mark.parametrize("world,max_short,cells", [(3, 256, 64), (5, 64, 64), (7, 256, 2),
+                                                 (6, 8192, 4)])
+def test_tree_incast_packers(world, max_short, cells, monkeypatch):
+    """SM-root incast: children pack into one cell at the
+    root - reducing packer (copy, then dst = mine (op) dst) or, for unsigned
+    SUM, the atomic packer - and the root receives one message per fragment."""
+    monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", "y")
+    codes, outs = launch("_worker_tree.py", world, args=(shm_name(), "host", max_short, cells),
+                         timeout=240)
+    assert codes == [0] * world, "\n".join(outs)
+    d = _digests(outs)
+    assert all(x == d[0] for x in d) and d[0], d
+    assert "incast (reducing packer)" in outs[1] and "incast (atomic packer)" in outs[1]
+    root_plan = [ln for ln in outs[0].splitlines() if "REDUCE_TERMINAL" in ln][0]
+    assert "incast" in root_plan
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [3, 5])
 def test_tree_multiprocess_device_staging(world):

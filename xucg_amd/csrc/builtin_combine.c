@@ -199,6 +199,21 @@ size_t ucg_builtin_combine_dtype_length(ucg_builtin_combine_t *cmb, void *dataty
     return cmb ? dtype_length(cmb, datatype) : 0;
 }
 
+size_t ucg_builtin_combine_atomic_sum_length(ucg_builtin_combine_t *cmb,
+                                             void *reduce_op, void *datatype)
+{
+    int is_signed = 1;
+    size_t len;
+    if (cmb == NULL || cmb->params.is_integer_f == NULL ||
+        cmb->params.is_sum_f == NULL ||
+        !cmb->params.is_integer_f(datatype, &is_signed) || is_signed ||
+        !cmb->params.is_sum_f(reduce_op)) {
+        return 0;
+    }
+    len = dtype_length(cmb, datatype);
+    return (len == 1 || len == 2 || len == 4 || len == 8) ? len : 0;
+}
+
 int ucg_builtin_combine_classify(ucg_builtin_combine_t *cmb, void *reduce_op,
                                  void *datatype, ucg_dev_op_t *op_out,
                                  ucg_dev_dtype_t *dt_out)

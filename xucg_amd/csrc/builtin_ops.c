@@ -39,6 +39,28 @@ typedef struct {
 #define SEG_CTL_BYTES 128
 #define UNEXP_GROUPS  64
 
+/* Incast cell (the SM-root "bcopy into a shared buffer" of the UCX
+ * collectives extension the reference's reducing packers are written for,
+ * builtin_pack.c:50-72, 100-148): every child of a root packs the same
+ * (header) message into one cell of the root's incast area - the first copies
+ * (or, for a concurrent packer, zeroes), the others reduce into it - and the
+ * root receives the cell as one message once all `expected` children packed. */
+typedef struct {
+    _Atomic uint32_t lock;
+    _Atomic uint32_t state;     /* INCAST_FREE / _FILLING / _READY */
+    _Atomic uint32_t count;     /* children packed so far */
+    uint32_t         expected;
+    uint32_t         length;    /* payload bytes */
+    uint32_t         reserved;
+    uint64_t         header;    /* followed by the payload: data = &header */
+} incast_cell_t;
+
+enum { INCAST_FREE, INCAST_FILLING, INCAST_READY };
+
+typedef struct {
+    _Alignas(64) _Atomic uint64_t ready;   /* cells in INCAST_READY */
+} incast_ctl_t;
+
 typedef struct stash {
     struct stash *next;
     uint64_t      header;
@@ -54,6 +76,9 @@ struct ucg_builtin_shm_iface {
     size_t    cell_size;
     unsigned  cells;
     size_t    ring_bytes;
+    size_t    incast_cell_size;
+    size_t    incast_bytes;    /* one member's incast area */
+    size_t    incast_base;     /* offset of member 0's incast area */
     size_t    seg_bytes;
     char     *seg;
     uint64_t  barrier_gen;
@@ -73,6 +98,18 @@ static ring_ctl_t *ring_ctl(ucg_builtin_shm_iface_t *it, unsigned src, unsigned 
 static cell_t *ring_cell(ucg_builtin_shm_iface_t *it, ring_ctl_t *r, uint64_t idx)
 {
     return (cell_t*)((char*)r + sizeof(ring_ctl_t) + (idx % it->cells) * it->cell_size);
+}
+
+static incast_ctl_t *incast_ctl(ucg_builtin_shm_iface_t *it, unsigned member)
+{
+    return (incast_ctl_t*)(it->seg + it->incast_base + member * it->incast_bytes);
+}
+
+static incast_cell_t *incast_cell(ucg_builtin_shm_iface_t *it, unsigned member,
+                                  unsigned idx)
+{
+    return (incast_cell_t*)((char*)incast_ctl(it, member) + sizeof(incast_ctl_t) +
+                            (size_t)idx * it->incast_cell_size);
 }
 
 static double now_s(void)
@@ -113,7 +150,10 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
     it->cells      = ring_cells;
     it->cell_size  = (sizeof(cell_t) + (max_short - 8) + 63) & ~(size_t)63;
     it->ring_bytes = sizeof(ring_ctl_t) + (size_t)ring_cells * it->cell_size;
-    it->seg_bytes  = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
+    it->incast_cell_size = (sizeof(incast_cell_t) + (max_short - 8) + 63) & ~(size_t)63;
+    it->incast_bytes     = sizeof(incast_ctl_t) + (size_t)ring_cells * it->incast_cell_size;
+    it->incast_base      = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
+    it->seg_bytes        = it->incast_base + (size_t)members * it->incast_bytes;
 
     fd = shm_open(it->name, O_CREAT | O_RDWR, 0600);
     if (fd < 0) {
@@ -207,10 +247,101 @@ ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *it, unsigned peer
     return UCS_OK;
 }
 
+static void spin_lock(_Atomic uint32_t *l)
+{
+    uint32_t z = 0;
+    while (!atomic_compare_exchange_weak_explicit(l, &z, 1, memory_order_acquire,
+                                                  memory_order_relaxed)) {
+        z = 0;
+        sched_yield();
+    }
+}
+
+static void spin_unlock(_Atomic uint32_t *l)
+{
+    atomic_store_explicit(l, 0, memory_order_release);
+}
+
+ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *it, unsigned root,
+                                       uint64_t header, unsigned expected,
+                                       size_t length, ucg_builtin_pack_cb_f pack,
+                                       void *arg, int concurrent)
+{
+    unsigned idx;
+    incast_cell_t *c;
+    int first;
+
+    if (root >= it->members || root == it->my || expected == 0 || pack == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (length + 8 > it->max_short) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    /* the cell of this message: a multiplicative hash of the whole header, so
+     * consecutive fragments (remote_offset) and ops (coll_id) spread out */
+    idx = (unsigned)(((header * 0x9E3779B97F4A7C15ull) >> 32) % it->cells);
+    c   = incast_cell(it, root, idx);
+    spin_lock(&c->lock);
+    /* acquire: the root's reads of a delivered cell precede our writes */
+    if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FREE) {
+        atomic_store_explicit(&c->state, INCAST_FILLING, memory_order_relaxed);
+        atomic_store_explicit(&c->count, 0, memory_order_relaxed);
+        c->header   = header;
+        c->expected = expected;
+        c->length   = (uint32_t)length;
+        first       = 1;
+    } else if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FILLING &&
+               c->header == header) {
+        first = 0;
+    } else {
+        spin_unlock(&c->lock);
+        return UCS_ERR_NO_RESOURCE;   /* cell busy with another message */
+    }
+    if (concurrent) {
+        /* atomic packers add into a zeroed cell outside the lock */
+        if (first) {
+            memset(c + 1, 0, length);
+        }
+        spin_unlock(&c->lock);
+        pack(arg, c + 1, 1);
+    } else {
+        pack(arg, c + 1, !first);     /* first copies, the others reduce */
+    }
+    if (atomic_fetch_add_explicit(&c->count, 1, memory_order_acq_rel) + 1 == expected) {
+        atomic_store_explicit(&c->state, INCAST_READY, memory_order_release);
+        atomic_fetch_add_explicit(&incast_ctl(it, root)->ready, 1, memory_order_release);
+    }
+    if (!concurrent) {
+        spin_unlock(&c->lock);
+    }
+    return UCS_OK;
+}
+
+static unsigned incast_progress(ucg_builtin_shm_iface_t *it, ucg_builtin_am_cb_f cb,
+                                void *arg)
+{
+    incast_ctl_t *ctl = incast_ctl(it, it->my);
+    unsigned i, n = 0;
+    if (atomic_load_explicit(&ctl->ready, memory_order_acquire) == 0) {
+        return 0;
+    }
+    for (i = 0; i < it->cells; i++) {
+        incast_cell_t *c = incast_cell(it, it->my, i);
+        if (atomic_load_explicit(&c->state, memory_order_acquire) != INCAST_READY) {
+            continue;
+        }
+        (void)cb(arg, &c->header, 8 + (size_t)c->length);
+        atomic_fetch_sub_explicit(&ctl->ready, 1, memory_order_relaxed);
+        atomic_store_explicit(&c->state, INCAST_FREE, memory_order_release);
+        n++;
+    }
+    return n;
+}
+
 unsigned ucg_builtin_shm_progress(ucg_builtin_shm_iface_t *it,
                                   ucg_builtin_am_cb_f cb, void *arg)
 {
-    unsigned src, n = 0;
+    unsigned src, n = incast_progress(it, cb, arg);
     for (src = 0; src < it->members; src++) {
         ring_ctl_t *r;
         uint64_t tail, head;
@@ -268,6 +399,11 @@ typedef enum {
 
 typedef enum { AGG_NOP, AGG_REDUCE, AGG_WRITE } op_aggregation_t;
 
+/* bcopy packers of an SM-root child (builtin_pack.c): plain copy, reducing
+ * (:50-72) or unsigned-SUM atomic (:100-148) */
+typedef enum { PACK_COPY, PACK_REDUCING, PACK_ATOMIC } op_packer_t;
+static const char *const packer_name[] = {"copy", "reducing", "atomic"};
+
 static const char *const method_name[] = {
     "REDUCE_RECURSIVE", "REDUCE_TERMINAL", "SEND_TO_SM_ROOT", "SEND_TERMINAL",
     "RECV_TERMINAL"
@@ -282,6 +418,9 @@ typedef struct {
     unsigned    recv_cnt;         /* endpoints received from */
     unsigned    recv_peers[UCG_BUILTIN_OPS_MAX_MEMBERS];  /* describe only */
     int         send_recv_buffer; /* 0: send.buffer, 1: recv.buffer */
+    int         incast;           /* sends / receives go through the incast */
+    uint8_t     packer;           /* op_packer_t of an incast send */
+    unsigned    incast_expected;  /* children packing each incast message */
     size_t      frag_len;         /* 0: single message */
     uint64_t    frags;            /* messages per endpoint */
     uint64_t    fragments_total;  /* recv_cnt x frags */
@@ -301,6 +440,7 @@ struct ucg_builtin_lgroup {
     ucg_builtin_combine_t   *cmb;
     op_slot_t                slots[UCG_BUILTIN_OPS_MAX_CONCURRENT];
     uint8_t                  next_coll_id;
+    int                      incast;   /* UCX_BUILTIN_SM_INCAST */
     uint64_t                 stats[4];
 };
 
@@ -429,6 +569,75 @@ static void step_complete(ucg_builtin_lcoll_t *c)
     }
 }
 
+typedef struct {
+    ucg_builtin_lcoll_t *c;
+    const char          *src;
+    size_t               length;
+    ucs_status_t         status;
+} pack_arg_t;
+
+/* UCG_BUILTIN_REDUCING_PACK_CB, builtin_pack.c:50-72: the first child's data
+ * is copied, every later child's is reduced into the transport buffer,
+ * dst = mine (op) dst, through ucg_builtin_atomic_reduce_part (:22-28) - here
+ * the combine dispatcher (device for large classified fragments). */
+static void pack_reducing(void *arg, void *dest, int reducing)
+{
+    pack_arg_t *a = arg;
+    ucg_builtin_lcoll_t *c = a->c;
+    if (!reducing) {
+        memcpy(dest, a->src, a->length);
+        return;
+    }
+    a->status = ucg_builtin_combine_reduce(c->g->cmb, c->op, (void*)a->src, dest,
+                                           (int)(a->length / c->dt_len), c->dtype);
+}
+
+/* UCG_BUILTIN_ATOMIC_{SINGLE,MULTIPLE}_PACK_CB, builtin_pack.c:100-148, for
+ * unsigned-integer SUM: ucs_atomic_add of each element into the zeroed cell.
+ * Unlike the reference's "multiple" packer (which adds send_buffer[0] to every
+ * element, :119-122) element i adds element i. */
+static void pack_atomic(void *arg, void *dest, int reducing)
+{
+    pack_arg_t *a = arg;
+    size_t i, n = a->length / a->c->dt_len;
+    (void)reducing;
+#define ADD_ALL(T)                                                            \
+    for (i = 0; i < n; i++) {                                                 \
+        T v;                                                                  \
+        memcpy(&v, a->src + i * sizeof(T), sizeof(T));                        \
+        __atomic_fetch_add((T*)dest + i, v, __ATOMIC_RELAXED);                \
+    }
+    switch (a->c->dt_len) {
+    case 1: ADD_ALL(uint8_t);  break;
+    case 2: ADD_ALL(uint16_t); break;
+    case 4: ADD_ALL(uint32_t); break;
+    case 8: ADD_ALL(uint64_t); break;
+    default: a->status = UCS_ERR_UNSUPPORTED; break;
+    }
+#undef ADD_ALL
+}
+
+/* one message of a step to one endpoint: uct_ep_am_short, or the incast
+ * bcopy with the step's packer */
+static ucs_status_t send_one(ucg_builtin_lcoll_t *c, const op_step_t *s,
+                             unsigned peer, uint64_t header, const char *buf,
+                             size_t n)
+{
+    pack_arg_t a;
+    ucs_status_t st;
+    if (!s->incast) {
+        return ucg_builtin_shm_am_short(c->g->iface, peer, header, buf, n);
+    }
+    a.c = c;
+    a.src = buf;
+    a.length = n;
+    a.status = UCS_OK;
+    st = ucg_builtin_shm_am_incast(c->g->iface, peer, header, s->incast_expected, n,
+                                   s->packer == PACK_ATOMIC ? pack_atomic : pack_reducing,
+                                   &a, s->packer == PACK_ATOMIC);
+    return (st == UCS_OK) ? a.status : st;
+}
+
 /* ucg_builtin_step_execute, builtin_data.c:411-668: send every fragment to
  * every endpoint of the step (endpoint-major, resumable at iter_ep /
  * iter_offset after UCS_ERR_NO_RESOURCE, :470-517 and ucg_builtin_step_
@@ -467,8 +676,7 @@ static void step_execute(ucg_builtin_lcoll_t *c)
         if (s->frag_len == 0) {
             if (c->iter_offset == 0) {
                 h.remote_offset = 0;
-                st = ucg_builtin_shm_am_short(g->iface, peer, h.header, sbuf,
-                                              c->length);
+                st = send_one(c, s, peer, h.header, sbuf, c->length);
                 if (st == UCS_ERR_NO_RESOURCE) {
                     c->send_pending = 1;  /* ucg_builtin_req_enqueue_resend */
                     return;
@@ -486,8 +694,7 @@ static void step_execute(ucg_builtin_lcoll_t *c)
                     n = s->frag_len;
                 }
                 h.remote_offset = (uint32_t)c->iter_offset;
-                st = ucg_builtin_shm_am_short(g->iface, peer, h.header,
-                                              sbuf + c->iter_offset, n);
+                st = send_one(c, s, peer, h.header, sbuf + c->iter_offset, n);
                 if (st == UCS_ERR_NO_RESOURCE) {
                     c->send_pending = 1;
                     return;
@@ -595,6 +802,10 @@ ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
     g->size     = member_count;
     g->my       = my_index;
     g->cmb      = combine;
+    {
+        const char *e = getenv("UCX_BUILTIN_SM_INCAST");
+        g->incast = e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1');
+    }
     iface->groups[group_id % UNEXP_GROUPS] = g;
     /* adopt messages that arrived before the group existed (builtin.c:
      * 424-446) */
@@ -759,6 +970,18 @@ static ucs_status_t plan_tree(ucg_builtin_lcoll_t *c, int fanout)
     s->send_recv_buffer = 0;
     if (step_fragments(c, s) != UCS_OK) {
         return UCS_ERR_UNSUPPORTED;
+    }
+    /* SM-root reduce (is_sm_reduce, builtin_control.c:535-537): with the
+     * incast transport the children pack into one message per fragment */
+    if (g->incast && ppn > 2) {
+        s->incast = 1;
+        if (is_root) {
+            s->fragments_total = s->frags;
+        } else {
+            s->incast_expected = nchild;
+            s->packer = ucg_builtin_combine_atomic_sum_length(g->cmb, c->op, c->dtype)
+                        ? PACK_ATOMIC : PACK_REDUCING;
+        }
     }
     if (!fanout) {
         return UCS_OK;
@@ -996,6 +1219,9 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             for (e = 0; e < s->recv_cnt; e++) {
                 PUT(" %u", s->recv_peers[e]);
             }
+        }
+        if (s->incast) {
+            PUT(s->send_cnt ? ", incast (%s packer)" : ", incast", packer_name[s->packer]);
         }
         PUT(", fragment length %zu, fragments per endpoint %llu, "
             "fragments total %llu, aggregation %s\n",

@@ -50,6 +50,7 @@ HOST_API = {
     "ucg_builtin_recursive_steps": (_u, [_u64, _u]),
     "ucg_builtin_recursive_peer": (_u64, [_u64, _u, _u, _u]),
     "ucg_builtin_combine_dtype_length": (_sz, [_vp, _vp]),
+    "ucg_builtin_combine_atomic_sum_length": (_sz, [_vp, _vp, _vp]),
     # include/ucg_builtin_ops.h
     "ucg_builtin_shm_iface_open": (_int, [ctypes.c_char_p, _u, _u, _sz, _u,
                                           ctypes.POINTER(_vp)]),
@@ -58,6 +59,7 @@ HOST_API = {
     "ucg_builtin_shm_am_short": (_int, [_vp, _u, _u64, _vp, _sz]),
     "ucg_builtin_shm_progress": (_u, [_vp, _vp, _vp]),
     "ucg_builtin_shm_barrier": (None, [_vp]),
+    "ucg_builtin_shm_am_incast": (_int, [_vp, _u, _u64, _u, _sz, _vp, _vp, _int]),
     "ucg_builtin_lgroup_create": (_int, [_vp, ctypes.c_uint16, _u, _u, _vp,
                                          ctypes.POINTER(_vp)]),
     "ucg_builtin_lgroup_destroy": (None, [_vp]),
