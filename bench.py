@@ -95,16 +95,24 @@ def cpu_baseline(count, budget_s=10.0):
 def c1_loopback(ranks=4, iters=20000):
     """BASELINE config 1 on this host's CPUs: 4 processes allreduce 4 KiB fp32
     through the builtin operation engine over the shared-memory transport
-    (tests/c/c1_allreduce.c; host combine, no GPU). Latency per allreduce."""
+    (tests/c/c1_allreduce.c; host combine, no GPU). Latency per allreduce.
+    max_short_*: the reference's plan for 4 members (recursive doubling);
+    tree_*: the tree plan forced on 4 members, plain and with the SM-root
+    incast packers; tree_3_ranks: the non-power-of-two case."""
     import subprocess
     import uuid
     exe = os.path.join(ROOT, "tests", "c", "_build", "c1_allreduce")
+    variants = [("max_short_256", ranks, 256, {}), ("max_short_8192", ranks, 8192, {}),
+                ("tree_max_short_256", ranks, 256, {"UCX_BUILTIN_ALLREDUCE_PLAN": "tree"}),
+                ("tree_incast_max_short_256", ranks, 256,
+                 {"UCX_BUILTIN_ALLREDUCE_PLAN": "tree", "UCX_BUILTIN_SM_INCAST": "y"}),
+                ("tree_3_ranks_max_short_256", 3, 256, {})]
     res = {}
-    for max_short in (256, 8192):
+    for key, world, max_short, extra_env in variants:
         name = f"ucg_bench_c1_{os.getpid()}_{uuid.uuid4().hex[:6]}"
         procs = []
-        for r in range(ranks):
-            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(ranks))
+        for r in range(world):
+            env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), **extra_env)
             procs.append(subprocess.Popen([exe, name, str(iters), str(max_short)], env=env,
                                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                           text=True))
@@ -116,9 +124,9 @@ def c1_loopback(ranks=4, iters=20000):
                 p.kill()
                 outs.append(p.communicate()[0] + " <timeout>")
         try:
-            res[f"max_short_{max_short}"] = json.loads(outs[0].strip().splitlines()[-1])
+            res[key] = json.loads(outs[0].strip().splitlines()[-1])
         except (ValueError, IndexError):
-            res[f"max_short_{max_short}"] = {"error": outs[0][-300:]}
+            res[key] = {"error": outs[0][-300:]}
     return res
 
 

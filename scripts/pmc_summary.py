@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""HBM bytes per launch of the headline combine kernel from the two rocprofv3
+PMC passes (FETCH_SIZE and WRITE_SIZE, collected separately).
+
+    python scripts/pmc_summary.py <fetch.csv> <write.csv> [out.json]
+
+Corrections per MI355X_MICROARCH.md (HBM / rocprofv3 section): counter unit is
+KB = 1024 B; gfx950 reports half the bytes of 16-B/lane streaming reads in
+FETCH_SIZE, so it is doubled; WRITE_SIZE is taken as is. Only launches of the
+2^26-element fp32 SUM kernel (grid 2^24 threads) are used; the median over
+launches is reported."""
+import csv
+import json
+import statistics
+import sys
+
+KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64>"
+COUNT = 1 << 26
+GRID = COUNT // 4          # one 16-B vector (4 fp32) per lane
+
+
+def values(path, counter):
+    out = []
+    for r in csv.DictReader(open(path)):
+        if KERNEL in r["Kernel_Name"] and int(r["Grid_Size"]) == GRID and \
+                r["Counter_Name"] == counter:
+            out.append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    fetch, write = values(sys.argv[1], "FETCH_SIZE"), values(sys.argv[2], "WRITE_SIZE")
+    if not fetch or not write:
+        sys.exit("no launches of the headline kernel in the PMC files")
+    f_kb, w_kb = statistics.median(fetch), statistics.median(write)
+    hbm = int(round((2 * f_kb + w_kb) * 1024))
+    alg = 3 * 4 * COUNT
+    res = {str(COUNT): {
+        "kernel": KERNEL, "grid_threads": GRID, "launches": [len(fetch), len(write)],
+        "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
+        "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
+        "ratio_to_algorithmic": round(hbm / alg, 5),
+        "correction": "FETCH_SIZE doubled (gfx950 reports half the bytes of 16-B/lane "
+                      "streaming reads, MI355X_MICROARCH.md SS HBM); WRITE_SIZE taken as is; "
+                      "KB = 1024 B",
+        "source": " / ".join(sys.argv[1:3])}}
+    text = json.dumps(res, indent=1)
+    if len(sys.argv) > 3:
+        open(sys.argv[3], "w").write(text + "\n")
+    print(text)
+
+
+if __name__ == "__main__":
+    main()

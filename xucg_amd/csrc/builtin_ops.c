@@ -249,11 +249,17 @@ ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *it, unsigned peer
 
 static void spin_lock(_Atomic uint32_t *l)
 {
+    unsigned spins = 0;
     uint32_t z = 0;
     while (!atomic_compare_exchange_weak_explicit(l, &z, 1, memory_order_acquire,
                                                   memory_order_relaxed)) {
         z = 0;
-        sched_yield();
+        /* the holder packs at most one fragment: spin briefly, then yield */
+        if (++spins < 256) {
+            __builtin_ia32_pause();
+        } else {
+            sched_yield();
+        }
     }
 }
 
@@ -277,9 +283,12 @@ ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *it, unsigned roo
     if (length + 8 > it->max_short) {
         return UCS_ERR_INVALID_PARAM;
     }
-    /* the cell of this message: a multiplicative hash of the whole header, so
-     * consecutive fragments (remote_offset) and ops (coll_id) spread out */
-    idx = (unsigned)(((header * 0x9E3779B97F4A7C15ull) >> 32) % it->cells);
+    /* the cell of this message: consecutive fragments of one message
+     * (remote_offset in steps of at most max_short - 8) take consecutive
+     * cells from a start that a multiplicative hash of the rest of the
+     * header (group, coll_id, step) spreads out */
+    idx = (unsigned)((((header & 0xffffffffull) * 0x9E3779B97F4A7C15ull) >> 40) +
+                     (header >> 32) / (it->max_short - 8)) % it->cells;
     c   = incast_cell(it, root, idx);
     spin_lock(&c->lock);
     /* acquire: the root's reads of a delivered cell precede our writes */
