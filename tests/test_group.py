@@ -1,5 +1,7 @@
 """Multi-rank paths: shard math, the reference recursive-doubling plan over
 gloo (CPU, world 2 and 4), and the peer-mapped one-shot kernel (GPU)."""
+import os
+
 import pytest
 
 from xucg_amd import group as G
@@ -36,3 +38,29 @@ def test_recursive_doubling_plan_over_gloo(world):
 def test_oneshot_reduce_scatter_over_ipc(world):
     codes, outs = launch("_worker_ipc.py", world, timeout=300)
     assert codes == [0] * world, "\n".join(outs)
+
+
+@pytest.mark.gpu
+def test_bench_collective_phases_world1():
+    """bench.py's N > 1 collective phases (C4 RCCL RS+AG, one-shot xGMI RS
+    with its parity check, C5 recursive doubling with its parity check) run
+    under torch.distributed.run at world 1 (only 1-GPU boxes are available to
+    the tests; the driver runs N = 2..8)."""
+    import json
+    import subprocess
+    import sys
+    from _launch import ROOT, free_port
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline", "--no-extra", "--collective-force"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    coll = line["collective"]
+    assert coll, line
+    for name, res in coll.items():
+        assert isinstance(res, dict) and "error" not in res, (name, res)
+    assert coll["c4_oneshot_xgmi_rs_4gib_fp32"]["bit_exact_vs_rccl_on_exact_inputs"] is True
+    c5 = [v for k, v in coll.items() if k.startswith("c5")][0]
+    assert any(v is True for k, v in c5.items() if "bit_exact" in k), c5
