@@ -130,6 +130,9 @@ def c1_loopback(ranks=4, iters=20000):
     return res
 
 
+XGMI_GBS = 7 * 153.0   # aggregate xGMI per MI355X
+
+
 def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     """BASELINE configs 4 and 5 across the N GPUs of the node (N > 1 only).
 
@@ -139,11 +142,16 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             all N peer-mapped buffers and combines them in the reference
             plan's association (ucg_builtin_dev_reduce_multi), then RCCL
             all-gather; parity vs (a) on exact-integer inputs (bit-exact)
-    C5: the reference recursive-doubling allreduce (builtin_recursive.c:
-        158-169) of 512 MiB fp64 per GPU: RCCL send/recv of the whole
-        accumulator + device combine per step; parity: bit-exact against a
-        local one-shot evaluation of the same association
-    busBW = (N-1)/N x S / t per collective. Every phase is
+    C5: allreduce of 512 MiB fp64 per GPU, device combine per step:
+        (a) the reference recursive-doubling plan (builtin_recursive.c:
+            158-169): RCCL send/recv of the whole accumulator per step;
+        (b) recursive halving + doubling with the plan's peer order (same
+            per-element association, 2 (N-1)/N x S sent per rank);
+        parity of both: bit-exact against a local one-shot evaluation of the
+        plan's association; (c) RCCL all_reduce, checked against the
+        SURVEY.md 8c tolerance
+    busBW = (N-1)/N x S / t per collective, also as a fraction
+    of the aggregate xGMI bandwidth (7 x 153 GB/s per GPU). Every phase is
     guarded; an error is recorded in the JSON instead of aborting the line."""
     import torch
     from xucg_amd import group as G
@@ -195,7 +203,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         return {"bytes": s_bytes, "rs_ms": round(t_rs * 1e3, 3),
                 "ag_ms": round(t_ag * 1e3, 3),
                 "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
-                "ag_busbw_gbs": round(bus / t_ag / 1e9, 1)}
+                "ag_busbw_gbs": round(bus / t_ag / 1e9, 1),
+                "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4)}
     agreed(rccl, "c4_rccl_rs_ag_4gib_fp32")
 
     def oneshot():
@@ -216,14 +225,35 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             torch.cuda.synchronize()
             same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
             t_ag = timed(lambda: dist.all_gather_into_tensor(ag_out, mine), steps)
+            # rounded inputs: RCCL's ring order vs the plan's association,
+            # SURVEY.md 8c bound |delta| <= 2 (n-1) u sum_i |x_i|, u = 2^-24
+            torch.cuda.synchronize()
+            dist.barrier()
+            ctx.fill("float32", "round", 0x5EED4100 + rank, x, n4)
+            torch.cuda.synchronize()
+            dist.barrier()
+            rs()
+            dist.reduce_scatter_tensor(rs_out, x)
+            absx = x.abs()
+            abs_rs = torch.empty_like(rs_out)
+            dist.reduce_scatter_tensor(abs_rs, absx)
+            del absx
+            tol = 2 * (world - 1) * 2.0 ** -24 * abs_rs
+            err = (mine - rs_out).abs()
+            within = bool((err <= tol).all())
+            ratio = float((err / tol.clamp_min(1e-30)).max())
+            del abs_rs, tol, err
         finally:
             torch.cuda.synchronize()
             dist.barrier()
             peers.close()
         return {"bytes": s_bytes, "rs_ms": round(t_rs * 1e3, 3),
                 "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
+                "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4),
                 "rs_ag_ms": round((t_rs + t_ag) * 1e3, 3),
                 "bit_exact_vs_rccl_on_exact_inputs": same,
+                "rccl_within_8c_tolerance_on_rounded_inputs": within,
+                "max_err_over_tolerance": round(ratio, 4),
                 "association": "recursive doubling (builtin_recursive.c:158-169)"}
     agreed(oneshot, "c4_oneshot_xgmi_rs_4gib_fp32")
     del x, rs_out, ag_out
@@ -231,7 +261,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
 
     def recursive_doubling():
         if world & (world - 1):
-            return {"skipped": "recursive doubling needs a power-of-two group"}
+            return {"skipped": "recursive doubling / halving need a power-of-two group"}
         n5 = 1 << 26                  # 512 MiB fp64 per rank (config 5)
         init = torch.empty(n5, dtype=torch.float64, device=dev)
         ctx.fill("float64", "round", 0x5EED5000 + rank, init, n5)
@@ -242,11 +272,18 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         def combine(a, t):
             ctx.reduce_checked("sum", "float64", a, t, n5)
 
+        def combine_n(a, t, n):
+            ctx.reduce_checked("sum", "float64", a, t, n)
+
         def once():
             acc.copy_(init)           # ucg_builtin_init_reduce: recv <- send
             G.recursive_doubling_allreduce(acc, tmp, rank, world, combine, exchange)
-        once()
-        torch.cuda.synchronize()
+
+        def once_halving():
+            acc.copy_(init)
+            G.recursive_halving_allreduce(acc, tmp, rank, world, combine_n, exchange,
+                                          n5, 8)
+
         # parity: every member's input regenerated locally, one-shot tree
         allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
         for r in range(world):
@@ -254,17 +291,41 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         ref = torch.empty_like(init)
         _lib_check = ctx.reduce_multi("sum", "float64", ref, allx, rank, n5)
         ctx.sync()
-        same = _lib_check == 0 and bool(torch.equal(acc.view(torch.int64),
-                                                    ref.view(torch.int64)))
-        del allx, ref
-        t = timed(once, steps)
-        steps_n = G.recursive_steps(world)
-        return {"bytes_per_rank": n5 * 8, "ms": round(t * 1e3, 3),
-                "steps": steps_n,
-                "algbw_gbs": round(n5 * 8 / t / 1e9, 1),
-                "link_gbs_per_step": round(n5 * 8 * steps_n / t / 1e9, 1),
-                "bit_exact_vs_oneshot_tree": same}
-    agreed(recursive_doubling, "c5_recursive_doubling_512mib_fp64")
+        del allx
+        res = {"bytes_per_rank": n5 * 8, "steps": G.recursive_steps(world)}
+        for name, fn, link_bytes in (
+                ("doubling", once, n5 * 8 * G.recursive_steps(world)),
+                ("halving", once_halving, 2 * (world - 1) * n5 * 8 // world)):
+            fn()
+            torch.cuda.synchronize()
+            same = _lib_check == 0 and bool(torch.equal(acc.view(torch.int64),
+                                                        ref.view(torch.int64)))
+            for _ in range(warmup):
+                fn()
+            t = timed(fn, steps)
+            res[name] = {"ms": round(t * 1e3, 3),
+                         "algbw_gbs": round(n5 * 8 / t / 1e9, 1),
+                         "sent_bytes_per_rank": link_bytes,
+                         "link_gbs": round(link_bytes / t / 1e9, 1),
+                         "bit_exact_vs_oneshot_tree": same}
+        # vendor baseline on the same buffer (ring association: tolerance only)
+        acc.copy_(init)
+        dist.all_reduce(acc)
+        torch.cuda.synchronize()
+        # |delta| <= 2 (n-1) u sum_i |x_i|, u = 2^-53
+        absx = init.abs()
+        dist.all_reduce(absx)
+        tol = 2 * (world - 1) * 2.0 ** -53 * absx
+        err = (acc - ref).abs()
+        res["rccl_allreduce_within_8c_tolerance_of_plan"] = bool((err <= tol).all())
+        res["rccl_allreduce_max_abs_err_over_tol"] = float((err / tol.clamp_min(1e-300)).max())
+        del absx, tol, err
+        t = timed(lambda: dist.all_reduce(acc), steps)
+        res["rccl_allreduce"] = {"ms": round(t * 1e3, 3),
+                                 "algbw_gbs": round(n5 * 8 / t / 1e9, 1)}
+        del ref
+        return res
+    agreed(recursive_doubling, "c5_recursive_allreduce_512mib_fp64")
     return out
 
 

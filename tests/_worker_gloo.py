@@ -40,6 +40,25 @@ def main():
         if not (O.bits(got) == O.bits(want)).all():
             print(f"rank {rank}: MISMATCH {dt} {op} {dist_name}", flush=True)
             sys.exit(1)
+        # recursive halving: every element equals the plan's result on the
+        # member that owns it after the reduce-scatter (all ranks identical)
+        acc2 = torch.from_numpy(inputs[rank].view(np.uint8).copy())
+        tmp2 = torch.empty_like(acc2)
+        size = np.dtype(st).itemsize
+
+        def combine_n(d, t, cnt):
+            dv = d.numpy().view(st)
+            dv[:] = O.reduce(op, dt, t.numpy().view(st), dv)
+
+        G.recursive_halving_allreduce(acc2, tmp2, rank, world, combine_n, exchange, n, size)
+        got2 = acc2.numpy().view(st)
+        for owner, (lo, hi) in enumerate(G.recursive_halving_segments(n, world,
+                                                                       max(1, 256 // size))):
+            want_o = O.reduce_multi(op, dt, inputs, owner)
+            if not (O.bits(got2[lo:hi]) == O.bits(want_o[lo:hi])).all():
+                print(f"rank {rank}: halving MISMATCH {dt} {op} {dist_name} owner {owner}",
+                      flush=True)
+                sys.exit(1)
         # the one-shot shard of this rank equals the plan's result on it
         lo, hi, shard = G.oracle_shard(op, dt, inputs, rank, world, O)
         if not (O.bits(shard) == O.bits(want[lo:hi])).all():

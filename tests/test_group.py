@@ -27,7 +27,16 @@ def test_recursive_steps_and_peers():
     assert [G.recursive_peer(5, s) for s in (1, 2, 3)] == [4, 7, 1]
 
 
-@pytest.mark.parametrize("world", [2, 4])
+def test_recursive_halving_segments_partition():
+    for count in (1, 7, 1001, 1 << 20):
+        for world in (1, 2, 4, 8):
+            segs = G.recursive_halving_segments(count, world, 32)
+            covered = sorted(segs)
+            assert covered[0][0] == 0 and covered[-1][1] == count
+            assert all(a[1] == b[0] for a, b in zip(covered, covered[1:]))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_recursive_doubling_plan_over_gloo(world):
     codes, outs = launch("_worker_gloo.py", world, timeout=240)
     assert codes == [0] * world, "\n".join(outs)
@@ -61,6 +70,10 @@ def test_bench_collective_phases_world1():
     assert coll, line
     for name, res in coll.items():
         assert isinstance(res, dict) and "error" not in res, (name, res)
-    assert coll["c4_oneshot_xgmi_rs_4gib_fp32"]["bit_exact_vs_rccl_on_exact_inputs"] is True
-    c5 = [v for k, v in coll.items() if k.startswith("c5")][0]
-    assert any(v is True for k, v in c5.items() if "bit_exact" in k), c5
+    c4 = coll["c4_oneshot_xgmi_rs_4gib_fp32"]
+    assert c4["bit_exact_vs_rccl_on_exact_inputs"] is True, c4
+    assert c4["rccl_within_8c_tolerance_on_rounded_inputs"] is True, c4
+    c5 = coll["c5_recursive_allreduce_512mib_fp64"]
+    assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
+    assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5
+    assert c5["rccl_allreduce_within_8c_tolerance_of_plan"] is True, c5

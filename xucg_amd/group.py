@@ -1,7 +1,7 @@
 """Multi-rank execution of the combine path: one process per GPU.
 
 torch.distributed is the plumbing (RCCL over xGMI on the GPU box, gloo for
-CPU tests); every combine runs through the C-ABI device shim. Three ways to
+CPU tests); every combine runs through the C-ABI device shim. Four ways to
 allreduce a buffer across 2^k members, all built on the same combine:
 
   recursive_doubling_allreduce  the reference plan itself
@@ -16,6 +16,15 @@ allreduce a buffer across 2^k members, all built on the same combine:
                                 (ucg_builtin_dev_reduce_multi); followed by an
                                 all-gather. Bit-exact with the plan's result
                                 on the shard owner.
+  recursive_halving_allreduce   reduce-scatter by recursive halving with the
+                                plan's peer order (my ^ 1, my ^ 2, ...) then
+                                all-gather by recursive doubling (SURVEY.md 8e,
+                                config 5). Every element gets the plan's
+                                association on the member that ends up owning
+                                it, so the result equals the plan's bit for bit
+                                (for a commutative op without NaN payload
+                                choices, on every member); it moves
+                                2 (N-1)/N x S per member instead of log2(N) x S.
   RCCL reduce_scatter + all_gather  the vendor baseline (ring association:
                                 within the fp tolerance of SURVEY.md 8c only).
 """
@@ -67,6 +76,66 @@ def recursive_doubling_allreduce(acc, tmp, rank, world, combine, exchange):
         peer = recursive_peer(rank, step)
         exchange(acc, tmp, peer)
         combine(acc, tmp)
+
+
+def _halve(lo, hi, align):
+    half = (hi - lo) // 2
+    if half >= align:
+        half -= half % align
+    return lo + half
+
+
+def recursive_halving_segments(count, world, align=1):
+    """Element range [lo, hi) each member owns after the halving
+    reduce-scatter (member bit k set: upper half at step k+1)."""
+    steps = recursive_steps(world)
+    out = []
+    for rank in range(world):
+        lo, hi = 0, count
+        for k in range(steps):
+            mid = _halve(lo, hi, align)
+            lo, hi = (mid, hi) if rank & (1 << k) else (lo, mid)
+        out.append((lo, hi))
+    return out
+
+
+def recursive_halving_allreduce(acc, tmp, rank, world, combine, exchange, count,
+                                elem_size, align_bytes=SHARD_ALIGN_BYTES):
+    """Recursive halving reduce-scatter + recursive doubling all-gather.
+
+    acc, tmp  1-D tensors holding `count` elements of `elem_size` bytes (any
+              torch dtype whose size divides elem_size)
+    combine   combine(dst, src, n): dst = src (op) dst over n elements
+    exchange  exchange(send, recv, peer): paired send/receive (lengths may
+              differ by the odd element of a split)
+    """
+    if world == 1:
+        return
+    steps = recursive_steps(world)
+    if steps == 0:
+        raise ValueError("recursive halving needs a power-of-two group")
+    per = elem_size // acc.element_size()
+    align = max(1, align_bytes // elem_size) if align_bytes % elem_size == 0 else 1
+
+    def seg(t, lo, hi):
+        return t.narrow(0, lo * per, (hi - lo) * per)
+
+    lo, hi = 0, count
+    ranges = []
+    for k in range(steps):                      # peers my^1, my^2, my^4, ...
+        peer = rank ^ (1 << k)
+        mid = _halve(lo, hi, align)
+        keep, give = ((mid, hi), (lo, mid)) if rank & (1 << k) else ((lo, mid), (mid, hi))
+        exchange(seg(acc, *give), seg(tmp, *keep), peer)
+        combine(seg(acc, *keep), seg(tmp, *keep), keep[1] - keep[0])
+        ranges.append((lo, hi))
+        lo, hi = keep
+    for k in reversed(range(steps)):            # all-gather: WRITE into acc
+        peer = rank ^ (1 << k)
+        plo, phi = ranges[k]
+        theirs = (plo, lo) if lo > plo else (hi, phi)
+        exchange(seg(acc, lo, hi), seg(acc, *theirs), peer)
+        lo, hi = plo, phi
 
 
 def torch_exchange(dist, group=None):
