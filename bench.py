@@ -133,6 +133,21 @@ def c1_loopback(ranks=4, iters=20000):
 XGMI_GBS = 7 * 153.0   # aggregate xGMI per MI355X
 
 
+def staged_step(total=64 << 20, frag=8184, reps=5):
+    """Row f1's device staging from C (tests/c/stage_bench.c): one fragmented
+    fp32 SUM step, one ucg_builtin_dev_combine per 8 KiB AM fragment between
+    stage_begin/stage_end, pageable host buffers, beside the 1-thread CPU
+    combine issued per fragment. Child process; bit-exact check inside."""
+    import subprocess
+    exe = os.path.join(ROOT, "tests", "c", "_build", "stage_bench")
+    try:
+        p = subprocess.run([exe, str(total), str(frag), str(reps)], capture_output=True,
+                           text=True, timeout=120)
+        return json.loads(p.stdout.strip().splitlines()[-1])
+    except Exception as e:  # reported, never fatal for the bench line
+        return {"error": f"{type(e).__name__}: {e}"[:300]}
+
+
 def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     """BASELINE configs 4 and 5 across the N GPUs of the node (N > 1 only).
 
@@ -442,6 +457,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(n)
         extra["c1_loopback_allreduce_4kib_fp32"] = c1_loopback()
+        extra["f1_staged_step_64mib_fp32"] = staged_step()
 
     if rank == 0:
         line = {

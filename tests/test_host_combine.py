@@ -213,3 +213,18 @@ def test_atomic_packer_condition():
         assert f(cmb.handle, OPS["sum"], DTYPES[dt]) == want, dt
         assert f(cmb.handle, OPS["max"], DTYPES[dt]) == 0, dt
     cmb.close()
+
+
+@pytest.mark.gpu
+def test_stage_bench_c_harness_bit_exact():
+    """tests/c/stage_bench.c: a fragmented step staged on the device from C,
+    bit-exact against the oracle's per-fragment combine."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "c", "_build", "stage_bench")
+    p = subprocess.run([exe, str(3 << 20), "8184", "1"], capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["bit_exact"] is True and line["fragments"] == -(-(3 << 20) // 8184)
