@@ -55,7 +55,10 @@ typedef struct ucg_builtin_reduce_params {
 /* Builtin-private knobs, read from the environment with the builtin
  * planner's prefix (UCX_BUILTIN_, builtin/builtin.c:1015). */
 typedef struct ucg_builtin_combine_config {
-    int      dev_enable;     /* UCX_BUILTIN_DEV_COMBINE      y/n  (default y)  */
+    int      dev_enable;     /* UCX_BUILTIN_DEV_COMBINE n|y|force (0/1/2, y):
+                                y: device-resident buffers on the GPU, host
+                                buffers on reduce_cb_f; force: host buffers
+                                of >= dev_min_bytes are staged on the GPU too */
     size_t   dev_min_bytes;  /* UCX_BUILTIN_DEV_MIN_BYTES    (default 1 MiB)   */
     size_t   stage_bytes;    /* UCX_BUILTIN_DEV_STAGE_BYTES  (default 8 MiB)   */
     unsigned stage_slots;    /* UCX_BUILTIN_DEV_STAGE_SLOTS  (default 4)       */

@@ -153,6 +153,16 @@ const char *ucg_builtin_dev_last_error(void);
 /* Number of HIP devices visible (0 when none); never initialises a context. */
 int         ucg_builtin_dev_device_count(void);
 
+/* Where a buffer lives (hipPointerGetAttributes): the dispatcher keeps host
+ * buffers on the host CPU by default and sends device-resident ones (a
+ * GPU-aware MPI's recv buffer, an IPC-mapped peer) to the GPU. */
+enum {
+    UCG_DEV_MEM_HOST   = 0,   /* host memory unknown to HIP (pageable)    */
+    UCG_DEV_MEM_PINNED = 1,   /* host memory registered with / from HIP   */
+    UCG_DEV_MEM_DEVICE = 2    /* GPU memory (local, peer-mapped, managed) */
+};
+int         ucg_builtin_dev_mem_kind(const void *ptr);
+
 /* ---- per-group device context --------------------------------------------*/
 ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *params,
                                         ucg_builtin_dev_ctx_t **ctx_p);
@@ -182,10 +192,11 @@ ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
                                           size_t count);
 
 /* ---- host-resident combine (the reduce_cb_f contract, staged) ------------*/
-/* Whole-buffer: dst_host[i] = src_host[i] (op) dst_host[i]. Chunks are copied
- * H2D, combined and copied back D2H on two streams, overlapped. Pinned host
- * buffers are DMA'd directly; pageable ones go through the pinned ring.
- * Returns when dst_host holds the result. */
+/* Whole-buffer: dst_host[i] = src_host[i] (op) dst_host[i]. Host chunks are
+ * copied H2D into the device ring, combined and copied back D2H on two
+ * streams, overlapped. An operand that is device memory is used in place (a
+ * device dst is combined in place, nothing is copied back). Returns when dst
+ * holds the result. */
 ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
                                           ucg_dev_op_t op, ucg_dev_dtype_t dt,
                                           void *dst_host, const void *src_host,
@@ -195,6 +206,9 @@ ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
  * mirrored on the device between stage_begin and stage_end; each fragment
  * combine copies the borrowed src into the pinned ring before returning and
  * consecutive fragments are aggregated into one launch per ring slot. */
+/* host_dst may also be device memory: the step then accumulates into it in
+ * place (no mirror copy either way). Fragments are always host memory (AM
+ * payloads). */
 ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
                                          void *host_dst, size_t bytes);
 ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,

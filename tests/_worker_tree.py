@@ -66,7 +66,7 @@ def main():
     world = int(os.environ["WORLD_SIZE"])
     mpi = MockMPI()
     if mode == "dev":
-        cfg = host.make_config(dev_enable=1, dev_min_bytes=0, stage_bytes=1 << 16)
+        cfg = host.make_config(dev_enable=2, dev_min_bytes=0, stage_bytes=1 << 16)
     else:
         cfg = host.make_config(dev_enable=0)
     cmb = host.BuiltinCombine(mpi.callbacks(), cfg, op_classifier=op_classifier,

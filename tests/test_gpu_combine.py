@@ -257,3 +257,21 @@ def test_profile_hook_and_counters(dev_ctx):
     assert 0 < us < 10_000
     assert after["launches"] - before["launches"] == 10
     assert after["combined_bytes"] - before["combined_bytes"] == 10 * 3 * n * 4
+
+
+@pytest.mark.gpu
+def test_mem_kind(dev_ctx):
+    """ucg_builtin_dev_mem_kind: pageable host 0, pinned host 1, device 2
+    (also at an interior offset of a device allocation)."""
+    from xucg_amd import _lib
+    f = _lib.dev().ucg_builtin_dev_mem_kind
+    a = np.zeros(64, np.float32)
+    hb = xucg_amd.HostBuffer(4096)
+    db = dev_ctx.alloc(4096)
+    try:
+        assert f(a.ctypes.data) == 0
+        assert f(hb.ptr) == 1
+        assert f(db.ptr) == 2 and f(db.ptr + 1000) == 2
+    finally:
+        hb.free()
+        db.free()

@@ -26,6 +26,8 @@ def test_config_from_environment(monkeypatch):
     c = host.read_config()
     assert (c.dev_enable, c.dev_min_bytes, c.stage_bytes, c.stage_slots, c.device) == \
         (0, 64 << 10, 2 << 20, 6, 3)
+    monkeypatch.setenv("UCX_BUILTIN_DEV_COMBINE", "force")
+    assert host.read_config().dev_enable == 2
     monkeypatch.delenv("UCX_BUILTIN_DEV_COMBINE")
     monkeypatch.delenv("UCX_BUILTIN_DEV_MIN_BYTES")
     c = host.read_config()
@@ -150,9 +152,9 @@ def test_recursive_factor3_peers_partition_the_group():
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt,op", [("float32", "sum"), ("float64", "sum"),
                                    ("int32", "max"), ("bfloat16", "prod")])
-def test_dispatcher_sends_large_calls_to_the_device(dt, op):
+def test_dispatcher_offloads_large_host_calls_when_forced(dt, op):
     mpi = MockMPI()
-    cfg = host.make_config(dev_enable=1, dev_min_bytes=1 << 16, stage_bytes=1 << 20)
+    cfg = host.make_config(dev_enable=2, dev_min_bytes=1 << 16, stage_bytes=1 << 20)
     cmb = host.BuiltinCombine(mpi.callbacks(), cfg, op_classifier=op_classifier,
                               dt_classifier=dt_classifier)
     assert cmb.has_device
@@ -179,7 +181,7 @@ def test_staged_step_on_device_matches_host_fallback():
     frag = host.fragment_length(8192, 4)
     src = O.fill("float32", "round", 3, n)
     results = []
-    for dev in (1, 0):
+    for dev in (2, 0):
         mpi = MockMPI()
         cfg = host.make_config(dev_enable=dev, dev_min_bytes=1 << 16, stage_bytes=1 << 20)
         cmb = host.BuiltinCombine(mpi.callbacks(), cfg)
@@ -228,3 +230,68 @@ def test_stage_bench_c_harness_bit_exact():
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["bit_exact"] is True and line["fragments"] == -(-(3 << 20) // 8184)
+
+
+@pytest.mark.gpu
+def test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu():
+    """UCX_BUILTIN_DEV_COMBINE=y (default): a host recv buffer is combined by
+    reduce_cb_f (staging would cross PCIe); a device-resident one
+    (GPU-aware MPI) on the GPU in place, whatever its size, with a host or a
+    device src; an op the device cannot classify is refused for device
+    memory (the host callback cannot dereference it)."""
+    import torch
+    from xucg_amd import _lib
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(), op_classifier=op_classifier,
+                              dt_classifier=dt_classifier)
+    assert cmb.has_device
+    n = (1 << 21) + 5
+    src = O.fill("float32", "round", 5, n)
+    dst = O.fill("float32", "round", 6, n)
+    want = O.reduce("sum", "float32", src, dst)
+    assert _lib.dev().ucg_builtin_dev_mem_kind(dst.ctypes.data) == 0
+    d = dst.copy()
+    assert cmb.reduce(OPS["sum"], src, d, n, DTYPES["float32"]) == 0
+    assert (O.bits(d) == O.bits(want)).all()
+    st = cmb.stats()
+    assert st["dev_calls"] == 0 and st["host_calls"] == 1
+    for small in (1, 100, n):
+        w = O.reduce("max", "float32", src[:small], dst[:small])
+        ddev = torch.from_numpy(dst[:small].copy()).cuda()
+        assert _lib.dev().ucg_builtin_dev_mem_kind(ddev.data_ptr()) == 2
+        for s_on_dev in (False, True):
+            dd = ddev.clone()
+            s = torch.from_numpy(src[:small].copy()).cuda() if s_on_dev else src[:small].copy()
+            torch.cuda.synchronize()
+            assert cmb.reduce(OPS["max"], s, dd, small, DTYPES["float32"]) == 0, \
+                xucg_amd._lib.last_error()
+            assert (O.bits(dd.cpu().numpy()) == O.bits(w)).all(), (small, s_on_dev)
+    assert cmb.stats()["host_calls"] == 1
+    ddev = torch.zeros(16, device="cuda")
+    assert cmb.reduce(OP_MINLOC, src[:16].copy(), ddev, 8, DT_DOUBLE_INT) != 0
+    cmb.close()
+
+
+@pytest.mark.gpu
+def test_staged_step_into_device_resident_recv_buffer():
+    """A fragmented step whose recv buffer is device memory accumulates into
+    it in place (no mirror copies), bit-exact with the host callback."""
+    import torch
+    n = (1 << 20) + 3
+    frag = host.fragment_length(8192, 4)
+    src = O.fill("float32", "round", 7, n)
+    acc0 = O.fill("float32", "round", 8, n)
+    want = O.reduce("sum", "float32", src, acc0, frag_bytes=frag)
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(stage_bytes=1 << 20))
+    acc = torch.from_numpy(acc0.copy()).cuda()
+    torch.cuda.synchronize()
+    assert cmb.step_begin(OPS["sum"], DTYPES["float32"], acc, acc0.nbytes) == 0
+    raw = src.view(np.uint8)
+    for off in range(0, acc0.nbytes, frag):
+        ln = min(frag, acc0.nbytes - off)
+        assert cmb.fragment(off, raw[off:off + ln], ln) == 0
+    assert cmb.step_end() == 0, xucg_amd._lib.last_error()
+    assert cmb.stats()["dev_steps"] == 1 and cmb.stats()["host_calls"] == 0
+    assert (O.bits(acc.cpu().numpy()) == O.bits(want)).all()
+    cmb.close()

@@ -57,6 +57,7 @@ DEV_API = {
     "ucg_builtin_dev_version": (ctypes.c_char_p, []),
     "ucg_builtin_dev_last_error": (ctypes.c_char_p, []),
     "ucg_builtin_dev_device_count": (_int, []),
+    "ucg_builtin_dev_mem_kind": (_int, [_vp]),
     "ucg_builtin_dev_ctx_create": (_st, [ctypes.POINTER(DevCtxParams),
                                          ctypes.POINTER(_vp)]),
     "ucg_builtin_dev_ctx_destroy": (None, [_vp]),

@@ -84,7 +84,11 @@ static int parse_bool(const char *s, int dflt)
 void ucg_builtin_combine_config_read(ucg_builtin_combine_config_t *cfg)
 {
     const char *dev = getenv("UCX_BUILTIN_DEV_DEVICE");
-    cfg->dev_enable    = parse_bool(getenv("UCX_BUILTIN_DEV_COMBINE"), 1);
+    {
+        const char *e = getenv("UCX_BUILTIN_DEV_COMBINE");
+        cfg->dev_enable = (e && (!strcasecmp(e, "force") || !strcmp(e, "2"))) ? 2 :
+                          parse_bool(e, 1);
+    }
     cfg->dev_min_bytes = parse_memunits(getenv("UCX_BUILTIN_DEV_MIN_BYTES"),
                                         1u << 20);
     cfg->stage_bytes   = parse_memunits(getenv("UCX_BUILTIN_DEV_STAGE_BYTES"),
@@ -277,6 +281,18 @@ static ucs_status_t host_reduce(ucg_builtin_combine_t *cmb, void *op, void *src,
     return UCS_OK;
 }
 
+/* Where a combine runs (measured on MI355X + EPYC 9575F): a
+ * device-resident accumulator always on the GPU (the host cannot touch it and
+ * nothing crosses PCIe); a host one on reduce_cb_f, because staging moves 3N
+ * bytes over PCIe (~22 GiB/s of N) while one host core combines at ~23 GiB/s
+ * of N - unless UCX_BUILTIN_DEV_COMBINE=force asks to offload it. */
+static int use_device(ucg_builtin_combine_t *cmb, int classified, int dst_on_dev,
+                      size_t bytes)
+{
+    return classified && (dst_on_dev ||
+                          (cmb->cfg.dev_enable == 2 && bytes >= cmb->cfg.dev_min_bytes));
+}
+
 ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
                                         void *reduce_op, void *src, void *dst,
                                         int dcount, void *datatype)
@@ -293,19 +309,28 @@ ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
         return UCS_OK;
     }
     pthread_mutex_lock(&cmb->lock);
-    if (cmb->dev && ucg_builtin_combine_classify(cmb, reduce_op, datatype, &op, &dt) &&
-        (bytes = (size_t)dcount * ucg_builtin_dev_dtype_size(dt)) >=
-            cmb->cfg.dev_min_bytes) {
-        st = ucg_builtin_dev_combine_host(cmb->dev, op, dt, dst, src,
-                                          (size_t)dcount);
-        if (st == UCS_OK) {
-            cmb->stats[2]++;
-            cmb->stats[3] += bytes;
+    if (cmb->dev) {
+        int on_dev = ucg_builtin_dev_mem_kind(dst) == UCG_DEV_MEM_DEVICE;
+        int cls    = ucg_builtin_combine_classify(cmb, reduce_op, datatype, &op, &dt);
+        if (on_dev && !cls) {
+            /* reduce_cb_f cannot dereference device memory */
+            pthread_mutex_unlock(&cmb->lock);
+            return UCS_ERR_UNSUPPORTED;
         }
-    } else {
-        st = host_reduce(cmb, reduce_op, src, dst, (unsigned)dcount, datatype,
-                         (size_t)dcount * dtype_length(cmb, datatype));
+        if (use_device(cmb, cls, on_dev,
+                       bytes = (size_t)dcount * ucg_builtin_dev_dtype_size(dt))) {
+            st = ucg_builtin_dev_combine_host(cmb->dev, op, dt, dst, src,
+                                              (size_t)dcount);
+            if (st == UCS_OK) {
+                cmb->stats[2]++;
+                cmb->stats[3] += bytes;
+            }
+            pthread_mutex_unlock(&cmb->lock);
+            return st;
+        }
     }
+    st = host_reduce(cmb, reduce_op, src, dst, (unsigned)dcount, datatype,
+                     (size_t)dcount * dtype_length(cmb, datatype));
     pthread_mutex_unlock(&cmb->lock);
     return st;
 }
@@ -335,14 +360,20 @@ ucs_status_t ucg_builtin_combine_step_begin(ucg_builtin_combine_t *cmb,
         pthread_mutex_unlock(&cmb->lock);
         return UCS_ERR_INVALID_PARAM;
     }
-    if (cmb->dev && length >= cmb->cfg.dev_min_bytes &&
-        ucg_builtin_combine_classify(cmb, reduce_op, datatype, &cmb->step.dop,
-                                     &cmb->step.ddt)) {
-        st = ucg_builtin_dev_stage_begin(cmb->dev, recv_buffer, length);
-        if (st == UCS_OK) {
-            cmb->step.on_dev = 1;
-            cmb->stats[4]++;
-        } else {
+    if (cmb->dev && length) {
+        int on_dev = ucg_builtin_dev_mem_kind(recv_buffer) == UCG_DEV_MEM_DEVICE;
+        int cls    = ucg_builtin_combine_classify(cmb, reduce_op, datatype,
+                                                  &cmb->step.dop, &cmb->step.ddt);
+        if (on_dev && !cls) {
+            st = UCS_ERR_UNSUPPORTED;   /* reduce_cb_f cannot touch it */
+        } else if (use_device(cmb, cls, on_dev, length)) {
+            st = ucg_builtin_dev_stage_begin(cmb->dev, recv_buffer, length);
+            if (st == UCS_OK) {
+                cmb->step.on_dev = 1;
+                cmb->stats[4]++;
+            }
+        }
+        if (st != UCS_OK) {
             cmb->step.active = 0;
         }
     }

@@ -309,11 +309,14 @@ struct ucg_builtin_dev_ctx {
     bool        *slot_used;
     unsigned     next_slot;
 
-    /* per-step accumulator mirror */
+    /* per-step accumulator: a device mirror of a host recv buffer, or the
+     * recv buffer itself when it is device memory (acc_in_place) */
     void        *host_dst;
     size_t       stage_len;
     char        *d_acc;
     size_t       d_acc_cap;
+    char        *acc;
+    bool         acc_in_place;
 
     /* pending fragment runs, each aggregated into one launch and flushed in
      * the order they were started (see ucg_builtin_dev_combine) */
@@ -392,6 +395,28 @@ const char *ucg_builtin_dev_last_error(void)
     return g_last_error.c_str();
 }
 
+int ucg_builtin_dev_mem_kind(const void *ptr)
+{
+    if (ptr == nullptr) {
+        return UCG_DEV_MEM_HOST;
+    }
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, ptr) != hipSuccess) {
+        (void)hipGetLastError();   /* plain malloc'd memory: not an error */
+        return UCG_DEV_MEM_HOST;
+    }
+    switch (a.type) {
+    case hipMemoryTypeDevice:
+    case hipMemoryTypeManaged:
+    case hipMemoryTypeArray:
+        return UCG_DEV_MEM_DEVICE;
+    case hipMemoryTypeHost:
+        return UCG_DEV_MEM_PINNED;
+    default:
+        return UCG_DEV_MEM_HOST;
+    }
+}
+
 int ucg_builtin_dev_device_count(void)
 {
     int n = 0;
@@ -428,6 +453,8 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
     ctx->stage_len   = 0;
     ctx->d_acc       = nullptr;
     ctx->d_acc_cap   = 0;
+    ctx->acc         = nullptr;
+    ctx->acc_in_place = false;
     for (auto &r : ctx->runs) {
         r.active = false;
     }
@@ -632,29 +659,50 @@ ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
     const size_t sz    = kDtSize[dt];
     const size_t chunk = (ctx->slot_bytes / sz) * sz;
     const size_t bytes = count * sz;
+    /* operands that already live on a GPU are used where they are: no PCIe
+     * copy for them, and a device dst is combined in place */
+    const bool dst_dev = ucg_builtin_dev_mem_kind(dst_host) == UCG_DEV_MEM_DEVICE;
+    const bool src_dev = ucg_builtin_dev_mem_kind(src_host) == UCG_DEV_MEM_DEVICE;
+    if (dst_dev && src_dev) {
+        if ((st = reduce_on(ctx, ctx->stream, op, dt, dst_host, src_host, count)) != UCS_OK) {
+            return st;
+        }
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        return UCS_OK;
+    }
     for (size_t off = 0; off < bytes; off += chunk) {
         const size_t n = (bytes - off < chunk) ? bytes - off : chunk;
         unsigned k;
         if ((st = slot_acquire(ctx, &k)) != UCS_OK) {
             return st;
         }
-        char *ds = ctx->d_ring + (size_t)k * ctx->slot_bytes;
-        char *dd = ctx->d_ring2 + (size_t)k * ctx->slot_bytes;
-        HIP_TRY(hipMemcpyAsync(ds, (const char*)src_host + off, n,
-                               hipMemcpyHostToDevice, ctx->stream));
-        HIP_TRY(hipMemcpyAsync(dd, (const char*)dst_host + off, n,
-                               hipMemcpyHostToDevice, ctx->stream));
+        const char *ds = (const char*)src_host + off;
+        char *dd       = (char*)dst_host + off;
+        if (!src_dev) {
+            char *slot = ctx->d_ring + (size_t)k * ctx->slot_bytes;
+            HIP_TRY(hipMemcpyAsync(slot, ds, n, hipMemcpyHostToDevice, ctx->stream));
+            ds = slot;
+            ctx->counters[2] += n;
+        }
+        if (!dst_dev) {
+            dd = ctx->d_ring2 + (size_t)k * ctx->slot_bytes;
+            HIP_TRY(hipMemcpyAsync(dd, (const char*)dst_host + off, n,
+                                   hipMemcpyHostToDevice, ctx->stream));
+            ctx->counters[2] += n;
+        }
         if ((st = reduce_on(ctx, ctx->stream, op, dt, dd, ds, n / sz)) != UCS_OK) {
             return st;
         }
         HIP_TRY(hipEventRecord(ctx->slot_ev[k], ctx->stream));
-        HIP_TRY(hipStreamWaitEvent(ctx->stream_d2h, ctx->slot_ev[k], 0));
-        HIP_TRY(hipMemcpyAsync((char*)dst_host + off, dd, n,
-                               hipMemcpyDeviceToHost, ctx->stream_d2h));
-        HIP_TRY(hipEventRecord(ctx->slot_ev[k], ctx->stream_d2h));
-        ctx->counters[2] += 2 * n;
-        ctx->counters[3] += n;
+        if (!dst_dev) {
+            HIP_TRY(hipStreamWaitEvent(ctx->stream_d2h, ctx->slot_ev[k], 0));
+            HIP_TRY(hipMemcpyAsync((char*)dst_host + off, dd, n,
+                                   hipMemcpyDeviceToHost, ctx->stream_d2h));
+            HIP_TRY(hipEventRecord(ctx->slot_ev[k], ctx->stream_d2h));
+            ctx->counters[3] += n;
+        }
     }
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
     for (unsigned i = 0; i < ctx->nslots; i++) {
         ctx->slot_used[i] = false;
@@ -675,7 +723,7 @@ static ucs_status_t run_flush(ucg_builtin_dev_ctx_t *ctx,
     HIP_TRY(hipMemcpyAsync(ds, ctx->h_ring + (size_t)r.slot * ctx->slot_bytes,
                            r.used, hipMemcpyHostToDevice, ctx->stream));
     ucs_status_t st = reduce_on(ctx, ctx->stream, (ucg_dev_op_t)r.op,
-                                (ucg_dev_dtype_t)r.dt, ctx->d_acc + r.off, ds,
+                                (ucg_dev_dtype_t)r.dt, ctx->acc + r.off, ds,
                                 r.used / sz);
     if (st != UCS_OK) {
         return st;
@@ -723,6 +771,14 @@ ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
         (st = runs_flush_all(ctx)) != UCS_OK) {
         return st;
     }
+    ctx->host_dst     = host_dst;
+    ctx->stage_len    = bytes;
+    ctx->acc_in_place = bytes && ucg_builtin_dev_mem_kind(host_dst) == UCG_DEV_MEM_DEVICE;
+    if (ctx->acc_in_place) {
+        /* GPU-resident recv buffer: accumulate into it directly */
+        ctx->acc = static_cast<char*>(host_dst);
+        return UCS_OK;
+    }
     if (bytes > ctx->d_acc_cap) {
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         if (ctx->d_acc) {
@@ -732,8 +788,7 @@ ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
         HIP_TRY(hipMalloc((void**)&ctx->d_acc, bytes));
         ctx->d_acc_cap = bytes;
     }
-    ctx->host_dst  = host_dst;
-    ctx->stage_len = bytes;
+    ctx->acc = ctx->d_acc;
     if (bytes) {
         HIP_TRY(hipMemcpyAsync(ctx->d_acc, host_dst, bytes,
                                hipMemcpyHostToDevice, ctx->stream));
@@ -855,7 +910,7 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
     if (st != UCS_OK) {
         return st;
     }
-    if (ctx->host_dst && ctx->stage_len) {
+    if (ctx->host_dst && ctx->stage_len && !ctx->acc_in_place) {
         HIP_TRY(hipMemcpyAsync(ctx->host_dst, ctx->d_acc, ctx->stage_len,
                                hipMemcpyDeviceToHost, ctx->stream));
         ctx->counters[3] += ctx->stage_len;
@@ -864,8 +919,10 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
     for (unsigned i = 0; i < ctx->nslots; i++) {
         ctx->slot_used[i] = false;
     }
-    ctx->host_dst  = nullptr;
-    ctx->stage_len = 0;
+    ctx->host_dst     = nullptr;
+    ctx->stage_len    = 0;
+    ctx->acc          = nullptr;
+    ctx->acc_in_place = false;
     return UCS_OK;
 }
 

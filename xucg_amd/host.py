@@ -26,6 +26,8 @@ def _vp(x):
         return x.ctypes.data
     if hasattr(x, "ptr"):
         return x.ptr
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
     return x
 
 
