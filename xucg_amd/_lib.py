@@ -108,8 +108,22 @@ def dev():
             raise NativeLibraryMissing(
                 f"{DEV_LIB} not built: run `python -c 'import __graft_entry__ as g; "
                 f"g.build()'` (hipcc --offload-arch=gfx950)")
+        _load_torch_runtime_first()
         _dev = _bind(ctypes.CDLL(DEV_LIB), DEV_API)
     return _dev
+
+
+def _load_torch_runtime_first():
+    """PyTorch-ROCm bundles its own libamdhip64 with the same soname
+    (libamdhip64.so.7) as /opt/rocm's. Whichever loads first serves the whole
+    process; torch fails to initialise ("No HIP GPUs are available") on the
+    /opt/rocm runtime, while this library runs on either. So when torch is
+    installed and not yet imported, import it before loading the shim: one
+    HIP runtime per process, and torch tensors / streams stay usable here."""
+    import importlib.util
+    import sys
+    if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
 
 
 def host():
