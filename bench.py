@@ -133,6 +133,20 @@ def c1_loopback(ranks=4, iters=20000):
 XGMI_GBS = 7 * 153.0   # aggregate xGMI per MI355X
 
 
+def max_ulps(a, b):
+    """Largest distance in units in the last place between two fp32/fp64
+    tensors (sign-magnitude bits mapped onto a monotonic integer line)."""
+    import torch
+    ity = torch.int32 if a.dtype == torch.float32 else torch.int64
+    mask = (1 << 31) - 1 if ity == torch.int32 else (1 << 63) - 1
+
+    def key(t):
+        i = t.view(ity).long()
+        mag = i & mask
+        return torch.where(i < 0, -mag, mag)
+    return int((key(a) - key(b)).abs().max().item())
+
+
 def staged_step(total=64 << 20, frag=8184, reps=5):
     """Row f1's device staging from C (tests/c/stage_bench.c): one fragmented
     fp32 SUM step, one ucg_builtin_dev_combine per 8 KiB AM fragment between
@@ -257,6 +271,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             err = (mine - rs_out).abs()
             within = bool((err <= tol).all())
             ratio = float((err / tol.clamp_min(1e-30)).max())
+            ulps = max_ulps(mine, rs_out)
             del abs_rs, tol, err
         finally:
             torch.cuda.synchronize()
@@ -269,6 +284,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "bit_exact_vs_rccl_on_exact_inputs": same,
                 "rccl_within_8c_tolerance_on_rounded_inputs": within,
                 "max_err_over_tolerance": round(ratio, 4),
+                "max_ulps_vs_rccl_on_rounded_inputs": ulps,
                 "association": "recursive doubling (builtin_recursive.c:158-169)"}
     agreed(oneshot, "c4_oneshot_xgmi_rs_4gib_fp32")
     del x, rs_out, ag_out
@@ -334,6 +350,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         err = (acc - ref).abs()
         res["rccl_allreduce_within_8c_tolerance_of_plan"] = bool((err <= tol).all())
         res["rccl_allreduce_max_abs_err_over_tol"] = float((err / tol.clamp_min(1e-300)).max())
+        res["rccl_allreduce_max_ulps"] = max_ulps(acc, ref)
         del absx, tol, err
         t = timed(lambda: dist.all_reduce(acc), steps)
         res["rccl_allreduce"] = {"ms": round(t * 1e3, 3),
@@ -413,6 +430,9 @@ def main():
     iters = 50
     avg_us = ctx.profile_reduce("sum", "float32", dst, src, n, iters)
     achieved = bytes_per_step / (avg_us * 1e-6) / 1e9
+    # SURVEY.md 8d also asks for the median of individually timed launches
+    singles = sorted(ctx.profile_reduce("sum", "float32", dst, src, n, 1) for _ in range(21))
+    median_us = singles[len(singles) // 2]
 
     extra = {}
     if not args.no_extra and rank == 0:
@@ -488,6 +508,9 @@ def main():
                 "traffic": pmc_traffic(n),
                 "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64>",
                 "kernel_avg_us": round(avg_us, 3),
+                "kernel_median_us_single_launches": round(median_us, 3),
+                "frac_from_median": round(bytes_per_step / (median_us * 1e-6) / 1e9
+                                          / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": bytes_per_step,
             },
             "cpu_baseline": cpu,
