@@ -361,7 +361,77 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     return out
 
 
+def run_collective_children(dist, rank, world, timeout_s=900):
+    """Run collective_phases in one child process per rank (a fresh process
+    group on a new port), so that a fault in the multi-GPU phases - the IPC
+    peer mappings cannot be exercised on the 1-GPU boxes this build is tested
+    on - costs the collective numbers only, never the bench line. Children
+    are started with subprocess (fork + exec in the child), never by
+    replacing this process. Returns rank 0's result dict (or an error)."""
+    import subprocess
+    import tempfile
+    import uuid
+    import torch
+    obj = [None]
+    if rank == 0:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        obj[0] = {"port": port,
+                  "out": os.path.join(tempfile.gettempdir(),
+                                      f"xucg_collective_{os.getpid()}_{uuid.uuid4().hex}.json")}
+    dist.broadcast_object_list(obj, src=0)
+    torch.cuda.synchronize()
+    dist.barrier()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(obj[0]["port"]),
+               XUCG_COLLECTIVE_OUT=obj[0]["out"])
+    try:
+        p = subprocess.run([sys.executable, os.path.abspath(__file__), "--collective-child"],
+                           env=env, capture_output=True, text=True, timeout=timeout_s)
+        rc, tail = p.returncode, (p.stdout + p.stderr)[-600:]
+    except subprocess.TimeoutExpired as e:
+        rc, tail = "timeout", str(e)[-300:]
+    if rank != 0:
+        return None, rc == 0
+    res = None
+    try:
+        with open(obj[0]["out"]) as f:
+            res = json.load(f)
+        os.unlink(obj[0]["out"])
+    except (OSError, ValueError):
+        pass
+    if rc != 0 or res is None:
+        res = dict(res or {}, error=f"collective child exited with {rc}", tail=tail)
+    return res, rc == 0
+
+
+def collective_child():
+    """--collective-child: one rank of the collective phases (see above)."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    import xucg_amd
+    world = int(os.environ["WORLD_SIZE"])
+    rank = int(os.environ["RANK"])
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=300),
+                            device_id=torch.device(f"cuda:{local_rank}"))
+    ctx = xucg_amd.DevContext(device=local_rank,
+                              stream=torch.cuda.current_stream(local_rank).cuda_stream)
+    res = collective_phases(ctx, dist, rank, world, local_rank)
+    if rank == 0:
+        with open(os.environ["XUCG_COLLECTIVE_OUT"], "w") as f:
+            json.dump(res, f)
+    ctx.close()
+    dist.destroy_process_group()
+
+
 def main():
+    if "--collective-child" in sys.argv:
+        collective_child()
+        return
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -467,11 +537,12 @@ def main():
         hs.free()
         hd.free()
 
-    collective = None
+    collective, children_ok = None, True
     if (world > 1 and not args.no_collective) or args.collective_force:
         src.free()
         dst.free()
-        collective = collective_phases(ctx, dist, rank, world, local_rank)
+        ctx.close()
+        collective, children_ok = run_collective_children(dist, rank, world)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -520,6 +591,10 @@ def main():
         print(json.dumps(line), flush=True)
 
     ctx.close()
+    if not children_ok:
+        # a child died on the GPU: leave without touching the device again
+        sys.stdout.flush()
+        os._exit(0)
     if dist is not None:
         dist.destroy_process_group()
 
