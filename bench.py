@@ -361,7 +361,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     return out
 
 
-def run_collective_children(dist, rank, world, timeout_s=900):
+def run_collective_children(dist, rank, world, timeout_s=600):
     """Run collective_phases in one child process per rank (a fresh process
     group on a new port), so that a fault in the multi-GPU phases - the IPC
     peer mappings cannot be exercised on the 1-GPU boxes this build is tested
@@ -384,7 +384,10 @@ def run_collective_children(dist, rank, world, timeout_s=900):
     dist.broadcast_object_list(obj, src=0)
     torch.cuda.synchronize()
     dist.barrier()
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(obj[0]["port"]),
+    # a fresh rendezvous: without torchrun's agent store (TORCHELASTIC_*
+    # would make the child wait for the agent's store on the new port)
+    env = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(obj[0]["port"]),
                XUCG_COLLECTIVE_OUT=obj[0]["out"])
     try:
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--collective-child"],
@@ -416,7 +419,7 @@ def collective_child():
     rank = int(os.environ["RANK"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
-    dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=300),
+    dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
                             device_id=torch.device(f"cuda:{local_rank}"))
     ctx = xucg_amd.DevContext(device=local_rank,
                               stream=torch.cuda.current_stream(local_rank).cuda_stream)

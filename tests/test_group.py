@@ -63,7 +63,7 @@ def test_bench_collective_phases_world1():
            "--master-addr=127.0.0.1", f"--master-port={free_port()}",
            os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "3", "--warmup", "1",
            "--no-cpu-baseline", "--no-extra", "--collective-force"]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
     coll = line["collective"]
