@@ -361,6 +361,35 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     return out
 
 
+def same_box_reference(n, iters=50):
+    """Vendor kernels on the same box, same buffers, same bytes: PyTorch's
+    in-place add (dst += src, 3N bytes) and a device-to-device copy (2N
+    bytes), timed with events on torch's stream. HBM throughput differs by a
+    few per cent from box to box; these put the combine's number in context."""
+    import torch
+    a = torch.rand(n, device="cuda")
+    b = torch.rand(n, device="cuda")
+
+    def time_us(fn):
+        for _ in range(5):
+            fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return e0.elapsed_time(e1) * 1e3 / iters
+    add_us = time_us(lambda: b.add_(a))
+    copy_us = time_us(lambda: b.copy_(a))
+    del a, b
+    torch.cuda.empty_cache()
+    return {"torch_add_inplace_us": round(add_us, 3),
+            "torch_add_inplace_gbs": round(3 * n * 4 / (add_us * 1e-6) / 1e9, 1),
+            "d2d_copy_us": round(copy_us, 3),
+            "d2d_copy_gbs": round(2 * n * 4 / (copy_us * 1e-6) / 1e9, 1)}
+
+
 def run_collective_children(dist, rank, world, timeout_s=600):
     """Run collective_phases in one child process per rank (a fresh process
     group on a new port), so that a fault in the multi-GPU phases - the IPC
@@ -523,6 +552,7 @@ def main():
             "frac_of_8tbs": round(g1 / HBM_PEAK_GBS, 4), "target_frac": 0.80}
         s1.free()
         d1.free()
+        extra["same_box_reference_kernels"] = same_box_reference(n)
         # H2D/D2H-inclusive rate: host-resident (pinned) buffers, pipelined
         hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)
         ctx.combine_host("sum", "float32", hd, hs, n)  # warm the ring
