@@ -77,3 +77,9 @@ def test_bench_collective_phases_world1():
     assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["rccl_allreduce_within_8c_tolerance_of_plan"] is True, c5
+
+
+@pytest.mark.parametrize("mode,bad", [("ok", 0), ("export", 1), ("import", 2), ("import", 0)])
+def test_peer_buffers_failures_are_agreed(mode, bad):
+    codes, outs = launch("_worker_peers.py", 3, args=(mode, bad), timeout=120)
+    assert codes == [0] * 3, "\n".join(outs)

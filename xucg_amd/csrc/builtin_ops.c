@@ -1174,15 +1174,31 @@ int ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *c, ucs_status_t *status)
 
 ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
 {
-    double t0 = now_s(), lim = wait_timeout_s();
+    static double lim = -1.0;
+    static long spin = -1;
+    unsigned idle = 0;
+    double t0 = now_s();
+    if (lim < 0.0) {
+        const char *e = getenv("UCX_BUILTIN_WAIT_SPIN");
+        lim  = wait_timeout_s();
+        spin = e ? atol(e) : 4096;
+    }
     while (!c->done) {
-        if (ucg_builtin_lgroup_progress(c->g) == 0) {
-            if (now_s() - t0 > lim) {
-                finish(c, UCS_ERR_TIMED_OUT);
-                break;
-            }
-            sched_yield();
+        if (ucg_builtin_lgroup_progress(c->g) != 0) {
+            idle = 0;
+            continue;
         }
+        /* a peer's message is usually a few hundred ns away: spin first,
+         * give the core away only when the wait gets long */
+        if (++idle < (unsigned long)spin) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        if (now_s() - t0 > lim) {
+            finish(c, UCS_ERR_TIMED_OUT);
+            break;
+        }
+        sched_yield();
     }
     return c->status;
 }

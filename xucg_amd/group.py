@@ -157,18 +157,39 @@ class PeerBuffers:
     def __init__(self, ctx, local_ptr, rank, world, dist, group=None):
         self.ctx = ctx
         self.rank = rank
-        blob = ctx.ipc_export(local_ptr)
-        blobs = [None] * world
-        dist.all_gather_object(blobs, blob, group=group)
         self.ptrs = []
         self._imported = []
-        for r, b in enumerate(blobs):
-            if r == rank:
-                self.ptrs.append(local_ptr)
-            else:
-                p = ctx.ipc_import(b)
-                self._imported.append(p)
-                self.ptrs.append(p)
+        # every member takes part in every collective below whatever fails
+        # locally, and all members agree on the outcome: a failure raises on
+        # all of them instead of leaving the others waiting
+        err = None
+        try:
+            blob = ctx.ipc_export(local_ptr)
+        except Exception as e:  # noqa: BLE001 - reported after agreement
+            blob, err = None, e
+        blobs = [None] * world
+        dist.all_gather_object(blobs, blob, group=group)
+        if err is None and any(b is None for b in blobs):
+            err = RuntimeError("a peer failed to export its buffer")
+        if err is None:
+            try:
+                for r, b in enumerate(blobs):
+                    if r == rank:
+                        self.ptrs.append(local_ptr)
+                    else:
+                        p = ctx.ipc_import(b)
+                        self._imported.append(p)
+                        self.ptrs.append(p)
+            except Exception as e:  # noqa: BLE001
+                err = e
+        ok = [err is None]
+        oks = [None] * world
+        dist.all_gather_object(oks, ok, group=group)
+        if err is None and not all(o[0] for o in oks):
+            err = RuntimeError("a peer failed to map the group's buffers")
+        if err is not None:
+            self.close()
+            raise RuntimeError(f"PeerBuffers: {err}")
 
     def close(self):
         for p in self._imported:
