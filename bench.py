@@ -450,8 +450,7 @@ def collective_child():
     torch.cuda.set_device(local_rank)
     dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
                             device_id=torch.device(f"cuda:{local_rank}"))
-    ctx = xucg_amd.DevContext(device=local_rank,
-                              stream=torch.cuda.current_stream(local_rank).cuda_stream)
+    ctx = xucg_amd.DevContext.on_torch_stream(local_rank)
     res = collective_phases(ctx, dist, rank, world, local_rank)
     if rank == 0:
         with open(os.environ["XUCG_COLLECTIVE_OUT"], "w") as f:
@@ -499,9 +498,8 @@ def main():
     n = args.count
     # multi-GPU: launch on torch's current stream so RCCL and the combine are
     # stream-ordered without host syncs
-    ctx = xucg_amd.DevContext(
-        device=local_rank,
-        stream=torch.cuda.current_stream(local_rank).cuda_stream if dist else None)
+    ctx = xucg_amd.DevContext.on_torch_stream(local_rank) if dist else \
+        xucg_amd.DevContext(device=local_rank)
     src = ctx.alloc(n * 4)
     dst = ctx.alloc(n * 4)
     ctx.fill("float32", "round", 0x5EED0000 + 2 * rank, src, n)

@@ -116,12 +116,32 @@ class DevContext:
     per-step device accumulator."""
 
     def __init__(self, device=-1, stream=None, stage_bytes=0, stage_slots=0):
+        if stream is not None and stream == 0:
+            # the C ABI reads NULL as "create a stream": the legacy null stream
+            # cannot be shared, and a private non-blocking stream would not be
+            # ordered with the caller's work. Share a real stream instead.
+            raise ValueError("stream 0 (the null stream) cannot be shared; use "
+                             "DevContext.on_torch_stream()")
         L = _lib.dev()
-        p = _lib.DevCtxParams(device, stream or None, stage_bytes, stage_slots)
+        p = _lib.DevCtxParams(device, stream, stage_bytes, stage_slots)
         h = ctypes.c_void_p()
         check(L.ucg_builtin_dev_ctx_create(ctypes.byref(p), ctypes.byref(h)),
               "ucg_builtin_dev_ctx_create")
         self.handle = h.value
+
+    @classmethod
+    def on_torch_stream(cls, device=0, **kw):
+        """A context that launches on torch's current stream, made a fresh
+        (non-null) stream here: torch ops, RCCL collectives (which order
+        themselves against the caller's current stream) and this context's
+        combines are then stream-ordered with no host syncs."""
+        import torch
+        torch.cuda.set_device(device)
+        s = torch.cuda.Stream(device=device)
+        torch.cuda.set_stream(s)
+        ctx = cls(device=device, stream=s.cuda_stream, **kw)
+        ctx.torch_stream = s        # keep the stream alive with the context
+        return ctx
 
     # -- lifecycle --------------------------------------------------------
     def close(self):
