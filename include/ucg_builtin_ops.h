@@ -118,6 +118,10 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *group,
                                       const void *sbuf, void *rbuf,
                                       int count, void *dtype, void *op,
                                       unsigned root, ucg_builtin_lcoll_t **coll_p);
+/* Up to UCG_BUILTIN_OPS_MAX_CONCURRENT ops of a group may be in flight. One
+ * REDUCE step at a time holds the combine's step staging (device mirror);
+ * a step that finds it busy combines each fragment on its own through
+ * ucg_builtin_combine_reduce (the reference's per-fragment call). */
 /* ucg_collective_start: UCS_OK if complete, UCS_INPROGRESS, or an error */
 ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *coll);
 /* 1 when the last start completed; its status in *status */

@@ -81,6 +81,30 @@ def main():
         print(f"rank {rank}: persistent op MISMATCH", flush=True)
         rc = 1
     coll.close()
+    # two ops in flight on one group at once (slots coll_id % 16,
+    # builtin_ops.h:388): the second finds the step staging busy and combines
+    # per fragment; both must still match the plan
+    cases2 = [("int32", "sum", "round", 3001), ("float32", "sum", "exact", 2500)]
+    colls, sends, outs, wants = [], [], [], []
+    for k, (dt, op, dist, count) in enumerate(cases2):
+        ins = [O.fill(dt, dist, 1300 + 17 * k + r, count) for r in range(world)]
+        wants.append(O.reduce_multi(op, dt, ins, rank))
+        sends.append(ins[rank])
+        outs.append(np.zeros_like(ins[rank]))
+        colls.append(group.allreduce(sends[-1], outs[-1], count, DTYPES[dt], OPS[op]))
+    sts = [c.start() for c in colls]
+    for c, st in zip(colls, sts):
+        if st == 1:   # UCS_INPROGRESS
+            st = c.wait()
+        if st != 0:
+            print(f"rank {rank}: concurrent op status {st}", flush=True)
+            rc = 1
+    for (dt, op, dist, count), got, want in zip(cases2, outs, wants):
+        if not (O.bits(got) == O.bits(want)).all():
+            print(f"rank {rank}: concurrent op MISMATCH {dt} {op}", flush=True)
+            rc = 1
+    for c in colls:
+        c.close()
     if ring_cells <= 4 and group.stats()["resends"] == 0:
         print(f"rank {rank}: expected UCS_ERR_NO_RESOURCE resends with {ring_cells} cells",
               flush=True)

@@ -665,11 +665,14 @@ static void step_execute(ucg_builtin_lcoll_t *c)
         if (s->aggregation == AGG_REDUCE) {
             st = ucg_builtin_combine_step_begin(g->cmb, c->op, c->dtype, c->rbuf,
                                                 c->length);
-            if (st != UCS_OK) {
+            if (st == UCS_OK) {
+                c->step_open = 1;
+            } else if (st != UCS_ERR_BUSY) {
                 finish(c, st);
                 return;
             }
-            c->step_open = 1;
+            /* UCS_ERR_BUSY: another op of this group holds the step staging;
+             * this step combines each fragment on its own (recv_cb) */
         }
         c->step_started = 1;
         c->pending      = s->fragments_total;
@@ -738,7 +741,12 @@ static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
     if (offset + length > c->length) {
         st = UCS_ERR_IO_ERROR;          /* a message outside recv.buffer */
     } else if (s->aggregation == AGG_REDUCE) {
-        st = ucg_builtin_combine_fragment(c->g->cmb, offset, data, length);
+        st = c->step_open ?
+             ucg_builtin_combine_fragment(c->g->cmb, offset, data, length) :
+             /* ucg_builtin_mpi_reduce_fragment, builtin_comp_step.inl:112-120 */
+             ucg_builtin_combine_reduce(c->g->cmb, c->op, (void*)data,
+                                        c->rbuf + offset, (int)(length / c->dt_len),
+                                        c->dtype);
     } else if (s->aggregation == AGG_WRITE) {
         memcpy(c->rbuf + offset, data, length);   /* :204-210 */
     }
