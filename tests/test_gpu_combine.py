@@ -275,3 +275,44 @@ def test_mem_kind(dev_ctx):
     finally:
         hb.free()
         db.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,count,multi", [
+    ("uint8", (1 << 32) + 4099, False),     # past 4 GiB per operand
+    ("float32", (1 << 32) + 5, False),      # past 2^32 elements (16 GiB per operand)
+    ("uint8", (1 << 36) + 4099, False),     # past 2^32 16-B vectors: several dispatches
+    ("uint8", (1 << 35) + 4099, True)])     # the multi-operand kernel (2 operands)
+def test_max_size_operands(dev_ctx, dt, count, multi):
+    """Maximum sizes on a 288 GB device: 64-bit indexing and the chunking of
+    launches whose work-item count would not fit a dispatch packet. Windows
+    around every boundary (4 GiB, 2^32 elements, each 2^31-vector chunk) and
+    the ragged end are checked bit for bit against the oracle."""
+    st = O.storage(dt)
+    sz = np.dtype(st).itemsize
+    nbytes = count * sz
+    src, dst = dev_ctx.alloc(nbytes), dev_ctx.alloc(nbytes)
+    try:
+        dev_ctx.fill(dt, "round", 31, src, count)
+        dev_ctx.fill(dt, "round", 32, dst, count)
+        dev_ctx.sync()
+        chunk = (1 << 31) * (16 // sz)
+        bounds = sorted({(1 << 32) // sz, 1 << 32, chunk, 2 * chunk, count})
+        starts = [0] + [max(0, b - 2048) for b in bounds if b <= count]
+        wins = [(a, min(count, a + 4096)) for a in starts]
+        before = [(src.download(st, b - a, a * sz), dst.download(st, b - a, a * sz))
+                  for a, b in wins]
+        if multi:
+            assert dev_ctx.reduce_multi("sum", dt, dst, [src, dst], 1, count) == 0, \
+                _lib.last_error()
+        else:
+            dev_ctx.reduce_checked("sum", dt, dst, src, count)
+        dev_ctx.sync()
+        for (a, b), (s, d) in zip(wins, before):
+            got = dst.download(st, b - a, a * sz)
+            # reduce_multi with self = 1: V(1, 1) = x0 (op) x1, src = member 0
+            want = O.reduce("sum", dt, s, d)
+            assert (O.bits(got) == O.bits(want)).all(), (dt, count, a)
+    finally:
+        src.free()
+        dst.free()

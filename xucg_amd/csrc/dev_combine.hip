@@ -111,14 +111,28 @@ static unsigned grid_for(size_t work_items, size_t per_block, int cap)
 typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
                                   hipStream_t st, int variant);
 
+/* A dispatch packet counts work-items in 32 bits, so one launch covers at
+ * most 2^31 16-B vectors (32 GiB per operand); larger operands (HBM holds
+ * 288 GB) are cut into such chunks, the ragged head in the first and the tail
+ * in the last. */
+constexpr size_t kMaxVecPerLaunch = (size_t)1 << 31;
+
 template <typename T, int OP, int U, int NT, int BS>
 static void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
                        hipStream_t st)
 {
-    /* one tile of U vectors per lane: grid sized to the data (no cap) */
-    const unsigned grid = grid_for(nvec, (size_t)BS * U, 0x7fffffff);
-    hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS>), dim3(grid), dim3(BS), 0, st,
-                       d, s, head, nvec, tail);
+    constexpr size_t V = 16 / sizeof(T);
+    size_t done = 0;
+    do {
+        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
+        const bool first = (done == 0), last = (done + chunk == nvec);
+        const size_t off = first ? 0 : head + done * V;
+        /* one tile of U vectors per lane: grid sized to the chunk (no loop) */
+        const unsigned grid = grid_for(chunk, (size_t)BS * U, 0x7fffffff);
+        hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS>), dim3(grid), dim3(BS), 0, st,
+                           d + off, s + off, first ? head : 0, chunk, last ? tail : 0);
+        done += chunk;
+    } while (done < nvec);
 }
 
 template <int DT, int OP>
@@ -216,9 +230,20 @@ static hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         head = count;
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
-    const unsigned grid = grid_for(nvec, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
-    hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
-                       st, d, srcs, self, head, nvec, tail);
+    size_t done = 0;
+    do {
+        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
+        const bool first = (done == 0), last = (done + chunk == nvec);
+        const size_t off = first ? 0 : head + done * V;
+        SrcList sl;
+        for (int m = 0; m < kMaxMulti; m++) {
+            sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
+        }
+        const unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
+        hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
+                           st, d + off, sl, self, first ? head : 0, chunk, last ? tail : 0);
+        done += chunk;
+    } while (done < nvec);
     return hipGetLastError();
 }
 
