@@ -122,7 +122,9 @@ def _load_torch_runtime_first():
     HIP runtime per process, and torch tensors / streams stay usable here."""
     import importlib.util
     import sys
-    if "torch" not in sys.modules and importlib.util.find_spec("torch") is not None:
+    if "torch" in sys.modules or not os.path.exists("/dev/kfd"):
+        return      # already loaded, or no GPU driver: no runtime will start
+    if importlib.util.find_spec("torch") is not None:
         import torch  # noqa: F401
 
 
