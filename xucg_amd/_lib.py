@@ -122,8 +122,9 @@ def _load_torch_runtime_first():
     HIP runtime per process, and torch tensors / streams stay usable here."""
     import importlib.util
     import sys
-    if "torch" in sys.modules or not os.path.exists("/dev/kfd"):
-        return      # already loaded, or no GPU driver: no runtime will start
+    if ("torch" in sys.modules or not os.path.exists("/dev/kfd") or
+            os.environ.get("XUCG_NO_TORCH_PRELOAD") == "1"):
+        return      # already loaded, no GPU driver, or the caller opted out
     if importlib.util.find_spec("torch") is not None:
         import torch  # noqa: F401
 
