@@ -126,6 +126,45 @@ k_oneshot3(float *dst, const float *src, size_t nvec)
     }
 }
 
+/* variant H: one-wave workgroups on a capped grid, each looping over tiles
+ * (fewer workgroups for the dispatcher to launch); PIPE = 1 loads the next
+ * tile before storing the current one */
+template <int PIPE>
+__global__ void __launch_bounds__(64)
+k_gs64(float *dst, const float *src, size_t nvec)
+{
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    const size_t stride = (size_t)gridDim.x * 64;
+    size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (!PIPE) {
+        for (; i < nvec; i += stride) {
+            st16<1>(d4 + i, vapply<float, 0>(ld16<1>(s4 + i), ld16<1>(d4 + i)));
+        }
+        return;
+    }
+    if (i >= nvec) {
+        return;
+    }
+    u32x4 a = ld16<1>(s4 + i), b = ld16<1>(d4 + i);
+    for (;;) {
+        const size_t j = i + stride;
+        const bool more = j < nvec;
+        u32x4 a2, b2;
+        if (more) {
+            a2 = ld16<1>(s4 + j);
+            b2 = ld16<1>(d4 + j);
+        }
+        st16<1>(d4 + i, vapply<float, 0>(a, b));
+        if (!more) {
+            break;
+        }
+        a = a2;
+        b = b2;
+        i = j;
+    }
+}
+
 /* variant G: oneshot with buffer loads/stores and explicit cache-policy aux
  * bits (gfx950: bit0 sc0, bit1 nt, bit4 sc1); byte offsets < 4 GiB */
 template <int U, int AUXL, int AUXS, int BS = 256>
@@ -318,6 +357,21 @@ int main(int argc, char **argv)
     os3(1, 64, 0, 1);
     os3(2, 128, 0, 0);
     os3(1, 128, 0, 0);
+    auto gs64 = [&](int PIPE, unsigned G) {
+        char buf[128];
+        snprintf(buf, sizeof(buf), "gs64 pipe%d grid%u", PIPE, G);
+        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)std::min<size_t>((nv + 63) / 64, G);
+            if (PIPE) hipLaunchKernelGGL((k_gs64<1>), dim3(g), dim3(64), 0, q, d, s, nv);
+            else      hipLaunchKernelGGL((k_gs64<0>), dim3(g), dim3(64), 0, q, d, s, nv);
+        }, {}});
+    };
+    gs64(0, 8192);
+    gs64(0, 32768);
+    gs64(0, 131072);
+    gs64(1, 8192);
+    gs64(1, 32768);
+    gs64(1, 131072);
     if (nvec * 16 <= 0xFFFFFFFFull) {
         auto osb = [&](int U, int AL, int AS, int BS) {
             char buf[128];
