@@ -251,15 +251,24 @@ static void spin_lock(_Atomic uint32_t *l)
 {
     unsigned spins = 0;
     uint32_t z = 0;
+    double t0 = 0.0;
     while (!atomic_compare_exchange_weak_explicit(l, &z, 1, memory_order_acquire,
                                                   memory_order_relaxed)) {
         z = 0;
-        /* the holder packs at most one fragment: spin briefly, then yield */
+        /* the holder packs at most one fragment: spin briefly, then yield;
+         * a holder that never lets go (a dead peer) is fatal, not a hang */
         if (++spins < 256) {
             __builtin_ia32_pause();
-        } else {
-            sched_yield();
+            continue;
         }
+        if (t0 == 0.0) {
+            t0 = now_s();
+        } else if ((spins & 1023) == 0 && now_s() - t0 > wait_timeout_s()) {
+            fprintf(stderr, "ucg_builtin_shm: incast cell lock held for over %.0f s\n",
+                    wait_timeout_s());
+            abort();
+        }
+        sched_yield();
     }
 }
 
