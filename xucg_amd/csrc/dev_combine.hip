@@ -19,7 +19,7 @@
 #include <utility>
 
 #include "ucg_builtin_dev.h"
-#include "dev_kernels.h"
+#include "dev_launch.h"
 
 using namespace ucgdev;
 
@@ -91,226 +91,38 @@ static const LaunchCfg &launch_cfg()
     return g_cfg;
 }
 
-static size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
-
-static unsigned grid_for(size_t work_items, size_t per_block, int cap)
+namespace ucgdev {
+int launch_max_blocks()
 {
-    size_t g = div_up(work_items, per_block);
-    if (g < 1) {
-        g = 1;
-    }
-    if (g > (size_t)cap) {
-        g = (size_t)cap;
-    }
-    return (unsigned)g;
+    return launch_cfg().max_blocks;
 }
+}  // namespace ucgdev
 
-/* ------------------------------------------------------------------------ */
-/* reduce launchers                                                         */
-/* ------------------------------------------------------------------------ */
-typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
-                                  hipStream_t st, int variant);
-
-/* A dispatch packet counts work-items in 32 bits, so one launch covers at
- * most 2^31 16-B vectors (32 GiB per operand); larger operands (HBM holds
- * 288 GB) are cut into such chunks, the ragged head in the first and the tail
- * in the last. */
-constexpr size_t kMaxVecPerLaunch = (size_t)1 << 31;
-
-template <typename T, int OP, int U, int NT, int BS>
-static void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
-                       hipStream_t st)
-{
-    constexpr size_t V = 16 / sizeof(T);
-    size_t done = 0;
-    do {
-        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
-        const bool first = (done == 0), last = (done + chunk == nvec);
-        const size_t off = first ? 0 : head + done * V;
-        /* one tile of U vectors per lane: grid sized to the chunk (no loop) */
-        const unsigned grid = grid_for(chunk, (size_t)BS * U, 0x7fffffff);
-        hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS>), dim3(grid), dim3(BS), 0, st,
-                           d + off, s + off, first ? head : 0, chunk, last ? tail : 0);
-        done += chunk;
-    } while (done < nvec);
-}
-
-template <int DT, int OP>
-static hipError_t launch_reduce(void *dst, const void *src, size_t count,
-                                hipStream_t st, int variant)
-{
-    typedef typename DtType<DT>::T T;
-    constexpr size_t sz = sizeof(T);
-    constexpr size_t V  = 16 / sz;
-    T *d       = static_cast<T*>(dst);
-    const T *s = static_cast<const T*>(src);
-    const uintptr_t md = (uintptr_t)dst & 15, ms = (uintptr_t)src & 15;
-
-    if (md != ms) {
-        /* operands disagree mod 16 B: no common vector alignment */
-        const unsigned grid = grid_for(count, (size_t)kBlock * 4,
-                                       launch_cfg().max_blocks);
-        hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(grid), dim3(kBlock),
-                           0, st, d, s, count);
-        return hipGetLastError();
-    }
-    size_t head = md ? (16 - md) / sz : 0;
-    if (head > count) {
-        head = count;
-    }
-    const size_t rem  = count - head;
-    const size_t nvec = rem / V, tail = rem % V;
-
-    if (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM && variant >= 0) {
-        /* tuning variants of the headline kernel (UCX_BUILTIN_DEV_VARIANT) */
-        switch (variant) {
-        case 1: launch_vec<T, OP, 4, 1, 256>(d, s, head, nvec, tail, st); break;
-        case 2: launch_vec<T, OP, 1, 1, 256>(d, s, head, nvec, tail, st); break;
-        case 3: launch_vec<T, OP, 1, 0, 64>(d, s, head, nvec, tail, st); break;
-        default:
-            launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
-            break;
-        }
-    } else {
-        launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
-    }
-    return hipGetLastError();
-}
-
-template <int DT, int OP>
-constexpr reduce_fn_t reduce_entry()
-{
-    if constexpr (pair_supported(DT, OP)) {
-        return &launch_reduce<DT, OP>;
-    } else {
-        return nullptr;
-    }
-}
-
-template <int DT, int... OPS>
-constexpr std::array<reduce_fn_t, UCG_DEV_OP_LAST>
-reduce_row(std::integer_sequence<int, OPS...>)
-{
-    return {reduce_entry<DT, OPS>()...};
-}
+/* dispatch tables, assembled from the per-dtype translation units */
+struct Tables {
+    std::array<std::array<reduce_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST> reduce;
+    std::array<std::array<multi_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>  multi;
+    std::array<fill_fn_t, UCG_DEV_DT_LAST>                                fill;
+};
 
 template <int... DTS>
-constexpr std::array<std::array<reduce_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>
-reduce_table(std::integer_sequence<int, DTS...>)
+static Tables build_tables(std::integer_sequence<int, DTS...>)
 {
-    return {reduce_row<DTS>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>())...};
-}
-
-static const auto g_reduce =
-    reduce_table(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
-
-/* ---- multi-operand (recursive-doubling association) --------------------- */
-typedef hipError_t (*multi_fn_t)(void *dst, const SrcList &srcs, unsigned n,
-                                 unsigned self, size_t count, hipStream_t st);
-
-template <typename T, int OP, int N>
-static hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
-                                 size_t count, hipStream_t st)
-{
-    constexpr size_t sz = sizeof(T), V = 16 / sz;
-    const uintptr_t md = (uintptr_t)dst & 15;
-    bool aligned = true;
-    for (int m = 0; m < N; m++) {
-        aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
+    const RowSet r[] = {rows<DTS>()...};
+    Tables t;
+    for (int d = 0; d < UCG_DEV_DT_LAST; d++) {
+        t.reduce[d] = r[d].reduce;
+        t.multi[d]  = r[d].multi;
+        t.fill[d]   = r[d].fill;
     }
-    T *d = static_cast<T*>(dst);
-    if (!aligned) {
-        const unsigned grid = grid_for(count, kBlock, launch_cfg().max_blocks);
-        hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP, N>), dim3(grid),
-                           dim3(kBlock), 0, st, d, srcs, self, count);
-        return hipGetLastError();
-    }
-    size_t head = md ? (16 - md) / sz : 0;
-    if (head > count) {
-        head = count;
-    }
-    const size_t rem = count - head, nvec = rem / V, tail = rem % V;
-    size_t done = 0;
-    do {
-        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
-        const bool first = (done == 0), last = (done + chunk == nvec);
-        const size_t off = first ? 0 : head + done * V;
-        SrcList sl;
-        for (int m = 0; m < kMaxMulti; m++) {
-            sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
-        }
-        const unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
-        hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
-                           st, d + off, sl, self, first ? head : 0, chunk, last ? tail : 0);
-        done += chunk;
-    } while (done < nvec);
-    return hipGetLastError();
+    return t;
 }
 
-template <int DT, int OP>
-static hipError_t launch_multi(void *dst, const SrcList &srcs, unsigned n,
-                               unsigned self, size_t count, hipStream_t st)
+static const Tables &tables()
 {
-    typedef typename DtType<DT>::T T;
-    switch (n) {
-    case 1:  return launch_multi_n<T, OP, 1>(dst, srcs, self, count, st);
-    case 2:  return launch_multi_n<T, OP, 2>(dst, srcs, self, count, st);
-    case 4:  return launch_multi_n<T, OP, 4>(dst, srcs, self, count, st);
-    case 8:  return launch_multi_n<T, OP, 8>(dst, srcs, self, count, st);
-    case 16: return launch_multi_n<T, OP, 16>(dst, srcs, self, count, st);
-    default: return hipErrorInvalidValue;
-    }
+    static const Tables t = build_tables(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
+    return t;
 }
-
-template <int DT, int OP>
-constexpr multi_fn_t multi_entry()
-{
-    if constexpr (pair_supported(DT, OP)) {
-        return &launch_multi<DT, OP>;
-    } else {
-        return nullptr;
-    }
-}
-
-template <int DT, int... OPS>
-constexpr std::array<multi_fn_t, UCG_DEV_OP_LAST>
-multi_row(std::integer_sequence<int, OPS...>)
-{
-    return {multi_entry<DT, OPS>()...};
-}
-
-template <int... DTS>
-constexpr std::array<std::array<multi_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>
-multi_table(std::integer_sequence<int, DTS...>)
-{
-    return {multi_row<DTS>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>())...};
-}
-
-static const auto g_multi =
-    multi_table(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
-
-/* ---- generator ---------------------------------------------------------- */
-typedef void (*fill_fn_t)(void *dst, int dist, uint64_t key, size_t count,
-                          hipStream_t st);
-
-template <int DT>
-static void launch_fill(void *dst, int dist, uint64_t key, size_t count,
-                        hipStream_t st)
-{
-    const unsigned grid = grid_for(count, kBlock, 4096);
-    hipLaunchKernelGGL((k_fill<DT>), dim3(grid), dim3(kBlock), 0, st, dst, dist,
-                       key, count);
-}
-
-template <int... DTS>
-constexpr std::array<fill_fn_t, UCG_DEV_DT_LAST>
-fill_table(std::integer_sequence<int, DTS...>)
-{
-    return {&launch_fill<DTS>...};
-}
-
-static const auto g_fill =
-    fill_table(std::make_integer_sequence<int, UCG_DEV_DT_LAST>());
 
 /* ------------------------------------------------------------------------ */
 /* context                                                                  */
@@ -407,7 +219,7 @@ int ucg_builtin_dev_is_supported(ucg_dev_dtype_t dt, ucg_dev_op_t op)
     if ((int)dt < 0 || dt >= UCG_DEV_DT_LAST || (int)op < 0 || op >= UCG_DEV_OP_LAST) {
         return 0;
     }
-    return g_reduce[dt][op] != nullptr;
+    return tables().reduce[dt][op] != nullptr;
 }
 
 const char *ucg_builtin_dev_version(void)
@@ -614,7 +426,7 @@ static ucs_status_t reduce_on(ucg_builtin_dev_ctx_t *ctx, hipStream_t st,
         return set_error(UCS_ERR_INVALID_PARAM, "reduce",
                          "src and dst partially overlap");
     }
-    HIP_TRY(g_reduce[dt][op](dst, src, count, st, launch_cfg().variant));
+    HIP_TRY(tables().reduce[dt][op](dst, src, count, st, launch_cfg().variant));
     ctx->counters[0]++;
     ctx->counters[1] += 3 * bytes;
     return UCS_OK;
@@ -661,7 +473,7 @@ ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
                              "NULL or misaligned source");
         }
     }
-    HIP_TRY(g_multi[dt][op](dst, list, nsrc, self, count, ctx->stream));
+    HIP_TRY(tables().multi[dt][op](dst, list, nsrc, self, count, ctx->stream));
     ctx->counters[0]++;
     ctx->counters[1] += (uint64_t)(nsrc + 1) * count * kDtSize[dt];
     return UCS_OK;
@@ -1085,7 +897,7 @@ ucs_status_t ucg_builtin_dev_fill(ucg_builtin_dev_ctx_t *ctx, ucg_dev_dtype_t dt
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
     const uint64_t key = z ^ (z >> 31);
-    g_fill[dt](dst, (int)dist, key, count, ctx->stream);
+    tables().fill[dt](dst, (int)dist, key, count, ctx->stream);
     HIP_TRY(hipGetLastError());
     return UCS_OK;
 }

@@ -1,0 +1,252 @@
+/*
+ * dev_launch.h - launchers of the combine kernels and the per-dtype rows of
+ * the dispatch tables. Each dtype's kernels are instantiated in their own
+ * translation unit (dev_inst.hip, compiled once per dtype) so the library
+ * builds in parallel; dev_combine.hip assembles the tables from rows<DT>().
+ */
+#ifndef UCG_DEV_LAUNCH_H_
+#define UCG_DEV_LAUNCH_H_
+
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <utility>
+
+#include "ucg_builtin_dev.h"
+#include "dev_kernels.h"
+
+namespace ucgdev {
+
+/* UCX_BUILTIN_DEV_MAX_BLOCKS: grid cap of the looping (scalar) kernels;
+ * defined in dev_combine.hip */
+int launch_max_blocks();
+
+inline size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
+
+inline unsigned grid_for(size_t work_items, size_t per_block, int cap)
+{
+    size_t g = div_up(work_items, per_block);
+    if (g < 1) {
+        g = 1;
+    }
+    if (g > (size_t)cap) {
+        g = (size_t)cap;
+    }
+    return (unsigned)g;
+}
+
+/* ------------------------------------------------------------------------ */
+/* reduce launchers                                                         */
+/* ------------------------------------------------------------------------ */
+typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
+                                  hipStream_t st, int variant);
+
+/* A dispatch packet counts work-items in 32 bits, so one launch covers at
+ * most 2^31 16-B vectors (32 GiB per operand); larger operands (HBM holds
+ * 288 GB) are cut into such chunks, the ragged head in the first and the tail
+ * in the last. */
+constexpr size_t kMaxVecPerLaunch = (size_t)1 << 31;
+
+template <typename T, int OP, int U, int NT, int BS>
+void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
+                       hipStream_t st)
+{
+    constexpr size_t V = 16 / sizeof(T);
+    size_t done = 0;
+    do {
+        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
+        const bool first = (done == 0), last = (done + chunk == nvec);
+        const size_t off = first ? 0 : head + done * V;
+        /* one tile of U vectors per lane: grid sized to the chunk (no loop) */
+        const unsigned grid = grid_for(chunk, (size_t)BS * U, 0x7fffffff);
+        hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS>), dim3(grid), dim3(BS), 0, st,
+                           d + off, s + off, first ? head : 0, chunk, last ? tail : 0);
+        done += chunk;
+    } while (done < nvec);
+}
+
+template <int DT, int OP>
+hipError_t launch_reduce(void *dst, const void *src, size_t count,
+                                hipStream_t st, int variant)
+{
+    typedef typename DtType<DT>::T T;
+    constexpr size_t sz = sizeof(T);
+    constexpr size_t V  = 16 / sz;
+    T *d       = static_cast<T*>(dst);
+    const T *s = static_cast<const T*>(src);
+    const uintptr_t md = (uintptr_t)dst & 15, ms = (uintptr_t)src & 15;
+
+    if (md != ms) {
+        /* operands disagree mod 16 B: no common vector alignment */
+        const unsigned grid = grid_for(count, (size_t)kBlock * 4,
+                                       launch_max_blocks());
+        hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(grid), dim3(kBlock),
+                           0, st, d, s, count);
+        return hipGetLastError();
+    }
+    size_t head = md ? (16 - md) / sz : 0;
+    if (head > count) {
+        head = count;
+    }
+    const size_t rem  = count - head;
+    const size_t nvec = rem / V, tail = rem % V;
+
+    if (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM && variant >= 0) {
+        /* tuning variants of the headline kernel (UCX_BUILTIN_DEV_VARIANT) */
+        switch (variant) {
+        case 1: launch_vec<T, OP, 4, 1, 256>(d, s, head, nvec, tail, st); break;
+        case 2: launch_vec<T, OP, 1, 1, 256>(d, s, head, nvec, tail, st); break;
+        case 3: launch_vec<T, OP, 1, 0, 64>(d, s, head, nvec, tail, st); break;
+        default:
+            launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
+            break;
+        }
+    } else {
+        launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
+    }
+    return hipGetLastError();
+}
+
+template <int DT, int OP>
+constexpr reduce_fn_t reduce_entry()
+{
+    if constexpr (pair_supported(DT, OP)) {
+        return &launch_reduce<DT, OP>;
+    } else {
+        return nullptr;
+    }
+}
+
+template <int DT, int... OPS>
+constexpr std::array<reduce_fn_t, UCG_DEV_OP_LAST>
+reduce_row(std::integer_sequence<int, OPS...>)
+{
+    return {reduce_entry<DT, OPS>()...};
+}
+
+
+/* ---- multi-operand (recursive-doubling association) --------------------- */
+typedef hipError_t (*multi_fn_t)(void *dst, const SrcList &srcs, unsigned n,
+                                 unsigned self, size_t count, hipStream_t st);
+
+template <typename T, int OP, int N>
+hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
+                                 size_t count, hipStream_t st)
+{
+    constexpr size_t sz = sizeof(T), V = 16 / sz;
+    const uintptr_t md = (uintptr_t)dst & 15;
+    bool aligned = true;
+    for (int m = 0; m < N; m++) {
+        aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
+    }
+    T *d = static_cast<T*>(dst);
+    if (!aligned) {
+        const unsigned grid = grid_for(count, kBlock, launch_max_blocks());
+        hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP, N>), dim3(grid),
+                           dim3(kBlock), 0, st, d, srcs, self, count);
+        return hipGetLastError();
+    }
+    size_t head = md ? (16 - md) / sz : 0;
+    if (head > count) {
+        head = count;
+    }
+    const size_t rem = count - head, nvec = rem / V, tail = rem % V;
+    size_t done = 0;
+    do {
+        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
+        const bool first = (done == 0), last = (done + chunk == nvec);
+        const size_t off = first ? 0 : head + done * V;
+        SrcList sl;
+        for (int m = 0; m < kMaxMulti; m++) {
+            sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
+        }
+        const unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
+        hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
+                           st, d + off, sl, self, first ? head : 0, chunk, last ? tail : 0);
+        done += chunk;
+    } while (done < nvec);
+    return hipGetLastError();
+}
+
+template <int DT, int OP>
+hipError_t launch_multi(void *dst, const SrcList &srcs, unsigned n,
+                               unsigned self, size_t count, hipStream_t st)
+{
+    typedef typename DtType<DT>::T T;
+    switch (n) {
+    case 1:  return launch_multi_n<T, OP, 1>(dst, srcs, self, count, st);
+    case 2:  return launch_multi_n<T, OP, 2>(dst, srcs, self, count, st);
+    case 4:  return launch_multi_n<T, OP, 4>(dst, srcs, self, count, st);
+    case 8:  return launch_multi_n<T, OP, 8>(dst, srcs, self, count, st);
+    case 16: return launch_multi_n<T, OP, 16>(dst, srcs, self, count, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+template <int DT, int OP>
+constexpr multi_fn_t multi_entry()
+{
+    if constexpr (pair_supported(DT, OP)) {
+        return &launch_multi<DT, OP>;
+    } else {
+        return nullptr;
+    }
+}
+
+template <int DT, int... OPS>
+constexpr std::array<multi_fn_t, UCG_DEV_OP_LAST>
+multi_row(std::integer_sequence<int, OPS...>)
+{
+    return {multi_entry<DT, OPS>()...};
+}
+
+
+/* ---- generator ---------------------------------------------------------- */
+typedef void (*fill_fn_t)(void *dst, int dist, uint64_t key, size_t count,
+                          hipStream_t st);
+
+template <int DT>
+void launch_fill(void *dst, int dist, uint64_t key, size_t count,
+                        hipStream_t st)
+{
+    const unsigned grid = grid_for(count, kBlock, 4096);
+    hipLaunchKernelGGL((k_fill<DT>), dim3(grid), dim3(kBlock), 0, st, dst, dist,
+                       key, count);
+}
+
+
+
+/* every launcher of one dtype */
+struct RowSet {
+    std::array<reduce_fn_t, UCG_DEV_OP_LAST> reduce;
+    std::array<multi_fn_t, UCG_DEV_OP_LAST>  multi;
+    fill_fn_t                                fill;
+};
+
+template <int DT>
+RowSet make_rows()
+{
+    return {reduce_row<DT>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>()),
+            multi_row<DT>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>()),
+            &launch_fill<DT>};
+}
+
+/* defined in dev_inst.hip, one translation unit per dtype */
+template <int DT> RowSet rows();
+template <> RowSet rows<0>();
+template <> RowSet rows<1>();
+template <> RowSet rows<2>();
+template <> RowSet rows<3>();
+template <> RowSet rows<4>();
+template <> RowSet rows<5>();
+template <> RowSet rows<6>();
+template <> RowSet rows<7>();
+template <> RowSet rows<8>();
+template <> RowSet rows<9>();
+template <> RowSet rows<10>();
+template <> RowSet rows<11>();
+static_assert(UCG_DEV_DT_LAST == 12, "one rows<> specialisation per dtype");
+
+}  // namespace ucgdev
+
+#endif
