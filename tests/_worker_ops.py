@@ -27,6 +27,7 @@ CASES = [  # (dtype, op, dist, count)
     ("uint8", "bxor", "round", 4099),
     ("bfloat16", "min", "special", 700),
     ("float32", "sum", "round", 1),
+    ("int64", "sum", "round", 0),           # empty: completes at start
 ]
 
 

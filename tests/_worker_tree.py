@@ -34,6 +34,7 @@ INT_CASES = [  # (dtype, op, count)
     ("int16", "min", 700),
     ("uint32", "land", 64),
     ("int8", "lor", 1),
+    ("int32", "max", 0),             # empty: completes at start on every member
     ("uint64", "band", 2048),
     ("uint8", "sum", 4099),          # unsigned SUM: the atomic packers with incast
     ("uint16", "sum", 513),
