@@ -86,7 +86,7 @@ static const LaunchCfg &launch_cfg()
         if (g_cfg.max_blocks < 1) {
             g_cfg.max_blocks = 2048;
         }
-        g_cfg.variant = v ? atoi(v) : 0; /* U = 4, non-temporal */
+        g_cfg.variant = v ? atoi(v) : 0; /* 0: the product geometry */
     });
     return g_cfg;
 }

@@ -72,13 +72,14 @@ __device__ __forceinline__ u32x4 vapply(u32x4 s, u32x4 d)
 
 /*
  * The streaming combine. One tile of U 16-B vectors per lane (lane stride
- * kBlock), no loop: the grid is sized to the data, so the hardware dispatcher
- * streams fresh workgroups onto the CUs and every wave issues its 2U loads
- * back to back before its first use. Loads and stores carry the non-temporal
- * hint: nothing is re-read, and measured on MI355X this geometry moved the
- * 2 x 256 MiB fp32 combine from 56% (grid-stride loop, temporal) to 85% of
- * 8 TB/s with one-wave workgroups and U = 1 (profiles/r01). The ragged head (until dst is 16-B aligned)
- * and tail (< 16 B) are done by the first lanes of the grid.
+ * BS), no loop: the grid is sized to the data (one dispatch covers up to 2^31
+ * vectors, see launch_vec), so the hardware dispatcher streams fresh
+ * workgroups onto the CUs and every wave issues its 2U loads back to back
+ * before its first use. Loads and stores carry the non-temporal hint: nothing
+ * is re-read. Measured on MI355X this geometry moved the 2 x 256 MiB fp32
+ * combine from 56% (grid-stride loop, temporal) to 85% of 8 TB/s with
+ * one-wave workgroups and U = 1 (profiles/r01). The ragged head
+ * (until dst is 16-B aligned) and tail (< 16 B) are done by the first lanes.
  */
 template <typename T, int OP, int U, int NT, int BS>
 __global__ void __launch_bounds__(BS)
