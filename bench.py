@@ -254,6 +254,27 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             torch.cuda.synchronize()
             same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
             t_ag = timed(lambda: dist.all_gather_into_tensor(ag_out, mine), steps)
+            # one-shot all-gather: every rank reads the N reduced shards in
+            # place over xGMI (ucg_builtin_dev_gather_multi); parity: bit-exact
+            # with RCCL's all-gather of the same shards
+            ag_rccl = ag_out.clone()
+            speers = G.PeerBuffers(ctx, mine.data_ptr(), rank, world, dist)
+            try:
+                def ag1():
+                    G.oneshot_all_gather(ctx, speers, ag_out.data_ptr(), n4, "float32",
+                                         world)
+                    torch.cuda.synchronize()
+                    dist.barrier()
+                for _ in range(warmup):
+                    ag1()
+                t_ag1 = timed(ag1, steps)
+                ag_same = bool(torch.equal(ag_out.view(torch.int32),
+                                           ag_rccl.view(torch.int32)))
+            finally:
+                torch.cuda.synchronize()
+                dist.barrier()
+                speers.close()
+            del ag_rccl
             # rounded inputs: RCCL's ring order vs the plan's association,
             # SURVEY.md 8c bound |delta| <= 2 (n-1) u sum_i |x_i|, u = 2^-24
             torch.cuda.synchronize()
@@ -281,6 +302,10 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
                 "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4),
                 "rs_ag_ms": round((t_rs + t_ag) * 1e3, 3),
+                "oneshot_ag_ms": round(t_ag1 * 1e3, 3),
+                "oneshot_ag_busbw_gbs": round(bus / t_ag1 / 1e9, 1),
+                "oneshot_rs_ag_ms": round((t_rs + t_ag1) * 1e3, 3),
+                "oneshot_ag_bit_exact_vs_rccl": ag_same,
                 "bit_exact_vs_rccl_on_exact_inputs": same,
                 "rccl_within_8c_tolerance_on_rounded_inputs": within,
                 "max_err_over_tolerance": round(ratio, 4),

@@ -186,6 +186,15 @@ ucs_status_t ucg_builtin_dev_reduce(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
  * (left operand = src, right = dst of the reduce_cb_f contract), and writes
  * dst[i] = V(self, log2(nsrc))[i]. nsrc must be a power of two <= 16; srcs may
  * be peer-mapped device pointers (xGMI). dst may alias srcs[self]. */
+/* The all-gather half of a one-shot reduce-scatter + all-gather (SURVEY.md
+ * 8e): dst[r * shard_bytes + i] = srcs[r][i] for r < nsrc, every source read in
+ * one launch (srcs may be peer-mapped device pointers: member r's shard over
+ * xGMI). A plain copy; no reference counterpart (the reference has no
+ * all-gather of reduced shards). nsrc <= 16. */
+ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
+                                          const void *const *srcs, unsigned nsrc,
+                                          size_t shard_bytes);
+
 ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
                                           ucg_dev_op_t op, ucg_dev_dtype_t dt,
                                           void *dst, const void *const *srcs,

@@ -42,6 +42,20 @@ def main():
         if not (O.bits(got) == O.bits(want)).all():
             print(f"rank {rank}: MISMATCH {dt} {op}", flush=True)
             sys.exit(1)
+        # one-shot all-gather of the reduced shards, read from every peer
+        full = ctx.alloc(n * sz)
+        speers = G.PeerBuffers(ctx, out.ptr, rank, world, dist)
+        G.oneshot_all_gather(ctx, speers, full.ptr, n, dt, world)
+        ctx.sync()
+        dist.barrier()
+        speers.close()
+        allgot = full.download(st, n)
+        for r in range(world):
+            rlo, rhi, rwant = G.oracle_shard(op, dt, inputs, r, world, O)
+            if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
+                print(f"rank {rank}: all-gather MISMATCH {dt} {op} shard {r}", flush=True)
+                sys.exit(1)
+        full.free()
         buf.free()
         out.free()
     dist.barrier()

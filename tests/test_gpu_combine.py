@@ -316,3 +316,26 @@ def test_max_size_operands(dev_ctx, dt, count, multi):
     finally:
         src.free()
         dst.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nsrc,shard,offset", [(1, 4096, 0), (4, 1 << 20, 0), (8, 100_000, 0),
+                                               (16, 4099, 0), (3, 65536, 4), (8, 33, 1)])
+def test_gather_multi(dev_ctx, nsrc, shard, offset):
+    """One-shot all-gather copy: dst[r * shard:] = srcs[r][:shard] (vector path
+    for 16-B aligned rows, byte path otherwise)."""
+    srcs = [np.frombuffer(np.random.default_rng(r).bytes(shard), np.uint8) for r in range(nsrc)]
+    bufs = [dev_ctx.alloc(shard + 16) for _ in range(nsrc)]
+    out = dev_ctx.alloc(nsrc * shard + 16)
+    try:
+        for b, s in zip(bufs, srcs):
+            b.upload(s, offset)
+        rc = dev_ctx.gather_multi(out.ptr + offset, [b.ptr + offset for b in bufs], shard)
+        assert rc == 0, _lib.last_error()
+        dev_ctx.sync()
+        got = out.download(np.uint8, nsrc * shard, offset)
+        assert (got == np.concatenate(srcs)).all()
+    finally:
+        for b in bufs:
+            b.free()
+        out.free()

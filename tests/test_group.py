@@ -73,6 +73,7 @@ def test_bench_collective_phases_world1():
     c4 = coll["c4_oneshot_xgmi_rs_4gib_fp32"]
     assert c4["bit_exact_vs_rccl_on_exact_inputs"] is True, c4
     assert c4["rccl_within_8c_tolerance_on_rounded_inputs"] is True, c4
+    assert c4["oneshot_ag_bit_exact_vs_rccl"] is True, c4
     c5 = coll["c5_recursive_allreduce_512mib_fp64"]
     assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5

@@ -479,6 +479,94 @@ ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
     return UCS_OK;
 }
 
+/* ---- one-shot all-gather: blockIdx.y = source member ------------------- */
+/* 16-B vectors of every source (one wave per workgroup, non-temporal, like
+ * the combine); the ragged tail of a shard (< 16 B) is copied byte-wise by
+ * the first lanes of the source's first workgroup. */
+static __global__ void __launch_bounds__(kReduceBlock)
+k_gather_multi(char *dst, SrcList srcs, size_t row_stride, size_t nbytes)
+{
+    const unsigned r  = blockIdx.y;
+    const char *src   = static_cast<const char*>(srcs.p[r]);
+    char *out         = dst + (size_t)r * row_stride;
+    const size_t nvec = nbytes / 16;
+    const size_t i    = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(out) + i,
+                ld16<1>(reinterpret_cast<const u32x4*>(src) + i));
+    }
+    const size_t tail = nbytes - nvec * 16;
+    if (blockIdx.x == 0 && threadIdx.x < tail) {
+        out[nvec * 16 + threadIdx.x] = src[nvec * 16 + threadIdx.x];
+    }
+}
+
+/* unaligned sources or destinations: byte-wise, grid-stride */
+static __global__ void __launch_bounds__(kBlock)
+k_gather_multi_bytes(char *dst, SrcList srcs, size_t shard_bytes)
+{
+    const unsigned r = blockIdx.y;
+    const char *src  = static_cast<const char*>(srcs.p[r]);
+    char *out        = dst + (size_t)r * shard_bytes;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < shard_bytes;
+         i += (size_t)gridDim.x * kBlock) {
+        out[i] = src[i];
+    }
+}
+
+ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
+                                          const void *const *srcs, unsigned nsrc,
+                                          size_t shard_bytes)
+{
+    if (ctx == nullptr || srcs == nullptr || nsrc == 0 ||
+        nsrc > (unsigned)kMaxMulti || (shard_bytes && dst == nullptr)) {
+        return set_error(UCS_ERR_INVALID_PARAM, "gather_multi",
+                         "bad arguments (nsrc must be 1..16)");
+    }
+    if (shard_bytes == 0) {
+        return UCS_OK;
+    }
+    SrcList list;
+    bool aligned = ((uintptr_t)dst % 16) == 0 && shard_bytes % 16 == 0;  /* rows too */
+    for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
+        list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
+        if (i < nsrc) {
+            if (srcs[i] == nullptr) {
+                return set_error(UCS_ERR_INVALID_PARAM, "gather_multi", "NULL source");
+            }
+            aligned = aligned && ((uintptr_t)srcs[i] % 16) == 0;
+        }
+    }
+    char *d = static_cast<char*>(dst);
+    if (!aligned) {
+        const unsigned grid = grid_for(shard_bytes, kBlock, 1024);
+        hipLaunchKernelGGL(k_gather_multi_bytes, dim3(grid, nsrc), dim3(kBlock), 0,
+                           ctx->stream, d, list, shard_bytes);
+    } else {
+        /* one dispatch covers up to 2^31 work-items per source row */
+        const size_t nvec = shard_bytes / 16;
+        size_t done = 0;
+        do {
+            const size_t chunk = nvec - done < ((size_t)1 << 31) ? nvec - done
+                                                                 : ((size_t)1 << 31);
+            SrcList sl = list;
+            for (unsigned i = 0; i < nsrc; i++) {
+                sl.p[i] = static_cast<const char*>(list.p[i]) + done * 16;
+            }
+            const unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
+            /* rows stay shard_bytes apart; this dispatch covers bytes
+             * [done*16, done*16 + chunk*16) of every row */
+            hipLaunchKernelGGL(k_gather_multi, dim3(grid, nsrc), dim3(kReduceBlock), 0,
+                               ctx->stream, d + done * 16, sl, shard_bytes, chunk * 16);
+            done += chunk;
+        } while (done < nvec);
+    }
+    HIP_TRY(hipGetLastError());
+    ctx->counters[0]++;
+    ctx->counters[1] += 2 * (uint64_t)nsrc * shard_bytes;
+    return UCS_OK;
+}
+
 /* ---- host-resident whole-buffer combine (pipelined) --------------------- */
 ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
                                           ucg_dev_op_t op, ucg_dev_dtype_t dt,

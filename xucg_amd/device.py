@@ -191,6 +191,12 @@ class DevContext:
                                                        dt_index(dt), _ptr(dst), arr,
                                                        len(srcs), self_index, count)
 
+    def gather_multi(self, dst, srcs, shard_bytes):
+        """dst[r * shard_bytes:...] = srcs[r][:shard_bytes] in one launch."""
+        arr = (ctypes.c_void_p * len(srcs))(*[_ptr(s) for s in srcs])
+        return _lib.dev().ucg_builtin_dev_gather_multi(self.handle, _ptr(dst), arr,
+                                                       len(srcs), shard_bytes)
+
     def combine_host(self, op, dt, dst_host, src_host, count):
         return _lib.dev().ucg_builtin_dev_combine_host(self.handle, op_index(op),
                                                        dt_index(dt), _ptr(dst_host),

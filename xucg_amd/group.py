@@ -210,6 +210,23 @@ def oneshot_reduce_scatter(ctx, peers, out_ptr, count, dt, op, rank, world):
     return lo, hi
 
 
+def oneshot_all_gather(ctx, shard_peers, out_ptr, count, dt, world):
+    """out = the concatenation of every member's shard (shard_bounds layout),
+    read in place from `shard_peers` (PeerBuffers over each member's shard
+    buffer) in one launch; the unequal last shard, if any, in a second."""
+    size = _lib.DTYPE_SIZE[_lib.dt_index(dt)]
+    lo0, hi0 = shard_bounds(count, size, world, 0)
+    per = (hi0 - lo0) * size
+    lo_l, hi_l = shard_bounds(count, size, world, world - 1)
+    last = (hi_l - lo_l) * size
+    if world == 1 or last == per:
+        _lib.check(ctx.gather_multi(out_ptr, shard_peers.ptrs, per), "gather_multi")
+        return
+    _lib.check(ctx.gather_multi(out_ptr, shard_peers.ptrs[:-1], per), "gather_multi")
+    _lib.check(ctx.gather_multi(out_ptr + lo_l * size, shard_peers.ptrs[-1:], last),
+               "gather_multi")
+
+
 def oracle_shard(op, dt, inputs, rank, world, oracle):
     """Expected one-shot shard for tests: the plan's result on the owner."""
     size = np.dtype(inputs[0].dtype).itemsize
