@@ -924,7 +924,12 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
     if (ctx) {
         (void)hipSetDevice(ctx->device);
     }
-    hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+    /* whole 2 MiB granules: a small hipMalloc may be carved out of a block
+     * the runtime shares with other allocations, and such memory cannot be
+     * exported through hipIpcGetMemHandle (ucg_builtin_dev_ipc_export) */
+    const size_t gran = (size_t)2 << 20;
+    bytes = bytes ? (bytes + gran - 1) / gran * gran : gran;
+    hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {
         hip_status(e, "hipMalloc");
         return nullptr;
