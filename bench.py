@@ -107,15 +107,21 @@ def c1_loopback(ranks=4, iters=20000):
                 ("tree_incast_max_short_256", ranks, 256,
                  {"UCX_BUILTIN_ALLREDUCE_PLAN": "tree", "UCX_BUILTIN_SM_INCAST": "y"}),
                 ("tree_3_ranks_max_short_256", 3, 256, {})]
-    res = {}
+    # one core per rank, as an MPI launcher binds them: the lowest-numbered
+    # allowed CPUs (neighbours on one CCD on EPYC); unpinned ranks land on
+    # random cores and the latency moves by 2x between runs
+    allowed = sorted(os.sched_getaffinity(0))
+    res = {"cpus": allowed[:max(v[1] for v in variants)]}
     for key, world, max_short, extra_env in variants:
         name = f"ucg_bench_c1_{os.getpid()}_{uuid.uuid4().hex[:6]}"
         procs = []
         for r in range(world):
             env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), **extra_env)
+            cpu = allowed[r % len(allowed)]
             procs.append(subprocess.Popen([exe, name, str(iters), str(max_short)], env=env,
                                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
-                                          text=True))
+                                          text=True,
+                                          preexec_fn=lambda c=cpu: os.sched_setaffinity(0, {c})))
         outs = []
         for p in procs:
             try:
