@@ -1,0 +1,72 @@
+"""One member of a randomized engine run: a seeded sequence of allreduce and
+reduce ops (random dtype, op, count, root, in-place) on one group, each
+checked bit for bit against the oracle (integer types and exact-integer
+floats, so the tree's arrival order cannot change a result).
+
+    _worker_fuzz.py <shm-name> <seed> <max_short> <ring_cells>"""
+import os
+import sys
+
+import numpy as np
+
+from oracle import oracle as O
+from xucg_amd import host, ops
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from mock_mpi import MockMPI, OPS, DTYPES  # noqa: E402
+
+INT_DTS = ["int8", "uint8", "int16", "uint16", "int32", "uint32", "int64", "uint64"]
+
+
+def main():
+    name, seed, max_short, cells = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), \
+        int(sys.argv[4])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    rng = np.random.default_rng(seed)          # same sequence on every member
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    iface = ops.ShmIface(name, world, rank, max_short=max_short, ring_cells=cells)
+    group = ops.Group(iface, 5, world, rank, cmb)
+    pow2 = (world & (world - 1)) == 0
+    rc = 0
+    for k in range(40):
+        if rng.random() < 0.75:
+            dt = INT_DTS[rng.integers(len(INT_DTS))]
+            op = ["sum", "prod", "max", "min", "land", "lor", "lxor", "band", "bor",
+                  "bxor"][rng.integers(10)]
+            dist = "round"
+        else:
+            dt, op, dist = ["float32", "float64"][rng.integers(2)], "sum", "exact"
+        count = int(rng.choice([0, 1, 3, 100, 1000, int(rng.integers(1, 6000))]))
+        kind = "reduce" if rng.random() < 0.35 else "allreduce"
+        root = int(rng.integers(world))
+        in_place = bool(rng.random() < 0.3)
+        inputs = [O.fill(dt, dist, seed * 1000 + 10 * k + r, count) for r in range(world)]
+        sbuf = inputs[rank].copy()
+        if kind == "allreduce":
+            want = O.reduce_multi(op, dt, inputs, rank) if pow2 else \
+                O.tree_reduce(op, dt, inputs, 0)
+            rbuf = sbuf if in_place else np.zeros_like(sbuf)
+            coll = group.allreduce(sbuf, rbuf, count, DTYPES[dt], OPS[op])
+        else:
+            want = O.tree_reduce(op, dt, inputs, root)
+            rbuf = (sbuf if in_place else np.zeros_like(sbuf)) if rank == root else None
+            coll = group.reduce(sbuf, rbuf, count, DTYPES[dt], OPS[op], root)
+        assert coll.status == 0, coll.status
+        st = coll.run()
+        ok = st == 0 and (rbuf is None or (O.bits(rbuf) == O.bits(want)).all())
+        if not ok:
+            print(f"rank {rank}: MISMATCH seed {seed} op#{k} {kind} {dt} {op} n={count} "
+                  f"root={root} in_place={in_place} status={st}", flush=True)
+            rc = 1
+        coll.close()
+    group.close()
+    iface.close()
+    cmb.close()
+    if rc == 0:
+        print(f"rank {rank}: ok", flush=True)
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    main()

@@ -339,3 +339,74 @@ def test_gather_multi(dev_ctx, nsrc, shard, offset):
         for b in bufs:
             b.free()
         out.free()
+
+
+@pytest.mark.gpu
+def test_random_cases_against_oracle(dev_ctx):
+    """Fuzz: 300 random (dtype, op, distribution, count, src offset, dst
+    offset) cases through ucg_builtin_dev_reduce, each bit-exact against the
+    oracle. Offsets are whole elements from 0 to 15, so src and dst are often
+    misaligned relative to each other (scalar kernel) or to 16 B (head/tail);
+    counts from 0 to 70,000."""
+    rng = np.random.default_rng(20261015)
+    cap = 70_000 * 8 + 256
+    bs, bd = dev_ctx.alloc(cap), dev_ctx.alloc(cap)
+    try:
+        pairs = [(dt, op) for dt in O.DTYPES for op in O.OPS if O.is_supported(dt, op)]
+        for case in range(300):
+            dt, op = pairs[rng.integers(len(pairs))]
+            dist = ("exact", "round", "special")[rng.integers(3)]
+            count = int(rng.choice([0, 1, 2, 3, 7, 15, 16, 17, 255, 4099,
+                                    int(rng.integers(1, 70_000))]))
+            st = O.storage(dt)
+            sz = np.dtype(st).itemsize
+            so, do = int(rng.integers(16)) * sz, int(rng.integers(16)) * sz
+            src = O.fill(dt, dist, 1000 + case, count)
+            dst = O.fill(dt, dist, 5000 + case, count)
+            bs.upload(src, so)
+            bd.upload(dst, do)
+            dev_ctx.reduce_checked(op, dt, bd.ptr + do, bs.ptr + so, count)
+            dev_ctx.sync()
+            got = bd.download(st, count, do)
+            want = O.reduce(op, dt, src, dst)
+            assert (O.bits(got) == O.bits(want)).all(), (case, dt, op, dist, count, so, do)
+    finally:
+        bs.free()
+        bd.free()
+
+
+@pytest.mark.gpu
+def test_random_multi_cases_against_oracle(dev_ctx):
+    """Fuzz of the one-shot multi-operand kernel: random N in {1,2,4,8,16},
+    member `self`, dtype/op, count and per-operand element offsets (vector
+    path when all agree mod 16 B, scalar path otherwise), against the oracle's
+    simulation of the recursive-doubling plan."""
+    rng = np.random.default_rng(7)
+    pairs = [(dt, op) for dt in O.DTYPES for op in O.OPS if O.is_supported(dt, op)]
+    cap = 20_000 * 8 + 256
+    bufs = [dev_ctx.alloc(cap) for _ in range(17)]
+    try:
+        for case in range(120):
+            dt, op = pairs[rng.integers(len(pairs))]
+            n = int(rng.choice([1, 2, 4, 8, 16]))
+            me = int(rng.integers(n))
+            count = int(rng.choice([0, 1, 5, 31, 4099, int(rng.integers(1, 20_000))]))
+            st = O.storage(dt)
+            sz = np.dtype(st).itemsize
+            same_off = rng.random() < 0.5
+            base_off = int(rng.integers(16)) * sz
+            offs = [base_off if same_off else int(rng.integers(16)) * sz for _ in range(n + 1)]
+            xs = [O.fill(dt, "special" if rng.random() < 0.3 else "round", 77 * case + r, count)
+                  for r in range(n)]
+            for r in range(n):
+                bufs[r].upload(xs[r], offs[r])
+            rc = dev_ctx.reduce_multi(op, dt, bufs[16].ptr + offs[n],
+                                      [bufs[r].ptr + offs[r] for r in range(n)], me, count)
+            assert rc == 0, _lib.last_error()
+            dev_ctx.sync()
+            got = bufs[16].download(st, count, offs[n])
+            want = O.reduce_multi(op, dt, xs, me) if count else got
+            assert (O.bits(got) == O.bits(want)).all(), (case, dt, op, n, me, count, offs)
+    finally:
+        for b in bufs:
+            b.free()

@@ -149,3 +149,19 @@ def test_tree_multiprocess_device_staging(world):
     assert codes == [0] * world, "\n".join(outs)
     d = _digests(outs)
     assert all(x == d[0] for x in d), d
+
+
+@pytest.mark.parametrize("seed,world,max_short,cells,env", [
+    (1, 2, 256, 64, {}), (2, 3, 64, 2, {}), (3, 4, 1024, 8, {}), (4, 5, 256, 64, {}),
+    (5, 6, 8192, 4, {"UCX_BUILTIN_SM_INCAST": "y"}), (6, 7, 64, 64, {}),
+    (7, 8, 256, 3, {}), (8, 4, 128, 64, {"UCX_BUILTIN_ALLREDUCE_PLAN": "tree",
+                                          "UCX_BUILTIN_SM_INCAST": "y"})])
+def test_engine_fuzz(seed, world, max_short, cells, env, monkeypatch):
+    """A seeded random sequence of 40 allreduce/reduce ops per configuration
+    (world 2-8, max_short 64-8192, rings of 2-64 cells, incast on/off), every
+    result bit-exact against the oracle's plan simulation."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    codes, outs = launch("_worker_fuzz.py", world, args=(shm_name(), seed, max_short, cells),
+                         timeout=300)
+    assert codes == [0] * world, "\n".join(outs)
