@@ -280,6 +280,25 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 torch.cuda.synchronize()
                 dist.barrier()
                 speers.close()
+            # the whole RS + AG as one operation (group.oneshot_allreduce):
+            # both halves one-shot over xGMI, ordered by stream barriers (a
+            # one-element RCCL all_reduce) instead of host syncs
+            sbar = G.stream_barrier(dist, dev)
+            rpeers = G.PeerBuffers(ctx, ag_out.data_ptr(), rank, world, dist)
+            try:
+                def ar1():
+                    G.oneshot_allreduce(ctx, peers, rpeers, n4, "float32", "sum", rank,
+                                        world, sbar)
+                ag_out.zero_()
+                for _ in range(warmup):
+                    ar1()
+                t_ar1 = timed(ar1, steps)
+                ar_same = bool(torch.equal(ag_out.view(torch.int32),
+                                           ag_rccl.view(torch.int32)))
+            finally:
+                torch.cuda.synchronize()
+                dist.barrier()
+                rpeers.close()
             del ag_rccl
             # rounded inputs: RCCL's ring order vs the plan's association,
             # SURVEY.md 8c bound |delta| <= 2 (n-1) u sum_i |x_i|, u = 2^-24
@@ -312,6 +331,10 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "oneshot_ag_busbw_gbs": round(bus / t_ag1 / 1e9, 1),
                 "oneshot_rs_ag_ms": round((t_rs + t_ag1) * 1e3, 3),
                 "oneshot_ag_bit_exact_vs_rccl": ag_same,
+                "oneshot_allreduce_ms": round(t_ar1 * 1e3, 3),
+                "oneshot_allreduce_busbw_gbs": round(2 * bus / t_ar1 / 1e9, 1),
+                "oneshot_allreduce_frac_of_xgmi": round(2 * bus / t_ar1 / 1e9 / XGMI_GBS, 4),
+                "oneshot_allreduce_bit_exact_vs_rccl_rs_ag": ar_same,
                 "bit_exact_vs_rccl_on_exact_inputs": same,
                 "rccl_within_8c_tolerance_on_rounded_inputs": within,
                 "max_err_over_tolerance": round(ratio, 4),
@@ -346,6 +369,15 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             G.recursive_halving_allreduce(acc, tmp, rank, world, combine_n, exchange,
                                           n5, 8)
 
+        sbar = G.stream_barrier(dist, dev)
+        ipeers = G.PeerBuffers(ctx, init.data_ptr(), rank, world, dist)
+        apeers = G.PeerBuffers(ctx, acc.data_ptr(), rank, world, dist)
+
+        def once_oneshot():
+            # reads every member's send buffer in place: no init_reduce copy
+            G.oneshot_allreduce(ctx, ipeers, apeers, n5, "float64", "sum", rank, world,
+                                sbar)
+
         # parity: every member's input regenerated locally, one-shot tree
         allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
         for r in range(world):
@@ -357,7 +389,9 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         res = {"bytes_per_rank": n5 * 8, "steps": G.recursive_steps(world)}
         for name, fn, link_bytes in (
                 ("doubling", once, n5 * 8 * G.recursive_steps(world)),
-                ("halving", once_halving, 2 * (world - 1) * n5 * 8 // world)):
+                ("halving", once_halving, 2 * (world - 1) * n5 * 8 // world),
+                ("oneshot_xgmi", once_oneshot, 2 * (world - 1) * n5 * 8 // world)):
+            acc.zero_()
             fn()
             torch.cuda.synchronize()
             same = _lib_check == 0 and bool(torch.equal(acc.view(torch.int64),
@@ -370,6 +404,10 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                          "sent_bytes_per_rank": link_bytes,
                          "link_gbs": round(link_bytes / t / 1e9, 1),
                          "bit_exact_vs_oneshot_tree": same}
+        torch.cuda.synchronize()
+        dist.barrier()
+        ipeers.close()
+        apeers.close()
         # vendor baseline on the same buffer (ring association: tolerance only)
         acc.copy_(init)
         dist.all_reduce(acc)

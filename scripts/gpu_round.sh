@@ -22,7 +22,7 @@ fatal() { # rc -> 0 if the step may be followed by another GPU step
 
 if [ "$WHAT" = all ] || [ "$WHAT" = tests ]; then
     echo "== pytest -m gpu" | tee -a "$OUT/steps.log"
-    timeout -k 10 900 python -m pytest tests -q -m gpu > "$OUT/pytest_gpu.log" 2>&1
+    timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
     rc=$?; echo "pytest rc=$rc" | tee -a "$OUT/steps.log"; tail -5 "$OUT/pytest_gpu.log"
     fatal $rc
 fi

@@ -55,6 +55,26 @@ def main():
             if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
                 print(f"rank {rank}: all-gather MISMATCH {dt} {op} shard {r}", flush=True)
                 sys.exit(1)
+        # one-shot allreduce: reduce-scatter into the recv buffer's own shard,
+        # then every other shard read from its owner; every member ends with
+        # the plan's result on every shard
+        ctx.fill(dt, "special", 999, full, n)      # stale contents must not pass
+        ctx.sync()
+        rpeers = G.PeerBuffers(ctx, full.ptr, rank, world, dist)
+        peers = G.PeerBuffers(ctx, buf.ptr, rank, world, dist)
+
+        def barrier():
+            ctx.sync()
+            dist.barrier()
+        G.oneshot_allreduce(ctx, peers, rpeers, n, dt, op, rank, world, barrier)
+        allgot = full.download(st, n)
+        rpeers.close()
+        peers.close()
+        for r in range(world):
+            rlo, rhi, rwant = G.oracle_shard(op, dt, inputs, r, world, O)
+            if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
+                print(f"rank {rank}: allreduce MISMATCH {dt} {op} shard {r}", flush=True)
+                sys.exit(1)
         full.free()
         buf.free()
         out.free()

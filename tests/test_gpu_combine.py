@@ -342,6 +342,31 @@ def test_gather_multi(dev_ctx, nsrc, shard, offset):
 
 
 @pytest.mark.gpu
+def test_gather_multi_split_dispatch(dev_ctx):
+    """16 rows of 2^31 + 48 bytes: past 2^31 / 16 vectors per row, so the
+    copy takes two dispatches (work-items are counted in 32 bits). The rows
+    alias one source buffer at 64-B steps; windows around the split and the
+    ends of every row are compared byte for byte."""
+    nsrc, shard = 16, (1 << 31) + 48
+    src = dev_ctx.alloc(shard + 64 * nsrc)
+    out = dev_ctx.alloc(nsrc * shard)
+    try:
+        dev_ctx.fill("uint8", "round", 77, src, shard + 64 * nsrc)
+        rc = dev_ctx.gather_multi(out, [src.ptr + 64 * r for r in range(nsrc)], shard)
+        assert rc == 0, _lib.last_error()
+        dev_ctx.sync()
+        split = (((1 << 31) // nsrc) // 64 * 64) * 16    # bytes per row, first dispatch
+        for r in range(nsrc):
+            for a in (0, split - 4096, shard - 4096):
+                got = out.download(np.uint8, 4096, r * shard + a)
+                want = src.download(np.uint8, 4096, 64 * r + a)
+                assert (got == want).all(), (r, a)
+    finally:
+        src.free()
+        out.free()
+
+
+@pytest.mark.gpu
 def test_random_cases_against_oracle(dev_ctx):
     """Fuzz: 300 random (dtype, op, distribution, count, src offset, dst
     offset) cases through ucg_builtin_dev_reduce, each bit-exact against the

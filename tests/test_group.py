@@ -2,6 +2,8 @@
 gloo (CPU, world 2 and 4), and the peer-mapped one-shot kernel (GPU)."""
 import os
 
+import numpy as np
+
 import pytest
 
 from xucg_amd import group as G
@@ -74,9 +76,11 @@ def test_bench_collective_phases_world1():
     assert c4["bit_exact_vs_rccl_on_exact_inputs"] is True, c4
     assert c4["rccl_within_8c_tolerance_on_rounded_inputs"] is True, c4
     assert c4["oneshot_ag_bit_exact_vs_rccl"] is True, c4
+    assert c4["oneshot_allreduce_bit_exact_vs_rccl_rs_ag"] is True, c4
     c5 = coll["c5_recursive_allreduce_512mib_fp64"]
     assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5
+    assert c5["oneshot_xgmi"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["rccl_allreduce_within_8c_tolerance_of_plan"] is True, c5
 
 
@@ -84,3 +88,81 @@ def test_bench_collective_phases_world1():
 def test_peer_buffers_failures_are_agreed(mode, bad):
     codes, outs = launch("_worker_peers.py", 3, args=(mode, bad), timeout=120)
     assert codes == [0] * 3, "\n".join(outs)
+
+
+class _SimCtx:
+    """Host stand-in for the device context of one member: pointers are
+    offsets into one shared byte array; reduce_multi is the oracle's
+    restatement of the plan association, gather_multi a row copy. Only the
+    schedule of group.oneshot_allreduce is under test here (the kernels
+    are covered by the GPU tests)."""
+
+    def __init__(self, mem, dt, calls):
+        self.mem, self.dt, self.calls = mem, dt, calls
+
+    def reduce_multi(self, op, dt, dst, srcs, self_index, count):
+        from oracle import oracle as O
+        st = np.dtype(O.storage(dt))
+        xs = [self.mem[s:s + count * st.itemsize].view(st) for s in srcs]
+        out = O.reduce_multi(op, dt, xs, self_index)
+        self.mem[dst:dst + count * st.itemsize] = out.view(np.uint8)
+        self.calls.append(("reduce_multi", len(srcs), count))
+        return 0
+
+    def gather_multi(self, dst, srcs, nbytes):
+        for i, s in enumerate(srcs):
+            self.mem[dst + i * nbytes:dst + (i + 1) * nbytes] = self.mem[s:s + nbytes]
+        self.calls.append(("gather_multi", len(srcs), nbytes))
+        return 0
+
+
+class _Peers:
+    def __init__(self, ptrs):
+        self.ptrs = ptrs
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("dt,op,count", [("float32", "sum", 1001), ("int64", "prod", 4099),
+                                         ("float16", "max", 7), ("float64", "sum", 1 << 14)])
+def test_oneshot_allreduce_schedule(world, dt, op, count):
+    """group.oneshot_allreduce with one thread per member over a shared
+    host array: every member ends with shard r = V(r, log2 N) (the plan's
+    association, from the oracle) for every r, and the all-gather skips the
+    member's own shard with one launch per run of equal shards."""
+    import threading
+    from oracle import oracle as O
+    st = np.dtype(O.storage(dt))
+    nb = count * st.itemsize
+    inputs = [O.fill(dt, "special" if dt == "float16" else "round", 70 + r, count)
+              for r in range(world)]
+    mem = np.zeros(2 * world * nb + 64, np.uint8)
+    send = [r * nb for r in range(world)]
+    recv = [(world + r) * nb for r in range(world)]
+    for r in range(world):
+        mem[send[r]:send[r] + nb] = inputs[r].view(np.uint8)
+    bar = threading.Barrier(world)
+    calls = [[] for _ in range(world)]
+    errs = []
+
+    def member(r):
+        try:
+            G.oneshot_allreduce(_SimCtx(mem, dt, calls[r]), _Peers(send), _Peers(recv),
+                                count, dt, op, r, world, bar.wait)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+            bar.abort()
+    ths = [threading.Thread(target=member, args=(r,)) for r in range(world)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs, errs
+    want = np.concatenate([G.oracle_shard(op, dt, inputs, r, world, O)[2]
+                           for r in range(world)])
+    for r in range(world):
+        got = mem[recv[r]:recv[r] + nb].view(st)
+        assert (O.bits(got) == O.bits(want)).all(), (r, dt, op)
+        gathered = sum(n for kind, n, _ in calls[r] if kind == "gather_multi")
+        assert gathered == world - 1
+        # runs: before self, after self, and the unequal last shard apart
+        assert len([c for c in calls[r] if c[0] == "gather_multi"]) <= 3

@@ -479,37 +479,45 @@ ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
     return UCS_OK;
 }
 
-/* ---- one-shot all-gather: blockIdx.y = source member ------------------- */
+/* ---- one-shot all-gather ------------------------------------------------ */
 /* 16-B vectors of every source (one wave per workgroup, non-temporal, like
- * the combine); the ragged tail of a shard (< 16 B) is copied byte-wise by
- * the first lanes of the source's first workgroup. */
+ * the combine). Workgroups are dealt round-robin over the sources
+ * (r = wg % nsrc): the dispatcher hands out workgroup ids in order, so a
+ * source-major grid (one grid row per source) would read one peer at a time
+ * and keep one xGMI link busy; dealt round-robin, every link streams at once.
+ * The ragged tail of a shard (< 16 B) is copied byte-wise by the first lanes
+ * of the source's first workgroup. */
 static __global__ void __launch_bounds__(kReduceBlock)
-k_gather_multi(char *dst, SrcList srcs, size_t row_stride, size_t nbytes)
+k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
+               size_t nbytes)
 {
-    const unsigned r  = blockIdx.y;
+    const unsigned r  = blockIdx.x % nsrc;
+    const size_t wg   = blockIdx.x / nsrc;
     const char *src   = static_cast<const char*>(srcs.p[r]);
     char *out         = dst + (size_t)r * row_stride;
     const size_t nvec = nbytes / 16;
-    const size_t i    = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+    const size_t i    = wg * kReduceBlock + threadIdx.x;
     if (i < nvec) {
         st16<1>(reinterpret_cast<u32x4*>(out) + i,
                 ld16<1>(reinterpret_cast<const u32x4*>(src) + i));
     }
     const size_t tail = nbytes - nvec * 16;
-    if (blockIdx.x == 0 && threadIdx.x < tail) {
+    if (wg == 0 && threadIdx.x < tail) {
         out[nvec * 16 + threadIdx.x] = src[nvec * 16 + threadIdx.x];
     }
 }
 
-/* unaligned sources or destinations: byte-wise, grid-stride */
+/* unaligned sources or destinations: byte-wise, grid-stride, workgroups
+ * dealt round-robin over the sources as above */
 static __global__ void __launch_bounds__(kBlock)
-k_gather_multi_bytes(char *dst, SrcList srcs, size_t shard_bytes)
+k_gather_multi_bytes(char *dst, SrcList srcs, unsigned nsrc, size_t shard_bytes)
 {
-    const unsigned r = blockIdx.y;
-    const char *src  = static_cast<const char*>(srcs.p[r]);
-    char *out        = dst + (size_t)r * shard_bytes;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < shard_bytes;
-         i += (size_t)gridDim.x * kBlock) {
+    const unsigned r   = blockIdx.x % nsrc;
+    const size_t wg    = blockIdx.x / nsrc;
+    const size_t nwg   = gridDim.x / nsrc;
+    const char *src    = static_cast<const char*>(srcs.p[r]);
+    char *out          = dst + (size_t)r * shard_bytes;
+    for (size_t i = wg * kBlock + threadIdx.x; i < shard_bytes; i += nwg * kBlock) {
         out[i] = src[i];
     }
 }
@@ -539,25 +547,29 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
     }
     char *d = static_cast<char*>(dst);
     if (!aligned) {
-        const unsigned grid = grid_for(shard_bytes, kBlock, 1024);
-        hipLaunchKernelGGL(k_gather_multi_bytes, dim3(grid, nsrc), dim3(kBlock), 0,
-                           ctx->stream, d, list, shard_bytes);
+        const unsigned grid = grid_for(shard_bytes, kBlock, 1024) * nsrc;
+        hipLaunchKernelGGL(k_gather_multi_bytes, dim3(grid), dim3(kBlock), 0,
+                           ctx->stream, d, list, nsrc, shard_bytes);
     } else {
-        /* one dispatch covers up to 2^31 work-items per source row */
-        const size_t nvec = shard_bytes / 16;
+        /* a dispatch counts work-items in 32 bits: at most 2^31 in total,
+         * i.e. 2^31 / nsrc vectors of every source per dispatch */
+        const size_t nvec    = shard_bytes / 16;
+        const size_t per_max = (((size_t)1 << 31) / nsrc) / kReduceBlock * kReduceBlock;
         size_t done = 0;
         do {
-            const size_t chunk = nvec - done < ((size_t)1 << 31) ? nvec - done
-                                                                 : ((size_t)1 << 31);
+            const size_t chunk = nvec - done < per_max ? nvec - done : per_max;
             SrcList sl = list;
             for (unsigned i = 0; i < nsrc; i++) {
                 sl.p[i] = static_cast<const char*>(list.p[i]) + done * 16;
             }
-            const unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
+            /* the tail rides with the last dispatch */
+            const size_t nbytes = (done + chunk == nvec) ? shard_bytes - done * 16
+                                                         : chunk * 16;
+            const size_t grid = div_up(chunk ? chunk : 1, kReduceBlock) * nsrc;
             /* rows stay shard_bytes apart; this dispatch covers bytes
-             * [done*16, done*16 + chunk*16) of every row */
-            hipLaunchKernelGGL(k_gather_multi, dim3(grid, nsrc), dim3(kReduceBlock), 0,
-                               ctx->stream, d + done * 16, sl, shard_bytes, chunk * 16);
+             * [done*16, done*16 + nbytes) of every row */
+            hipLaunchKernelGGL(k_gather_multi, dim3((unsigned)grid), dim3(kReduceBlock), 0,
+                               ctx->stream, d + done * 16, sl, nsrc, shard_bytes, nbytes);
             done += chunk;
         } while (done < nvec);
     }

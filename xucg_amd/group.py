@@ -227,6 +227,72 @@ def oneshot_all_gather(ctx, shard_peers, out_ptr, count, dt, world):
                "gather_multi")
 
 
+def _gather_rows(ctx, out_ptr, ptrs, rows, count, size, world):
+    """out[shard r] = ptrs[r][0 : len(shard r)] for every r in `rows` (sorted
+    member indices), as few launches as the shard_bounds layout allows: one
+    per run of consecutive equal-sized rows."""
+    runs = []
+    for r in rows:
+        lo, hi = shard_bounds(count, size, world, r)
+        nbytes = (hi - lo) * size
+        if runs and runs[-1][1] + runs[-1][2] == r and runs[-1][3] == nbytes:
+            runs[-1][2] += 1
+        else:
+            runs.append([lo * size, r, 1, nbytes])
+    for off, first, n, nbytes in runs:
+        _lib.check(ctx.gather_multi(out_ptr + off, ptrs[first:first + n], nbytes),
+                   "ucg_builtin_dev_gather_multi")
+
+
+def oneshot_allreduce(ctx, send_peers, recv_peers, count, dt, op, rank, world, barrier):
+    """Allreduce in two one-shot launches over peer-mapped buffers (xGMI):
+
+      1. reduce-scatter: member r reads shard r of every member's send buffer
+         (send_peers) and writes V(r, log2 N) - the reference recursive-doubling
+         plan's per-element association (builtin_recursive.c:158-169) - into
+         shard r of its own recv buffer;
+      2. barrier();
+      3. all-gather: member r reads every other shard from its owner's recv
+         buffer (recv_peers), all peers at once;
+      4. barrier() - no member may overwrite its recv buffer (the next
+         operation's step 1) while a peer still reads it.
+
+    Same result as the plan on every member, bit for bit, for a commutative op
+    (every member's V(self, log2 N) pairs the same subsets); it moves
+    2 (N-1)/N x S per member instead of the plan's log2(N) x S, over all N-1
+    links at once instead of one link per step. `barrier` must order the
+    device work of all members: a stream-ordered collective (RCCL all_reduce
+    of one element on the launch stream) or, for members sharing one GPU in
+    tests, ctx.sync() + a host barrier."""
+    size = _lib.DTYPE_SIZE[_lib.dt_index(dt)]
+    lo, hi = shard_bounds(count, size, world, rank)
+    out = recv_peers.ptrs[rank]
+    srcs = [p + lo * size for p in send_peers.ptrs]
+    _lib.check(ctx.reduce_multi(op, dt, out + lo * size, srcs, rank, hi - lo),
+               "ucg_builtin_dev_reduce_multi")
+    barrier()
+    if world > 1:
+        shard_ptrs = [p + shard_bounds(count, size, world, r)[0] * size
+                      for r, p in enumerate(recv_peers.ptrs)]
+        for rows in (list(range(rank)), list(range(rank + 1, world))):
+            if rows:
+                _gather_rows(ctx, out, shard_ptrs, rows, count, size, world)
+    barrier()
+
+
+def stream_barrier(dist, device, group=None):
+    """A barrier on the device streams of all members, without a host sync:
+    an RCCL all_reduce of one element enqueued on the current stream completes
+    only after every member's earlier work on its stream has (each member's
+    contribution is sent after that work), and later work waits for it."""
+    import torch
+    flag = torch.zeros(1, dtype=torch.int32, device=device)
+
+    def barrier():
+        dist.all_reduce(flag, group=group)
+    return barrier
+
+
 def oracle_shard(op, dt, inputs, rank, world, oracle):
     """Expected one-shot shard for tests: the plan's result on the owner."""
     size = np.dtype(inputs[0].dtype).itemsize
