@@ -228,12 +228,15 @@ ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
 ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx);
 
 /* ---- peer mapping (xGMI) for the one-shot multi-operand combine ----------*/
-/* An exported device buffer: the HIP IPC handle of its allocation plus the
- * byte offset of the pointer inside that allocation. Opaque, fixed size.
+/* An exported device buffer: the HIP IPC handle of its allocation, the byte
+ * offset of the pointer inside that allocation and the allocation's size
+ * (import refuses a mapping that does not cover it). Opaque, fixed size.
+ * Lifetime (HIP IPC contract): every importer releases its mapping before
+ * the exporter frees the memory.
  * The memory must come from an allocation of its own (ucg_builtin_dev_malloc,
  * a hipMalloc of >= 2 MiB, a caching-allocator segment): the runtime may carve
  * small hipMalloc blocks out of a shared block, which it refuses to export. */
-#define UCG_BUILTIN_DEV_IPC_HANDLE_BYTES 80
+#define UCG_BUILTIN_DEV_IPC_HANDLE_BYTES 96
 ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
                                         const void *dev_ptr, void *handle);
 /* Map a peer's exported buffer into this process (lazy peer access). */

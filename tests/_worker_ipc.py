@@ -1,7 +1,14 @@
 """One rank of the GPU peer-mapping test: every rank lives on cuda:0 (the
-only GPU of the test box), maps every other rank's buffer through the IPC
-C-ABI and computes its shard with the one-shot recursive-doubling kernel,
-checked bit for bit against the oracle's simulation of the reference plan."""
+only GPU of the test box), maps every other rank's buffers through the IPC
+C-ABI and runs the one-shot kernels over them, each result checked bit for bit
+against the oracle's simulation of the reference plan:
+
+  reduce-scatter  shard r of every member's send buffer -> V(r, log2 N)
+  all-gather      every member's reduced shard, read in place
+  allreduce       both in one operation into a recv buffer
+
+Every buffer is exported once, and all mappings are released by every
+member (PeerBuffers.close, a collective) before any member frees a buffer."""
 import os
 import sys
 
@@ -17,67 +24,60 @@ CASES = [("float32", "sum", "special"), ("float64", "sum", "round"),
          ("bfloat16", "max", "special")]
 
 
+def fail(rank, what):
+    print(f"rank {rank}: MISMATCH {what}", flush=True)
+    sys.exit(1)
+
+
 def main():
     rank = int(os.environ["RANK"])
     world = int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ctx = xucg_amd.DevContext(device=0)
+
+    def barrier():
+        ctx.sync()
+        dist.barrier()
+
     n = 100_003
     for dt, op, dname in CASES:
         st = O.storage(dt)
         sz = np.dtype(st).itemsize
         inputs = [O.fill(dt, dname, 300 + r, n) for r in range(world)]
-        buf = ctx.alloc(n * sz)
+        shards = [G.oracle_shard(op, dt, inputs, r, world, O) for r in range(world)]
+        buf, out, full = ctx.alloc(n * sz), ctx.alloc(n * sz), ctx.alloc(n * sz)
         buf.upload(inputs[rank])
-        out = ctx.alloc(n * sz)
-        peers = G.PeerBuffers(ctx, buf.ptr, rank, world, dist)
-        ctx.sync()
-        dist.barrier()                      # every input is complete
-        lo, hi = G.oneshot_reduce_scatter(ctx, peers, out.ptr, n, dt, op, rank, world)
-        ctx.sync()
-        dist.barrier()                      # every reader is done
-        got = out.download(st, hi - lo)
-        _, _, want = G.oracle_shard(op, dt, inputs, rank, world, O)
-        peers.close()
-        if not (O.bits(got) == O.bits(want)).all():
-            print(f"rank {rank}: MISMATCH {dt} {op}", flush=True)
-            sys.exit(1)
-        # one-shot all-gather of the reduced shards, read from every peer
-        full = ctx.alloc(n * sz)
-        speers = G.PeerBuffers(ctx, out.ptr, rank, world, dist)
-        G.oneshot_all_gather(ctx, speers, full.ptr, n, dt, world)
-        ctx.sync()
-        dist.barrier()
-        speers.close()
-        allgot = full.download(st, n)
-        for r in range(world):
-            rlo, rhi, rwant = G.oracle_shard(op, dt, inputs, r, world, O)
-            if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
-                print(f"rank {rank}: all-gather MISMATCH {dt} {op} shard {r}", flush=True)
-                sys.exit(1)
-        # one-shot allreduce: reduce-scatter into the recv buffer's own shard,
-        # then every other shard read from its owner; every member ends with
-        # the plan's result on every shard
         ctx.fill(dt, "special", 999, full, n)      # stale contents must not pass
         ctx.sync()
-        rpeers = G.PeerBuffers(ctx, full.ptr, rank, world, dist)
         peers = G.PeerBuffers(ctx, buf.ptr, rank, world, dist)
+        speers = G.PeerBuffers(ctx, out.ptr, rank, world, dist)
+        rpeers = G.PeerBuffers(ctx, full.ptr, rank, world, dist)
+        dist.barrier()                      # every input is complete
 
-        def barrier():
-            ctx.sync()
-            dist.barrier()
+        lo, hi = G.oneshot_reduce_scatter(ctx, peers, out.ptr, n, dt, op, rank, world)
+        barrier()                           # every shard reduced, every reader done
+        if not (O.bits(out.download(st, hi - lo)) == O.bits(shards[rank][2])).all():
+            fail(rank, f"reduce-scatter {dt} {op}")
+
+        G.oneshot_all_gather(ctx, speers, full.ptr, n, dt, world)
+        barrier()
+        allgot = full.download(st, n)
+        for r, (rlo, rhi, rwant) in enumerate(shards):
+            if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
+                fail(rank, f"all-gather {dt} {op} shard {r}")
+
+        ctx.fill(dt, "special", 998, full, n)
+        barrier()
         G.oneshot_allreduce(ctx, peers, rpeers, n, dt, op, rank, world, barrier)
         allgot = full.download(st, n)
-        rpeers.close()
-        peers.close()
-        for r in range(world):
-            rlo, rhi, rwant = G.oracle_shard(op, dt, inputs, r, world, O)
+        for r, (rlo, rhi, rwant) in enumerate(shards):
             if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
-                print(f"rank {rank}: allreduce MISMATCH {dt} {op} shard {r}", flush=True)
-                sys.exit(1)
-        full.free()
-        buf.free()
-        out.free()
+                fail(rank, f"allreduce {dt} {op} shard {r}")
+
+        for p in (peers, speers, rpeers):
+            p.close()                       # collective: all mappings gone
+        for b in (buf, out, full):
+            b.free()
     dist.barrier()
     ctx.close()
     dist.destroy_process_group()

@@ -35,7 +35,7 @@ UCS_ERR_CANCELED = -16
 UCS_ERR_OUT_OF_RANGE = -19
 UCS_ERR_TIMED_OUT = -20
 UCS_ERR_UNSUPPORTED = -22
-IPC_HANDLE_BYTES = 80  # UCG_BUILTIN_DEV_IPC_HANDLE_BYTES
+IPC_HANDLE_BYTES = 96  # UCG_BUILTIN_DEV_IPC_HANDLE_BYTES
 
 # every exported C-ABI function: name -> (restype, argtypes)
 _vp = ctypes.c_void_p

@@ -866,7 +866,8 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
 /* ---- peer mapping ------------------------------------------------------- */
 struct ipc_blob {
     hipIpcMemHandle_t handle;
-    uint64_t          offset;
+    uint64_t          offset;   /* of the exported pointer in its allocation */
+    uint64_t          size;     /* of the allocation, checked on import */
     uint64_t          magic;
 };
 static_assert(sizeof(ipc_blob) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES,
@@ -890,6 +891,7 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
     memset(&b, 0, sizeof(b));
     HIP_TRY(hipIpcGetMemHandle(&b.handle, (void*)base));
     b.offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
+    b.size   = (uint64_t)size;
     b.magic  = kIpcMagic;
     memset(handle, 0, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
     memcpy(handle, &b, sizeof(b));
@@ -913,6 +915,17 @@ ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
     }
     void *base = nullptr;
     HIP_TRY(hipIpcOpenMemHandle(&base, b.handle, hipIpcMemLazyEnablePeerAccess));
+    /* the mapping must span the exporter's whole allocation: a short or
+     * stale mapping is refused here instead of faulting a kernel later */
+    hipDeviceptr_t mbase = nullptr;
+    size_t msize = 0;
+    const hipError_t e = hipMemGetAddressRange(&mbase, &msize, (hipDeviceptr_t)base);
+    if (e != hipSuccess || mbase != (hipDeviceptr_t)base || msize < b.size ||
+        b.offset >= b.size) {
+        (void)hipIpcCloseMemHandle(base);
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import",
+                         "mapped range does not cover the exported allocation");
+    }
     *dev_ptr = (char*)base + b.offset;
     return UCS_OK;
 }

@@ -152,11 +152,14 @@ class PeerBuffers:
     """Every member's buffer mapped into this process (IPC over xGMI).
 
     ptrs[r] is a device pointer to member r's buffer (the local one for
-    r == rank). Collective: every member must construct it together."""
+    r == rank). Collective: every member must construct it together, and
+    close it together before any member frees its buffer (HIP leaves a free
+    under a live importer undefined); close() ends with a barrier for that."""
 
     def __init__(self, ctx, local_ptr, rank, world, dist, group=None):
         self.ctx = ctx
         self.rank = rank
+        self._dist, self._group = dist, group
         self.ptrs = []
         self._imported = []
         # every member takes part in every collective below whatever fails
@@ -192,9 +195,21 @@ class PeerBuffers:
             raise RuntimeError(f"PeerBuffers: {err}")
 
     def close(self):
+        """Release the peer mappings, then wait for every member to have done
+        the same: after close() returns each member may free its buffer."""
+        if self._dist is None:
+            return
+        err = None
         for p in self._imported:
-            self.ctx.ipc_release(p)
+            try:
+                self.ctx.ipc_release(p)
+            except Exception as e:  # noqa: BLE001 - after the barrier
+                err = err or e
         self._imported = []
+        dist, self._dist = self._dist, None
+        dist.barrier(group=self._group)
+        if err is not None:
+            raise err
 
 
 def oneshot_reduce_scatter(ctx, peers, out_ptr, count, dt, op, rank, world):
