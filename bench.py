@@ -633,7 +633,7 @@ def main():
             "bytes": n * 4, "ms": round(th * 1e3, 3),
             "gibs_3n": round(3 * n * 4 / th / GIB, 2),
             "gibs_n": round(n * 4 / th / GIB, 2),
-            "note": "pinned host src/dst -> H2D -> kernel -> D2H, 8 MiB chunks on 2 streams"}
+            "note": "pinned host src/dst -> H2D -> kernel -> D2H, 16 MiB chunks on 2 streams"}
         hs.free()
         hd.free()
 

@@ -60,7 +60,7 @@ typedef struct ucg_builtin_combine_config {
                                 buffers on reduce_cb_f; force: host buffers
                                 of >= dev_min_bytes are staged on the GPU too */
     size_t   dev_min_bytes;  /* UCX_BUILTIN_DEV_MIN_BYTES    (default 1 MiB)   */
-    size_t   stage_bytes;    /* UCX_BUILTIN_DEV_STAGE_BYTES  (default 8 MiB)   */
+    size_t   stage_bytes;    /* UCX_BUILTIN_DEV_STAGE_BYTES  (default 16 MiB)  */
     unsigned stage_slots;    /* UCX_BUILTIN_DEV_STAGE_SLOTS  (default 4)       */
     int      device;         /* UCX_BUILTIN_DEV_DEVICE       (default -1)      */
 } ucg_builtin_combine_config_t;

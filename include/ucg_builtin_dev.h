@@ -141,7 +141,7 @@ typedef struct ucg_builtin_dev_ctx_params {
     int      device;       /* HIP device ordinal; -1 = the calling thread's */
     void    *stream;       /* hipStream_t to launch on; NULL = create one
                               (so the legacy null stream cannot be chosen) */
-    size_t   stage_bytes;  /* pinned staging slot size; 0 = 8 MiB */
+    size_t   stage_bytes;  /* pinned staging slot size; 0 = 16 MiB */
     unsigned stage_slots;  /* staging ring depth; 0 = 4 */
 } ucg_builtin_dev_ctx_params_t;
 

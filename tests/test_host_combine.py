@@ -30,8 +30,9 @@ def test_config_from_environment(monkeypatch):
     assert host.read_config().dev_enable == 2
     monkeypatch.delenv("UCX_BUILTIN_DEV_COMBINE")
     monkeypatch.delenv("UCX_BUILTIN_DEV_MIN_BYTES")
+    monkeypatch.delenv("UCX_BUILTIN_DEV_STAGE_BYTES")
     c = host.read_config()
-    assert c.dev_enable == 1 and c.dev_min_bytes == 1 << 20
+    assert c.dev_enable == 1 and c.dev_min_bytes == 1 << 20 and c.stage_bytes == 16 << 20
 
 
 def test_classification_through_api_callbacks():

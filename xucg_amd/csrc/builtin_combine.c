@@ -92,7 +92,7 @@ void ucg_builtin_combine_config_read(ucg_builtin_combine_config_t *cfg)
     cfg->dev_min_bytes = parse_memunits(getenv("UCX_BUILTIN_DEV_MIN_BYTES"),
                                         1u << 20);
     cfg->stage_bytes   = parse_memunits(getenv("UCX_BUILTIN_DEV_STAGE_BYTES"),
-                                        8u << 20);
+                                        16u << 20);
     cfg->stage_slots   = (unsigned)parse_memunits(
                                         getenv("UCX_BUILTIN_DEV_STAGE_SLOTS"), 4);
     cfg->device        = dev ? atoi(dev) : -1;
