@@ -285,6 +285,12 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             # one-element RCCL all_reduce) instead of host syncs
             sbar = G.stream_barrier(dist, dev)
             rpeers = G.PeerBuffers(ctx, ag_out.data_ptr(), rank, world, dist)
+            # push forms (every transfer a write into a peer's buffer): the
+            # shards go into the owners' stages, combined there; the reduced
+            # shard is written into every peer's recv buffer
+            slot = G.stage_slot_bytes(n4, 4, world)
+            stage = torch.empty(world * slot // 4, dtype=torch.float32, device=dev)
+            tpeers = G.PeerBuffers(ctx, stage.data_ptr(), rank, world, dist)
             try:
                 def ar1():
                     G.oneshot_allreduce(ctx, peers, rpeers, n4, "float32", "sum", rank,
@@ -295,11 +301,32 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 t_ar1 = timed(ar1, steps)
                 ar_same = bool(torch.equal(ag_out.view(torch.int32),
                                            ag_rccl.view(torch.int32)))
+
+                def prs():
+                    G.push_reduce_scatter(ctx, x.data_ptr(), tpeers, mine.data_ptr(), n4,
+                                          "float32", "sum", rank, world, sbar)
+                    sbar()
+                mine.zero_()
+                for _ in range(warmup):
+                    prs()
+                t_prs = timed(prs, steps)
+                prs_same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
+
+                def par():
+                    G.push_allreduce(ctx, x.data_ptr(), tpeers, rpeers, n4, "float32", "sum",
+                                     rank, world, sbar)
+                ag_out.zero_()
+                for _ in range(warmup):
+                    par()
+                t_par = timed(par, steps)
+                par_same = bool(torch.equal(ag_out.view(torch.int32),
+                                            ag_rccl.view(torch.int32)))
             finally:
                 torch.cuda.synchronize()
                 dist.barrier()
                 rpeers.close()
-            del ag_rccl
+                tpeers.close()
+            del ag_rccl, stage
             # rounded inputs: RCCL's ring order vs the plan's association,
             # SURVEY.md 8c bound |delta| <= 2 (n-1) u sum_i |x_i|, u = 2^-24
             torch.cuda.synchronize()
@@ -335,6 +362,13 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "oneshot_allreduce_busbw_gbs": round(2 * bus / t_ar1 / 1e9, 1),
                 "oneshot_allreduce_frac_of_xgmi": round(2 * bus / t_ar1 / 1e9 / XGMI_GBS, 4),
                 "oneshot_allreduce_bit_exact_vs_rccl_rs_ag": ar_same,
+                "push_rs_ms": round(t_prs * 1e3, 3),
+                "push_rs_busbw_gbs": round(bus / t_prs / 1e9, 1),
+                "push_rs_frac_of_xgmi": round(bus / t_prs / 1e9 / XGMI_GBS, 4),
+                "push_rs_bit_exact_vs_rccl": prs_same,
+                "push_allreduce_ms": round(t_par * 1e3, 3),
+                "push_allreduce_busbw_gbs": round(2 * bus / t_par / 1e9, 1),
+                "push_allreduce_bit_exact_vs_rccl_rs_ag": par_same,
                 "bit_exact_vs_rccl_on_exact_inputs": same,
                 "rccl_within_8c_tolerance_on_rounded_inputs": within,
                 "max_err_over_tolerance": round(ratio, 4),
@@ -373,10 +407,18 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         ipeers = G.PeerBuffers(ctx, init.data_ptr(), rank, world, dist)
         apeers = G.PeerBuffers(ctx, acc.data_ptr(), rank, world, dist)
 
+        slot5 = G.stage_slot_bytes(n5, 8, world)
+        stage5 = torch.empty(world * slot5 // 8, dtype=torch.float64, device=dev)
+        tpeers = G.PeerBuffers(ctx, stage5.data_ptr(), rank, world, dist)
+
         def once_oneshot():
             # reads every member's send buffer in place: no init_reduce copy
             G.oneshot_allreduce(ctx, ipeers, apeers, n5, "float64", "sum", rank, world,
                                 sbar)
+
+        def once_push():
+            G.push_allreduce(ctx, init.data_ptr(), tpeers, apeers, n5, "float64", "sum",
+                             rank, world, sbar)
 
         # parity: every member's input regenerated locally, one-shot tree
         allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
@@ -390,7 +432,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         for name, fn, link_bytes in (
                 ("doubling", once, n5 * 8 * G.recursive_steps(world)),
                 ("halving", once_halving, 2 * (world - 1) * n5 * 8 // world),
-                ("oneshot_xgmi", once_oneshot, 2 * (world - 1) * n5 * 8 // world)):
+                ("oneshot_xgmi", once_oneshot, 2 * (world - 1) * n5 * 8 // world),
+                ("oneshot_xgmi_push", once_push, 2 * (world - 1) * n5 * 8 // world)):
             acc.zero_()
             fn()
             torch.cuda.synchronize()
@@ -408,6 +451,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         dist.barrier()
         ipeers.close()
         apeers.close()
+        tpeers.close()
+        del stage5
         # vendor baseline on the same buffer (ring association: tolerance only)
         acc.copy_(init)
         dist.all_reduce(acc)

@@ -180,12 +180,6 @@ ucs_status_t ucg_builtin_dev_reduce(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
                                     ucg_dev_dtype_t dt, void *dst,
                                     const void *src, size_t count);
 
-/* One-shot multi-operand combine in the recursive-doubling association of
- * builtin/plan/builtin_recursive.c:158-169 as seen from member `self`:
- *   V(r,0) = srcs[r];  V(r,k) = V(r ^ 2^(k-1), k-1) (op) V(r, k-1)
- * (left operand = src, right = dst of the reduce_cb_f contract), and writes
- * dst[i] = V(self, log2(nsrc))[i]. nsrc must be a power of two <= 16; srcs may
- * be peer-mapped device pointers (xGMI). dst may alias srcs[self]. */
 /* The all-gather half of a one-shot reduce-scatter + all-gather (SURVEY.md
  * 8e): dst[r * shard_bytes + i] = srcs[r][i] for r < nsrc, every source read in
  * one launch (srcs may be peer-mapped device pointers: member r's shard over
@@ -195,6 +189,21 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                           const void *const *srcs, unsigned nsrc,
                                           size_t shard_bytes);
 
+/* n independent copies of nbytes each in one launch: dsts[i][0:nbytes] =
+ * srcs[i][0:nbytes]. Either side may be peer-mapped (a push over xGMI when the
+ * destinations are peers' buffers); workgroups are dealt round-robin over the
+ * pairs so every link streams at once. Sources may repeat (a broadcast of one
+ * shard to every peer); destinations must not overlap. n <= 16. */
+ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
+                                        void *const *dsts, const void *const *srcs,
+                                        unsigned n, size_t nbytes);
+
+/* One-shot multi-operand combine in the recursive-doubling association of
+ * builtin/plan/builtin_recursive.c:158-169 as seen from member `self`:
+ *   V(r,0) = srcs[r];  V(r,k) = V(r ^ 2^(k-1), k-1) (op) V(r, k-1)
+ * (left operand = src, right = dst of the reduce_cb_f contract), and writes
+ * dst[i] = V(self, log2(nsrc))[i]. nsrc must be a power of two <= 16; srcs may
+ * be peer-mapped device pointers (xGMI). dst may alias srcs[self]. */
 ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
                                           ucg_dev_op_t op, ucg_dev_dtype_t dt,
                                           void *dst, const void *const *srcs,

@@ -6,6 +6,8 @@ against the oracle's simulation of the reference plan:
   reduce-scatter  shard r of every member's send buffer -> V(r, log2 N)
   all-gather      every member's reduced shard, read in place
   allreduce       both in one operation into a recv buffer
+  push forms      the same reduce-scatter and allreduce with every transfer a
+                  write into a peer's buffer (stage slots, recv shards)
 
 Every buffer is exported once, and all mappings are released by every
 member (PeerBuffers.close, a collective) before any member frees a buffer."""
@@ -46,12 +48,14 @@ def main():
         inputs = [O.fill(dt, dname, 300 + r, n) for r in range(world)]
         shards = [G.oracle_shard(op, dt, inputs, r, world, O) for r in range(world)]
         buf, out, full = ctx.alloc(n * sz), ctx.alloc(n * sz), ctx.alloc(n * sz)
+        stage = ctx.alloc(world * G.stage_slot_bytes(n, sz, world))
         buf.upload(inputs[rank])
         ctx.fill(dt, "special", 999, full, n)      # stale contents must not pass
         ctx.sync()
         peers = G.PeerBuffers(ctx, buf.ptr, rank, world, dist)
         speers = G.PeerBuffers(ctx, out.ptr, rank, world, dist)
         rpeers = G.PeerBuffers(ctx, full.ptr, rank, world, dist)
+        tpeers = G.PeerBuffers(ctx, stage.ptr, rank, world, dist)
         dist.barrier()                      # every input is complete
 
         lo, hi = G.oneshot_reduce_scatter(ctx, peers, out.ptr, n, dt, op, rank, world)
@@ -74,9 +78,25 @@ def main():
             if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
                 fail(rank, f"allreduce {dt} {op} shard {r}")
 
-        for p in (peers, speers, rpeers):
+        # push forms: shards written into the peers' stages, then combined
+        # locally; the reduced shard written into every peer's recv buffer
+        ctx.fill(dt, "special", 997, out, n)
+        barrier()
+        G.push_reduce_scatter(ctx, buf.ptr, tpeers, out.ptr, n, dt, op, rank, world, barrier)
+        barrier()
+        if not (O.bits(out.download(st, hi - lo)) == O.bits(shards[rank][2])).all():
+            fail(rank, f"push reduce-scatter {dt} {op}")
+        ctx.fill(dt, "special", 996, full, n)
+        barrier()
+        G.push_allreduce(ctx, buf.ptr, tpeers, rpeers, n, dt, op, rank, world, barrier)
+        allgot = full.download(st, n)
+        for r, (rlo, rhi, rwant) in enumerate(shards):
+            if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
+                fail(rank, f"push allreduce {dt} {op} shard {r}")
+
+        for p in (peers, speers, rpeers, tpeers):
             p.close()                       # collective: all mappings gone
-        for b in (buf, out, full):
+        for b in (buf, out, full, stage):
             b.free()
     dist.barrier()
     ctx.close()

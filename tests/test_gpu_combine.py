@@ -342,6 +342,33 @@ def test_gather_multi(dev_ctx, nsrc, shard, offset):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,nbytes,offset", [(1, 4096, 0), (7, 1 << 20, 0), (16, 100_000, 0),
+                                             (5, 4099, 0), (3, 65536, 4), (8, 33, 1)])
+def test_copy_multi(dev_ctx, n, nbytes, offset):
+    """n independent copies in one launch; sources repeat (pairs 0 and 1 read
+    the same source, as the push all-gather's broadcast does)."""
+    srcs = [np.frombuffer(np.random.default_rng(10 + r).bytes(nbytes), np.uint8)
+            for r in range(n)]
+    sbufs = [dev_ctx.alloc(nbytes + 16) for _ in range(n)]
+    dbufs = [dev_ctx.alloc(nbytes + 16) for _ in range(n)]
+    try:
+        for b, s in zip(sbufs, srcs):
+            b.upload(s, offset)
+        src_ptrs = [b.ptr + offset for b in sbufs]
+        if n > 1:
+            src_ptrs[1] = src_ptrs[0]
+            srcs[1] = srcs[0]
+        rc = dev_ctx.copy_multi([b.ptr + offset for b in dbufs], src_ptrs, nbytes)
+        assert rc == 0, _lib.last_error()
+        dev_ctx.sync()
+        for b, s in zip(dbufs, srcs):
+            assert (b.download(np.uint8, nbytes, offset) == s).all()
+    finally:
+        for b in sbufs + dbufs:
+            b.free()
+
+
+@pytest.mark.gpu
 def test_gather_multi_split_dispatch(dev_ctx):
     """16 rows of 2^31 + 48 bytes: past 2^31 / 16 vectors per row, so the
     copy takes two dispatches (work-items are counted in 32 bits). The rows

@@ -77,10 +77,13 @@ def test_bench_collective_phases_world1():
     assert c4["rccl_within_8c_tolerance_on_rounded_inputs"] is True, c4
     assert c4["oneshot_ag_bit_exact_vs_rccl"] is True, c4
     assert c4["oneshot_allreduce_bit_exact_vs_rccl_rs_ag"] is True, c4
+    assert c4["push_rs_bit_exact_vs_rccl"] is True, c4
+    assert c4["push_allreduce_bit_exact_vs_rccl_rs_ag"] is True, c4
     c5 = coll["c5_recursive_allreduce_512mib_fp64"]
     assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["oneshot_xgmi"]["bit_exact_vs_oneshot_tree"] is True, c5
+    assert c5["oneshot_xgmi_push"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["rccl_allreduce_within_8c_tolerance_of_plan"] is True, c5
 
 
@@ -109,6 +112,13 @@ class _SimCtx:
         self.calls.append(("reduce_multi", len(srcs), count))
         return 0
 
+    def copy_multi(self, dsts, srcs, nbytes):
+        assert len(dsts) == len(srcs) <= 16
+        for d, s in zip(dsts, srcs):
+            self.mem[d:d + nbytes] = self.mem[s:s + nbytes]
+        self.calls.append(("copy_multi", len(dsts), nbytes))
+        return 0
+
     def gather_multi(self, dst, srcs, nbytes):
         for i, s in enumerate(srcs):
             self.mem[dst + i * nbytes:dst + (i + 1) * nbytes] = self.mem[s:s + nbytes]
@@ -121,10 +131,11 @@ class _Peers:
         self.ptrs = ptrs
 
 
+@pytest.mark.parametrize("variant", ["pull", "push"])
 @pytest.mark.parametrize("world", [1, 2, 4, 8, 16])
 @pytest.mark.parametrize("dt,op,count", [("float32", "sum", 1001), ("int64", "prod", 4099),
                                          ("float16", "max", 7), ("float64", "sum", 1 << 14)])
-def test_oneshot_allreduce_schedule(world, dt, op, count):
+def test_oneshot_allreduce_schedule(variant, world, dt, op, count):
     """group.oneshot_allreduce with one thread per member over a shared
     host array: every member ends with shard r = V(r, log2 N) (the plan's
     association, from the oracle) for every r, and the all-gather skips the
@@ -135,9 +146,11 @@ def test_oneshot_allreduce_schedule(world, dt, op, count):
     nb = count * st.itemsize
     inputs = [O.fill(dt, "special" if dt == "float16" else "round", 70 + r, count)
               for r in range(world)]
-    mem = np.zeros(2 * world * nb + 64, np.uint8)
+    slot = G.stage_slot_bytes(count, st.itemsize, world)
+    mem = np.zeros(2 * world * nb + world * world * slot + 64, np.uint8)
     send = [r * nb for r in range(world)]
     recv = [(world + r) * nb for r in range(world)]
+    stage = [2 * world * nb + r * world * slot for r in range(world)]
     for r in range(world):
         mem[send[r]:send[r] + nb] = inputs[r].view(np.uint8)
     bar = threading.Barrier(world)
@@ -146,8 +159,13 @@ def test_oneshot_allreduce_schedule(world, dt, op, count):
 
     def member(r):
         try:
-            G.oneshot_allreduce(_SimCtx(mem, dt, calls[r]), _Peers(send), _Peers(recv),
-                                count, dt, op, r, world, bar.wait)
+            ctx = _SimCtx(mem, dt, calls[r])
+            if variant == "pull":
+                G.oneshot_allreduce(ctx, _Peers(send), _Peers(recv), count, dt, op, r, world,
+                                    bar.wait)
+            else:
+                G.push_allreduce(ctx, send[r], _Peers(stage), _Peers(recv), count, dt, op,
+                                 r, world, bar.wait)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
             bar.abort()
@@ -162,7 +180,14 @@ def test_oneshot_allreduce_schedule(world, dt, op, count):
     for r in range(world):
         got = mem[recv[r]:recv[r] + nb].view(st)
         assert (O.bits(got) == O.bits(want)).all(), (r, dt, op)
-        gathered = sum(n for kind, n, _ in calls[r] if kind == "gather_multi")
-        assert gathered == world - 1
-        # runs: before self, after self, and the unequal last shard apart
-        assert len([c for c in calls[r] if c[0] == "gather_multi"]) <= 3
+        if variant == "pull":
+            gathered = sum(n for kind, n, _ in calls[r] if kind == "gather_multi")
+            assert gathered == world - 1
+            # runs: before self, after self, and the unequal last shard apart
+            assert len([c for c in calls[r] if c[0] == "gather_multi"]) <= 3
+        else:
+            # scatter: one launch per shard size (the last shard may differ);
+            # all-gather: one launch
+            pushes = [c for c in calls[r] if c[0] == "copy_multi"]
+            assert sum(n for _, n, _ in pushes) == 2 * (world - 1)
+            assert len(pushes) <= 3

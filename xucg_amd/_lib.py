@@ -67,6 +67,8 @@ DEV_API = {
     "ucg_builtin_dev_reduce_multi": (_st, [_vp, _int, _int, _vp,
                                            ctypes.POINTER(_vp), _u, _u, _sz]),
     "ucg_builtin_dev_gather_multi": (_st, [_vp, _vp, ctypes.POINTER(_vp), _u, _sz]),
+    "ucg_builtin_dev_copy_multi": (_st, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _u,
+                                         _sz]),
     "ucg_builtin_dev_combine_host": (_st, [_vp, _int, _int, _vp, _vp, _sz]),
     "ucg_builtin_dev_stage_begin": (_st, [_vp, _vp, _sz]),
     "ucg_builtin_dev_combine": (_st, [_vp, _int, _int, _sz, _vp, _sz]),

@@ -579,6 +579,94 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
     return UCS_OK;
 }
 
+/* ---- n independent copies in one launch (push over xGMI) --------------- */
+struct PairList {
+    void       *d[kMaxMulti];
+    const void *s[kMaxMulti];
+};
+
+/* one 16-B vector per lane of pair (wg % n), as k_gather_multi */
+static __global__ void __launch_bounds__(kReduceBlock)
+k_copy_multi(PairList pl, unsigned n, size_t nbytes)
+{
+    const unsigned r  = blockIdx.x % n;
+    const size_t wg   = blockIdx.x / n;
+    const char *src   = static_cast<const char*>(pl.s[r]);
+    char *out         = static_cast<char*>(pl.d[r]);
+    const size_t nvec = nbytes / 16;
+    const size_t i    = wg * kReduceBlock + threadIdx.x;
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(out) + i,
+                ld16<1>(reinterpret_cast<const u32x4*>(src) + i));
+    }
+}
+
+static __global__ void __launch_bounds__(kBlock)
+k_copy_multi_bytes(PairList pl, unsigned n, size_t nbytes)
+{
+    const unsigned r = blockIdx.x % n;
+    const size_t wg  = blockIdx.x / n;
+    const size_t nwg = gridDim.x / n;
+    const char *src  = static_cast<const char*>(pl.s[r]);
+    char *out        = static_cast<char*>(pl.d[r]);
+    for (size_t i = wg * kBlock + threadIdx.x; i < nbytes; i += nwg * kBlock) {
+        out[i] = src[i];
+    }
+}
+
+ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
+                                        void *const *dsts, const void *const *srcs,
+                                        unsigned n, size_t nbytes)
+{
+    if (ctx == nullptr || dsts == nullptr || srcs == nullptr || n == 0 ||
+        n > (unsigned)kMaxMulti) {
+        return set_error(UCS_ERR_INVALID_PARAM, "copy_multi",
+                         "bad arguments (n must be 1..16)");
+    }
+    if (nbytes == 0) {
+        return UCS_OK;
+    }
+    PairList pl;
+    bool aligned = nbytes % 16 == 0;
+    for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
+        pl.d[i] = (i < n) ? dsts[i] : nullptr;
+        pl.s[i] = (i < n) ? srcs[i] : nullptr;
+        if (i < n) {
+            if (dsts[i] == nullptr || srcs[i] == nullptr) {
+                return set_error(UCS_ERR_INVALID_PARAM, "copy_multi", "NULL pointer");
+            }
+            aligned = aligned && ((uintptr_t)dsts[i] % 16) == 0 &&
+                      ((uintptr_t)srcs[i] % 16) == 0;
+        }
+    }
+    if (!aligned) {
+        const unsigned grid = grid_for(nbytes, kBlock, 1024) * n;
+        hipLaunchKernelGGL(k_copy_multi_bytes, dim3(grid), dim3(kBlock), 0, ctx->stream,
+                           pl, n, nbytes);
+    } else {
+        /* at most 2^31 work-items per dispatch: 2^31 / n vectors of every pair */
+        const size_t nvec    = nbytes / 16;
+        const size_t per_max = (((size_t)1 << 31) / n) / kReduceBlock * kReduceBlock;
+        size_t done = 0;
+        do {
+            const size_t chunk = nvec - done < per_max ? nvec - done : per_max;
+            PairList c = pl;
+            for (unsigned i = 0; i < n; i++) {
+                c.d[i] = static_cast<char*>(pl.d[i]) + done * 16;
+                c.s[i] = static_cast<const char*>(pl.s[i]) + done * 16;
+            }
+            const size_t grid = div_up(chunk, kReduceBlock) * n;
+            hipLaunchKernelGGL(k_copy_multi, dim3((unsigned)grid), dim3(kReduceBlock), 0,
+                               ctx->stream, c, n, chunk * 16);
+            done += chunk;
+        } while (done < nvec);
+    }
+    HIP_TRY(hipGetLastError());
+    ctx->counters[0]++;
+    ctx->counters[1] += 2 * (uint64_t)n * nbytes;
+    return UCS_OK;
+}
+
 /* ---- host-resident whole-buffer combine (pipelined) --------------------- */
 ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
                                           ucg_dev_op_t op, ucg_dev_dtype_t dt,

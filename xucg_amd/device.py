@@ -197,6 +197,15 @@ class DevContext:
         return _lib.dev().ucg_builtin_dev_gather_multi(self.handle, _ptr(dst), arr,
                                                        len(srcs), shard_bytes)
 
+    def copy_multi(self, dsts, srcs, nbytes):
+        """dsts[i][:nbytes] = srcs[i][:nbytes] for every pair, one launch."""
+        n = len(dsts)
+        if len(srcs) != n:
+            raise ValueError("copy_multi: as many sources as destinations")
+        da = (ctypes.c_void_p * n)(*[_ptr(d) for d in dsts])
+        sa = (ctypes.c_void_p * n)(*[_ptr(s) for s in srcs])
+        return _lib.dev().ucg_builtin_dev_copy_multi(self.handle, da, sa, n, nbytes)
+
     def combine_host(self, op, dt, dst_host, src_host, count):
         return _lib.dev().ucg_builtin_dev_combine_host(self.handle, op_index(op),
                                                        dt_index(dt), _ptr(dst_host),

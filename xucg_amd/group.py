@@ -295,6 +295,75 @@ def oneshot_allreduce(ctx, send_peers, recv_peers, count, dt, op, rank, world, b
     barrier()
 
 
+def stage_slot_bytes(count, elem_size, world):
+    """Slot size of the push reduce-scatter's stage: the largest shard (the
+    last one), rounded up to 256 B."""
+    lo, hi = shard_bounds(count, elem_size, world, world - 1)
+    return ((hi - lo) * elem_size + 255) // 256 * 256
+
+
+def _copy_pairs(ctx, pairs):
+    """pairs: (dst, src, nbytes); one copy_multi launch per distinct size."""
+    by_size = {}
+    for d, s_, n in pairs:
+        by_size.setdefault(n, []).append((d, s_))
+    for n, ps in by_size.items():
+        for i in range(0, len(ps), 16):
+            chunk = ps[i:i + 16]
+            _lib.check(ctx.copy_multi([d for d, _ in chunk], [s_ for _, s_ in chunk], n),
+                       "ucg_builtin_dev_copy_multi")
+
+
+def push_reduce_scatter(ctx, x_ptr, stage_peers, out_ptr, count, dt, op, rank, world,
+                        barrier):
+    """The push form of the one-shot reduce-scatter, for links that move
+    writes better than reads:
+
+      1. member r writes shard p of its buffer x into slot r of member p's
+         stage, all peers at once (one copy_multi launch);
+      2. barrier();
+      3. member r combines its stage's slots (slot r read in place from x) in
+         the plan's association: out = V(r, log2 N) (reduce_multi, self = r).
+
+    stage_peers maps every member's stage of `world` slots of
+    stage_slot_bytes(). Same result, bit for bit, as oneshot_reduce_scatter.
+    The caller's next barrier must pass before any member writes into the
+    stages again. Returns the shard's [lo, hi)."""
+    size = _lib.DTYPE_SIZE[_lib.dt_index(dt)]
+    slot = stage_slot_bytes(count, size, world)
+    pairs = []
+    for p in range(world):
+        if p != rank:
+            plo, phi = shard_bounds(count, size, world, p)
+            pairs.append((stage_peers.ptrs[p] + rank * slot, x_ptr + plo * size,
+                          (phi - plo) * size))
+    _copy_pairs(ctx, pairs)
+    barrier()
+    lo, hi = shard_bounds(count, size, world, rank)
+    stage = stage_peers.ptrs[rank]
+    srcs = [x_ptr + lo * size if m == rank else stage + m * slot for m in range(world)]
+    _lib.check(ctx.reduce_multi(op, dt, out_ptr, srcs, rank, hi - lo),
+               "ucg_builtin_dev_reduce_multi")
+    return lo, hi
+
+
+def push_allreduce(ctx, x_ptr, stage_peers, recv_peers, count, dt, op, rank, world,
+                   barrier):
+    """Allreduce by pushes only: push_reduce_scatter into this member's shard
+    of its recv buffer, then the reduced shard written into every peer's recv
+    buffer at the same offset (one copy_multi launch), then barrier(). A
+    member's pushes land only on the peers' copies of its own shard, which no
+    peer writes meanwhile, so one barrier in the middle suffices."""
+    size = _lib.DTYPE_SIZE[_lib.dt_index(dt)]
+    out = recv_peers.ptrs[rank]
+    lo, hi = shard_bounds(count, size, world, rank)
+    push_reduce_scatter(ctx, x_ptr, stage_peers, out + lo * size, count, dt, op, rank,
+                        world, barrier)
+    _copy_pairs(ctx, [(recv_peers.ptrs[p] + lo * size, out + lo * size, (hi - lo) * size)
+                      for p in range(world) if p != rank])
+    barrier()
+
+
 def stream_barrier(dist, device, group=None):
     """A barrier on the device streams of all members, without a host sync:
     an RCCL all_reduce of one element enqueued on the current stream completes
