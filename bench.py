@@ -194,8 +194,13 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     dev = torch.device(f"cuda:{local_rank}")
     out = {}
 
+    t_start = time.perf_counter()
+
     def agreed(fn, name):
         err = None
+        if rank == 0:  # progress on stderr: a multi-minute phase is never silent
+            print(f"[collective] {name} starting at {time.perf_counter() - t_start:.1f} s",
+                  file=sys.stderr, flush=True)
         try:
             res = fn()
         except Exception as e:  # recorded, then agreed on by every rank
@@ -472,6 +477,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         del ref
         return res
     agreed(recursive_doubling, "c5_recursive_allreduce_512mib_fp64")
+    out["wall_s"] = round(time.perf_counter() - t_start, 1)
     return out
 
 
@@ -504,7 +510,7 @@ def same_box_reference(n, iters=50):
             "d2d_copy_gbs": round(2 * n * 4 / (copy_us * 1e-6) / 1e9, 1)}
 
 
-def run_collective_children(dist, rank, world, timeout_s=600):
+def run_collective_children(dist, rank, world, timeout_s=300):
     """Run collective_phases in one child process per rank (a fresh process
     group on a new port), so that a fault in the multi-GPU phases - the IPC
     peer mappings cannot be exercised on the 1-GPU boxes this build is tested
@@ -533,9 +539,10 @@ def run_collective_children(dist, rank, world, timeout_s=600):
     env.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(obj[0]["port"]),
                XUCG_COLLECTIVE_OUT=obj[0]["out"])
     try:
+        # stderr passes through (progress lines), stdout is kept for the error tail
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--collective-child"],
-                           env=env, capture_output=True, text=True, timeout=timeout_s)
-        rc, tail = p.returncode, (p.stdout + p.stderr)[-600:]
+                           env=env, stdout=subprocess.PIPE, text=True, timeout=timeout_s)
+        rc, tail = p.returncode, p.stdout[-600:]
     except subprocess.TimeoutExpired as e:
         rc, tail = "timeout", str(e)[-300:]
     if rank != 0:
