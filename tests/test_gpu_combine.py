@@ -462,3 +462,93 @@ def test_random_multi_cases_against_oracle(dev_ctx):
     finally:
         for b in bufs:
             b.free()
+
+
+SHIFT_COUNTS = [1, 5, 16, 17, 63 * 4 + 3, 64 * 16, 64 * 16 + 1, 65 * 16 + 7, 128 * 16, 4099,
+                64 * 64 * 16 + 9]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["int8", "float16", "float32", "float64"])
+def test_shift_kernel_every_phase(dev_ctx, dt):
+    """k_reduce_shift (src and dst disagree mod 16 B): every (src, dst)
+    phase pair in whole elements, counts that end a wave on its last lane or
+    just past it (vector counts that are multiples of 64 and their
+    neighbours), with guard bytes around dst checked untouched, and src
+    placed both at the start and flush with the end of its allocation."""
+    st = O.storage(dt)
+    sz = np.dtype(st).itemsize
+    op = "sum"
+    granule = 2 << 20
+    bs, bd = dev_ctx.alloc(granule), dev_ctx.alloc(granule)
+    try:
+        for count in SHIFT_COUNTS:
+            nb = count * sz
+            src = O.fill(dt, "round", 77 + count, count)
+            dst = O.fill(dt, "round", 99 + count, count)
+            want = O.reduce(op, dt, src, dst)
+            for sp in range(0, 16, sz):
+                for dp in range(0, 16, sz):
+                    if sp == dp and count not in (17, 4099):
+                        continue  # the aligned kernel: covered elsewhere
+                    for at_end in (False, True):
+                        # at_end: the last offset of phase sp that still fits
+                        so = ((granule - nb - sp) // 16) * 16 + sp if at_end else sp
+                        do = 64 + dp
+                        guard = np.full(do + nb + 64, 0xA5, np.uint8)
+                        bd.upload(guard)
+                        bd.upload(dst, do)
+                        bs.upload(src, so)
+                        dev_ctx.reduce_checked(op, dt, bd.ptr + do, bs.ptr + so, count)
+                        dev_ctx.sync()
+                        got = bd.download(st, count, do)
+                        assert (O.bits(got) == O.bits(want)).all(), (count, sp, dp, at_end)
+                        raw = bd.download(np.uint8, do + nb + 64)
+                        assert (raw[:do] == 0xA5).all() and (raw[do + nb:] == 0xA5).all(), \
+                            (count, sp, dp, "guard bytes overwritten")
+    finally:
+        bs.free()
+        bd.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["float32", "float16", "int8", "float64"])
+def test_staged_runs_keep_the_accumulator_phase(dt):
+    """Staged fragments into a device-resident recv buffer at every 16-B
+    phase (the accumulator is the buffer itself): each run is laid out in the
+    ring at the accumulator's phase, so the run's launch is an aligned one.
+    Fragments of the reference's AM size from two interleaved senders,
+    bit-exact against the per-fragment oracle in arrival order, and one
+    launch per run (no more launches than with a phase-0 buffer)."""
+    st = O.storage(dt)
+    sz = np.dtype(st).itemsize
+    n = 20_000 + 1
+    frag = O.frag_length(256, sz)
+    acc = O.fill(dt, "round", 17, n)
+    peers = [O.fill(dt, "round", 18 + p, n) for p in range(2)]
+    want = acc.copy()
+    order = [(p, off) for off in range(0, n * sz, frag) for p in range(2)]
+    for p, off in order:
+        cnt = min(frag, n * sz - off) // sz
+        i0 = off // sz
+        want[i0:i0 + cnt] = O.reduce("sum", dt, peers[p][i0:i0 + cnt], want[i0:i0 + cnt])
+    launches = {}
+    for phase in range(0, 16, sz):
+        ctx = xucg_amd.DevContext(device=0, stage_bytes=16 << 10, stage_slots=4)
+        try:
+            buf = ctx.alloc(n * sz + 64)
+            buf.upload(acc, phase)
+            assert ctx.stage_begin(buf.ptr + phase, n * sz) == 0, _lib.last_error()
+            for p, off in order:
+                cnt = min(frag, n * sz - off) // sz
+                i0 = off // sz
+                piece = np.ascontiguousarray(peers[p][i0:i0 + cnt])
+                assert ctx.combine("sum", dt, off, piece, cnt) == 0, _lib.last_error()
+            assert ctx.stage_end() == 0, _lib.last_error()
+            got = buf.download(st, n, phase)
+            assert (bits(got) == bits(want)).all(), (dt, phase)
+            launches[phase] = ctx.counters()["launches"]
+            buf.free()
+        finally:
+            ctx.close()
+    assert max(launches.values()) <= min(launches.values()) + 2, launches

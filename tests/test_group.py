@@ -70,6 +70,7 @@ def test_bench_collective_phases_world1():
     line = json.loads(p.stdout.strip().splitlines()[-1])
     coll = line["collective"]
     assert coll, line
+    assert isinstance(coll.pop("wall_s"), float), coll
     for name, res in coll.items():
         assert isinstance(res, dict) and "error" not in res, (name, res)
     c4 = coll["c4_oneshot_xgmi_rs_4gib_fp32"]

@@ -297,8 +297,8 @@ ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
                                         void *reduce_op, void *src, void *dst,
                                         int dcount, void *datatype)
 {
-    ucg_dev_op_t op;
-    ucg_dev_dtype_t dt;
+    ucg_dev_op_t op    = UCG_DEV_OP_SUM;
+    ucg_dev_dtype_t dt = UCG_DEV_DT_LAST;   /* set by a successful classify */
     ucs_status_t st;
     size_t bytes;
 
@@ -317,8 +317,8 @@ ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
             pthread_mutex_unlock(&cmb->lock);
             return UCS_ERR_UNSUPPORTED;
         }
-        if (use_device(cmb, cls, on_dev,
-                       bytes = (size_t)dcount * ucg_builtin_dev_dtype_size(dt))) {
+        bytes = cls ? (size_t)dcount * ucg_builtin_dev_dtype_size(dt) : 0;
+        if (use_device(cmb, cls, on_dev, bytes)) {
             st = ucg_builtin_dev_combine_host(cmb->dev, op, dt, dst, src,
                                               (size_t)dcount);
             if (st == UCS_OK) {

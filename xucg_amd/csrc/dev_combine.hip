@@ -161,6 +161,8 @@ struct ucg_builtin_dev_ctx {
         bool     active;
         unsigned slot;
         size_t   used, off;
+        size_t   pad;      /* data starts at slot + pad, pad = (acc + off) mod 16,
+                            * so the run's src and dst share their 16-B phase */
         int      op, dt;
         uint64_t seq;
     }            runs[4];
@@ -744,8 +746,8 @@ static ucs_status_t run_flush(ucg_builtin_dev_ctx_t *ctx,
     }
     r.active = false;
     const size_t sz = kDtSize[r.dt];
-    char *ds = ctx->d_ring + (size_t)r.slot * ctx->slot_bytes;
-    HIP_TRY(hipMemcpyAsync(ds, ctx->h_ring + (size_t)r.slot * ctx->slot_bytes,
+    char *ds = ctx->d_ring + (size_t)r.slot * ctx->slot_bytes + r.pad;
+    HIP_TRY(hipMemcpyAsync(ds, ctx->h_ring + (size_t)r.slot * ctx->slot_bytes + r.pad,
                            r.used, hipMemcpyHostToDevice, ctx->stream));
     ucs_status_t st = reduce_on(ctx, ctx->stream, (ucg_dev_op_t)r.op,
                                 (ucg_dev_dtype_t)r.dt, ctx->acc + r.off, ds,
@@ -848,20 +850,22 @@ ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
         return set_error(UCS_ERR_OUT_OF_RANGE, "combine",
                          "fragment outside the staged step buffer");
     }
-    const char *src  = static_cast<const char*>(host_src);
-    const size_t cap = (ctx->slot_bytes / sz) * sz;
+    const char *src = static_cast<const char*>(host_src);
+    /* whole elements that fit in a slot after a run's pad */
+    auto cap = [&](size_t pad) { return ((ctx->slot_bytes - pad) / sz) * sz; };
     while (bytes > 0) {
         ucg_builtin_dev_ctx::Run *run = nullptr;
         for (auto &r : ctx->runs) {
             if (r.active && r.op == (int)op && r.dt == (int)dt &&
-                r.off + r.used == dst_offset && r.used < cap) {
+                r.off + r.used == dst_offset && r.used < cap(r.pad)) {
                 run = &r;
                 break;
             }
         }
+        const size_t new_pad = ((uintptr_t)ctx->acc + dst_offset) & 15;
         const size_t lo = dst_offset;
-        const size_t hi = dst_offset + (run ? std::min(bytes, cap - run->used) :
-                                              std::min(bytes, cap));
+        const size_t hi = dst_offset + (run ? std::min(bytes, cap(run->pad) - run->used) :
+                                              std::min(bytes, cap(new_pad)));
         /* growing a run over a range that a LATER run already holds would
          * flush this contribution before an earlier-arrived one; a brand-new
          * run is always flushed last, so it never clashes */
@@ -896,21 +900,22 @@ ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
             run->slot   = k;
             run->used   = 0;
             run->off    = dst_offset;
+            run->pad    = new_pad;
             run->op     = op;
             run->dt     = dt;
             run->seq    = ctx->run_seq++;
         }
-        const size_t room = cap - run->used;
+        const size_t room = cap(run->pad) - run->used;
         const size_t n    = bytes < room ? bytes : room;
         /* src is borrowed (released right after the callback returns,
          * builtin/ops/builtin_comp_step.inl:443-449): copy it now */
-        memcpy(ctx->h_ring + (size_t)run->slot * ctx->slot_bytes + run->used,
+        memcpy(ctx->h_ring + (size_t)run->slot * ctx->slot_bytes + run->pad + run->used,
                src, n);
         run->used  += n;
         src        += n;
         dst_offset += n;
         bytes      -= n;
-        if (run->used == cap) {
+        if (run->used == cap(run->pad)) {
             /* a full run can only be flushed if nothing older is pending */
             bool older = false;
             for (auto &r : ctx->runs) {

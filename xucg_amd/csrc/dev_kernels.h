@@ -6,7 +6,10 @@
  *                   sized to the data; the unaligned head and the ragged
  *                   tail (< 16 B each) are done by the first lanes of the
  *                   grid with lane-masked scalar accesses.
- *   k_reduce_scalar same contract when src and dst disagree mod 16 B.
+ *   k_reduce_shift  same contract when src and dst disagree mod 16 B:
+ *                   aligned src loads realigned by a wavefront shuffle.
+ *   k_reduce_scalar element-wise fallback for operands that are not even
+ *                   element-aligned.
  *   k_reduce_multi  one-shot N-operand combine in the recursive-doubling
  *                   association (builtin/plan/builtin_recursive.c:158-169).
  *   k_fill          counter-based synthetic generator.
@@ -114,6 +117,105 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
         const size_t i = base + (size_t)u * BS;
         if (i < nvec) {
             st16<NT>(d4 + i, vapply<T, OP>(a[u], b[u]));
+        }
+    }
+}
+
+/*
+ * The streaming combine when src and dst disagree mod 16 B (a fragment landing
+ * at an arbitrary remote_offset, a peer's buffer at another offset). After the
+ * head, dst is 16-B aligned and src sits r = 4Q + rb bytes past a 16-B
+ * boundary A. Lane L loads the aligned src vector A[i] (i = its dst vector);
+ * the vector after it, A[i+1], is lane L+1's load, fetched with a wavefront
+ * shuffle (ds_bpermute), and lane 63 loads it itself. The src bytes under
+ * dst vector i are then funnel-shifted out of the 32-B pair (v_alignbyte).
+ * Every src vector is loaded once (lane 63's extra load aside), so the HBM
+ * traffic is the aligned kernel's. The aligned vectors A[0] and A[nvec] each
+ * hold bytes of the operand, so they lie in its pages even where they reach
+ * past its ends.
+ */
+/* lane L gets lane L+1's value (lane 63: undefined, overwritten by the
+ * caller). DPP=1: one v_mov_dpp wave_shl:1 (GFX9 whole-wave DPP, kept on
+ * CDNA); DPP=0: ds_bpermute through the LDS crossbar. */
+template <int DPP>
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t x)
+{
+    if (DPP) {
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
+    }
+    return __shfl_down(x, 1, 64);
+}
+
+template <typename T, int OP, int Q, int U = 1, int DPP = 0>
+__global__ void __launch_bounds__(kReduceBlock)
+k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
+               unsigned rb)
+{
+    constexpr int V   = 16 / sizeof(T);
+    constexpr int BS  = kReduceBlock;
+    const size_t gtid = (size_t)blockIdx.x * BS + threadIdx.x;
+
+    if (gtid < head) {
+        dst[gtid] = Comb<T, OP>::apply(src[gtid], dst[gtid]);
+    }
+    if (gtid < tail) {
+        const size_t j = head + nvec * V + gtid;
+        dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
+    }
+    if (nvec == 0) {
+        return;
+    }
+
+    const char *sp  = reinterpret_cast<const char*>(src + head);
+    const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
+    /* the wave's tile: U rows of 64 vectors; lane L holds column L */
+    const size_t base    = (size_t)blockIdx.x * (BS * U) + threadIdx.x;
+    const bool last_lane = threadIdx.x == BS - 1;
+    u32x4 lo[U], b[U], ex;
+    /* every load in flight before the first wait; lanes past the end load
+     * the last vector again (unmasked loads keep the compiler from
+     * serialising them) and store nothing */
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * BS;
+        b[u]  = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
+        lo[u] = ld16<1>(a4 + (i < nvec ? i : nvec));
+    }
+    {
+        const size_t i = base + (size_t)(U - 1) * BS + 1;
+        ex = ld16<1>(a4 + (last_lane && i <= nvec ? i : nvec));
+    }
+    __builtin_amdgcn_sched_barrier(0);  /* keep the shuffles behind all loads */
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * BS;
+        /* A[i + 1]: the next lane's load; for lane 63 the first lane's load
+         * of the next row, or its own extra load after the last row */
+        u32x4 hi;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hi[k] = from_next_lane<DPP>(lo[u][k]);
+        }
+        if (last_lane) {
+            if (u + 1 < U) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    hi[k] = __builtin_amdgcn_readlane(lo[u + 1 < U ? u + 1 : u][k], 0);
+                }
+            } else {
+                hi = ex;
+            }
+        }
+        if (i < nvec) {
+            const uint32_t w[8] = {lo[u][0], lo[u][1], lo[u][2], lo[u][3],
+                                   hi[0], hi[1], hi[2], hi[3]};
+            u32x4 sv;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
+            }
+            st16<1>(d4 + i, vapply<T, OP>(sv, b[u]));
         }
     }
 }

@@ -65,6 +65,36 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
     } while (done < nvec);
 }
 
+/* k_reduce_shift, chunked like launch_vec. Q = (src - dst) mod 16 B in
+ * whole words, rb the remaining bytes; pairs a dtype cannot produce (rb != 0
+ * for 4-B elements, anything but Q = 2 for 8-B ones) are not instantiated. */
+template <typename T, int OP, int Q, int U = 1, int DPP = 0>
+void launch_shift(T *d, const T *s, size_t head, size_t nvec, size_t tail,
+                  unsigned rb, hipStream_t st)
+{
+    constexpr size_t V = 16 / sizeof(T);
+    if constexpr ((sizeof(T) == 8 && Q != 2) || (sizeof(T) == 4 && Q == 0)) {
+        (void)d; (void)s; (void)head; (void)nvec; (void)tail; (void)rb; (void)st;
+        return;
+    } else {
+        size_t done = 0;
+        do {
+            const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done
+                                                                : kMaxVecPerLaunch;
+            const bool first = (done == 0), last = (done + chunk == nvec);
+            const size_t off = first ? 0 : head + done * V;
+            size_t items = chunk;
+            if (first && head > items) items = head;
+            if (last && tail > items) items = tail;
+            const unsigned grid = grid_for(items, (size_t)kReduceBlock * U, 0x7fffffff);
+            hipLaunchKernelGGL((k_reduce_shift<T, OP, Q, U, DPP>), dim3(grid), dim3(kReduceBlock),
+                               0, st, d + off, s + off, first ? head : 0, chunk,
+                               last ? tail : 0, rb);
+            done += chunk;
+        } while (done < nvec);
+    }
+}
+
 template <int DT, int OP>
 hipError_t launch_reduce(void *dst, const void *src, size_t count,
                                 hipStream_t st, int variant)
@@ -76,8 +106,8 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
     const T *s = static_cast<const T*>(src);
     const uintptr_t md = (uintptr_t)dst & 15, ms = (uintptr_t)src & 15;
 
-    if (md != ms) {
-        /* operands disagree mod 16 B: no common vector alignment */
+    if (md != ms && ((md | ms) % sz != 0 || variant == 4)) {
+        /* not even element-aligned (or the A/B variant 4): element loop */
         const unsigned grid = grid_for(count, (size_t)kBlock * 4,
                                        launch_max_blocks());
         hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(grid), dim3(kBlock),
@@ -90,6 +120,28 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
     }
     const size_t rem  = count - head;
     const size_t nvec = rem / V, tail = rem % V;
+
+    if (md != ms) {
+        /* operands disagree mod 16 B: src realigned in registers */
+        const unsigned r = (unsigned)((ms + 16 - md) & 15);
+        if constexpr (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM) {
+            if (variant >= 5 && variant <= 7 && r == 4) {
+                /* A/B: U = 2 or 4 vectors per lane (one extra load per 64 U),
+                 * or the DPP lane shift instead of ds_bpermute */
+                if (variant == 5)      launch_shift<T, OP, 1, 2>(d, s, head, nvec, tail, 0, st);
+                else if (variant == 6) launch_shift<T, OP, 1, 4>(d, s, head, nvec, tail, 0, st);
+                else                   launch_shift<T, OP, 1, 1, 1>(d, s, head, nvec, tail, 0, st);
+                return hipGetLastError();
+            }
+        }
+        switch (r >> 2) {
+        case 0:  launch_shift<T, OP, 0>(d, s, head, nvec, tail, r & 3, st); break;
+        case 1:  launch_shift<T, OP, 1>(d, s, head, nvec, tail, r & 3, st); break;
+        case 2:  launch_shift<T, OP, 2>(d, s, head, nvec, tail, r & 3, st); break;
+        default: launch_shift<T, OP, 3>(d, s, head, nvec, tail, r & 3, st); break;
+        }
+        return hipGetLastError();
+    }
 
     if (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM && variant >= 0) {
         /* tuning variants of the headline kernel (UCX_BUILTIN_DEV_VARIANT) */
