@@ -76,6 +76,18 @@ def cpu_baseline(count, budget_s=10.0):
     except OSError:
         pass
     b = 3 * count * 4
+    # the combine the reference itself calls: reduce_cb_f = the MPI library's
+    # MPI_Reduce_local (MPICH 3.3.2 in this image), same count, 1 thread
+    mpich = None
+    exe = os.path.join(ROOT, "oracle", "_build", "mpich_bench")
+    if os.path.exists(exe):
+        import subprocess
+        try:
+            p = subprocess.run([exe, str(count), "6", "8192"], capture_output=True, text=True,
+                               timeout=60)
+            mpich = json.loads(p.stdout.strip().splitlines()[-1])
+        except Exception as e:  # reported, never fatal for the bench line
+            mpich = {"error": f"{type(e).__name__}: {e}"[:300]}
     return {
         "value": round(b / med / GIB, 3),
         "unit": "GiB/s",
@@ -89,6 +101,7 @@ def cpu_baseline(count, budget_s=10.0):
         f"threads_{threads}_gibs": round(b / med_mt / GIB, 3),
         "cpu_model": cpu_model,
         "online_cpus": os.cpu_count(),
+        "reference_callback_mpich": mpich,
     }
 
 

@@ -127,3 +127,21 @@ def test_fragmented_equals_whole_for_elementwise():
     a = O.reduce("sum", "float64", s, d)
     b = O.reduce("sum", "float64", s, d, frag_bytes=O.frag_length(256, 8))
     assert (a.view(np.uint64) == b.view(np.uint64)).all()
+
+
+def test_mpich_callback_bench_agrees_with_oracle():
+    """oracle/_build/mpich_bench times MPI_Reduce_local - the combine the
+    reference calls through reduce_cb_f - for bench.py's CPU baseline; its
+    whole-buffer result must equal the oracle's bit for bit (it exits 3
+    otherwise). Skipped where MPICH is absent."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "oracle", "_build", "mpich_bench")
+    if not os.path.exists(exe):
+        pytest.skip("MPICH not present: mpich_bench not built")
+    p = subprocess.run([exe, str(100_003), "0.2", "256"], capture_output=True, text=True,
+                       timeout=60)
+    assert p.returncode == 0, p.stdout + p.stderr
+    res = json.loads(p.stdout.strip().splitlines()[-1])
+    assert res["bit_exact_vs_oracle"] is True and res["fragment_bytes"] == 248
