@@ -277,6 +277,33 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             dist.reduce_scatter_tensor(rs_out, x)
             torch.cuda.synchronize()
             same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
+            # north_star's 8-GPU target is stated on the 1 GiB buffer of the
+            # single-GPU target: the first 1 GiB of x, same peers, both ways
+            n1 = 1 << 28
+            lo1, hi1 = G.shard_bounds(n1, 4, world, rank)
+            mine1 = torch.empty(hi1 - lo1, dtype=torch.float32, device=dev)
+            rccl1 = torch.empty(n1 // world, dtype=torch.float32, device=dev)
+            x1 = x.narrow(0, 0, n1)
+
+            def rs1():
+                G.oneshot_reduce_scatter(ctx, peers, mine1.data_ptr(), n1, "float32", "sum",
+                                         rank, world)
+                torch.cuda.synchronize()
+                dist.barrier()
+            for _ in range(warmup):
+                rs1()
+                dist.reduce_scatter_tensor(rccl1, x1)
+            t_rs1 = timed(rs1, steps)
+            t_rccl1 = timed(lambda: dist.reduce_scatter_tensor(rccl1, x1), steps)
+            same1 = bool(torch.equal(mine1.view(torch.int32), rccl1.view(torch.int32)))
+            bus1 = (world - 1) / world * n1 * 4
+            rs_1gib = {"bytes": n1 * 4, "oneshot_rs_ms": round(t_rs1 * 1e3, 3),
+                       "oneshot_rs_busbw_gbs": round(bus1 / t_rs1 / 1e9, 1),
+                       "oneshot_rs_frac_of_xgmi": round(bus1 / t_rs1 / 1e9 / XGMI_GBS, 4),
+                       "rccl_rs_ms": round(t_rccl1 * 1e3, 3),
+                       "rccl_rs_busbw_gbs": round(bus1 / t_rccl1 / 1e9, 1),
+                       "oneshot_bit_exact_vs_rccl_on_exact_inputs": same1}
+            del mine1, rccl1, x1
             t_ag = timed(lambda: dist.all_gather_into_tensor(ag_out, mine), steps)
             # one-shot all-gather: every rank reads the N reduced shards in
             # place over xGMI (ucg_builtin_dev_gather_multi); parity: bit-exact
@@ -388,6 +415,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "push_allreduce_busbw_gbs": round(2 * bus / t_par / 1e9, 1),
                 "push_allreduce_bit_exact_vs_rccl_rs_ag": par_same,
                 "bit_exact_vs_rccl_on_exact_inputs": same,
+                "rs_1gib": rs_1gib,
                 "rccl_within_8c_tolerance_on_rounded_inputs": within,
                 "max_err_over_tolerance": round(ratio, 4),
                 "max_ulps_vs_rccl_on_rounded_inputs": ulps,
@@ -661,8 +689,14 @@ def main():
     value = world * args.steps * bytes_per_step / elapsed / GIB
 
     # roofline of the combine kernel: HIP events on the context's own stream
+    # (right after the timed steps, so the clocks are up): average launch
+    # duration of each of 5 batches of 50 back-to-back launches, median batch;
+    # the spread is reported because HBM runs in slower phases of seconds on
+    # some boxes ("Slow phases")
     iters = 50
-    avg_us = ctx.profile_reduce("sum", "float32", dst, src, n, iters)
+    batch_us = sorted(ctx.profile_reduce("sum", "float32", dst, src, n, iters)
+                      for _ in range(5))
+    avg_us = batch_us[len(batch_us) // 2]
     achieved = bytes_per_step / (avg_us * 1e-6) / 1e9
     # SURVEY.md 8d also asks for the median of individually timed launches
     singles = sorted(ctx.profile_reduce("sum", "float32", dst, src, n, 1) for _ in range(21))
@@ -751,6 +785,7 @@ def main():
                 "traffic": pmc_traffic(n),
                 "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64>",
                 "kernel_avg_us": round(avg_us, 3),
+                "kernel_avg_us_batches": [round(b, 2) for b in batch_us],
                 "kernel_median_us_single_launches": round(median_us, 3),
                 "frac_from_median": round(bytes_per_step / (median_us * 1e-6) / 1e9
                                           / HBM_PEAK_GBS, 4),

@@ -80,6 +80,7 @@ def test_bench_collective_phases_world1():
     assert c4["oneshot_allreduce_bit_exact_vs_rccl_rs_ag"] is True, c4
     assert c4["push_rs_bit_exact_vs_rccl"] is True, c4
     assert c4["push_allreduce_bit_exact_vs_rccl_rs_ag"] is True, c4
+    assert c4["rs_1gib"]["oneshot_bit_exact_vs_rccl_on_exact_inputs"] is True, c4
     c5 = coll["c5_recursive_allreduce_512mib_fp64"]
     assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
     assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5

@@ -50,8 +50,118 @@ static float time_pair(float *d, const float *s, size_t n, hipStream_t st)
     return ms[ms.size() / 2];
 }
 
+/* VMM allocation: one physical chunk of `bytes` (rounded to the minimum
+ * granularity) mapped into a fresh VA range */
+static void *vmm_alloc(size_t bytes, size_t *mapped)
+{
+    hipMemAllocationProp prop = {};
+    prop.type          = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id   = 0;
+    size_t gran = 0;
+    CHECK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended));
+    const size_t sz = (bytes + gran - 1) / gran * gran;
+    hipMemGenericAllocationHandle_t h;
+    CHECK(hipMemCreate(&h, sz, &prop, 0));
+    void *va = nullptr;
+    CHECK(hipMemAddressReserve(&va, sz, 0, nullptr, 0));
+    CHECK(hipMemMap(va, sz, 0, h, 0));
+    hipMemAccessDesc acc = {};
+    acc.location = prop.location;
+    acc.flags    = hipMemAccessFlagsProtReadWrite;
+    CHECK(hipMemSetAccess(va, sz, &acc, 1));
+    CHECK(hipMemRelease(h));      /* the mapping keeps it alive */
+    *mapped = sz;
+    return va;
+}
+
+static void vmm_free(void *va, size_t sz)
+{
+    CHECK(hipMemUnmap(va, sz));
+    CHECK(hipMemAddressFree(va, sz));
+}
+
+/* scenario mode (argv[1] = "scen"): the same 256 MiB pair shape allocated
+ * after different histories of the device heap, interleaved over trials */
+static int scenarios(int trials)
+{
+    hipStream_t st;
+    CHECK(hipStreamCreate(&st));
+    const size_t n = (size_t)1 << 26, nb = n * 4;
+    for (int t = 0; t < trials; t++) {
+        float *s, *d;
+        /* S1: fresh hipMalloc */
+        CHECK(hipMalloc(&s, nb));
+        CHECK(hipMalloc(&d, nb));
+        CHECK(hipMemset(s, 0, nb));
+        CHECK(hipMemset(d, 0, nb));
+        printf("trial %d S1 fresh hipMalloc          %5.1f%%\n", t,
+               100.0 * 3 * nb / (time_pair(d, s, n, st) * 1e-3) / 8e12);
+        CHECK(hipFree(s));
+        CHECK(hipFree(d));
+        /* S2: after a freed 1 GiB pair */
+        {
+            float *a, *b;
+            CHECK(hipMalloc(&a, nb * 4));
+            CHECK(hipMalloc(&b, nb * 4));
+            CHECK(hipMemset(a, 0, nb * 4));
+            CHECK(hipMemset(b, 0, nb * 4));
+            CHECK(hipFree(a));
+            CHECK(hipFree(b));
+        }
+        CHECK(hipMalloc(&s, nb));
+        CHECK(hipMalloc(&d, nb));
+        CHECK(hipMemset(s, 0, nb));
+        CHECK(hipMemset(d, 0, nb));
+        printf("trial %d S2 after freed 1 GiB pair   %5.1f%%\n", t,
+               100.0 * 3 * nb / (time_pair(d, s, n, st) * 1e-3) / 8e12);
+        CHECK(hipFree(s));
+        CHECK(hipFree(d));
+        /* S3: a heap with holes: 96 x 8 MiB, every other one freed */
+        {
+            std::vector<void*> v(96);
+            for (auto &p : v) CHECK(hipMalloc(&p, 8u << 20));
+            for (size_t i = 0; i < v.size(); i += 2) CHECK(hipFree(v[i]));
+            CHECK(hipMalloc(&s, nb));
+            CHECK(hipMalloc(&d, nb));
+            CHECK(hipMemset(s, 0, nb));
+            CHECK(hipMemset(d, 0, nb));
+            printf("trial %d S3 heap with 8 MiB holes    %5.1f%%\n", t,
+                   100.0 * 3 * nb / (time_pair(d, s, n, st) * 1e-3) / 8e12);
+            CHECK(hipFree(s));
+            CHECK(hipFree(d));
+            for (size_t i = 1; i < v.size(); i += 2) CHECK(hipFree(v[i]));
+        }
+        /* S4: VMM physical chunks */
+        {
+            size_t ms_, md_;
+            s = (float*)vmm_alloc(nb, &ms_);
+            d = (float*)vmm_alloc(nb, &md_);
+            CHECK(hipMemset(s, 0, nb));
+            CHECK(hipMemset(d, 0, nb));
+            printf("trial %d S4 VMM hipMemCreate/Map     %5.1f%%\n", t,
+                   100.0 * 3 * nb / (time_pair(d, s, n, st) * 1e-3) / 8e12);
+            vmm_free(s, ms_);
+            vmm_free(d, md_);
+        }
+        /* S5: contiguous flag */
+        CHECK(hipExtMallocWithFlags((void**)&s, nb, hipDeviceMallocContiguous));
+        CHECK(hipExtMallocWithFlags((void**)&d, nb, hipDeviceMallocContiguous));
+        CHECK(hipMemset(s, 0, nb));
+        CHECK(hipMemset(d, 0, nb));
+        printf("trial %d S5 hipDeviceMallocContiguous %5.1f%%\n", t,
+               100.0 * 3 * nb / (time_pair(d, s, n, st) * 1e-3) / 8e12);
+        CHECK(hipFree(s));
+        CHECK(hipFree(d));
+    }
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc > 1 && argv[1][0] == 's') {
+        return scenarios(argc > 2 ? atoi(argv[2]) : 4);
+    }
     const int trials = argc > 1 ? atoi(argv[1]) : 4;
     hipStream_t st;
     CHECK(hipStreamCreate(&st));

@@ -126,6 +126,40 @@ k_oneshot3(float *dst, const float *src, size_t nvec)
     }
 }
 
+/* variant X: the product geometry (one wave, one vector per lane) with the
+ * workgroup -> tile map made XCD-aware. The dispatcher deals workgroup b to
+ * XCD b % 8; here XCD x takes chunks of C consecutive tiles (C = 0: one
+ * contiguous eighth of the buffer), so each XCD's UTCL2 and L2 see 1/8 of
+ * the pages instead of all of them. Tests the TLB-reach hypothesis for the
+ * 1 GiB operands (2 GiB working set). */
+template <int C>
+__global__ void __launch_bounds__(64)
+k_xcd(float *dst, const float *src, size_t nvec, unsigned ntiles)
+{
+    const unsigned b = blockIdx.x;
+    const unsigned x = b & 7, j = b >> 3;
+    const unsigned full = ntiles & ~7u;           /* tiles in whole rounds of 8 */
+    const unsigned T = full >> 3;                 /* tiles per XCD */
+    unsigned tile;
+    if (b >= full) {
+        tile = b;                                 /* ragged last round: identity */
+    } else if (C == 0) {
+        tile = x * T + j;
+    } else {
+        const unsigned R = T / C, r = T % C;      /* whole chunk rows, remainder */
+        tile = (j < R * C) ? (j / C) * (8u * C) + x * C + (j % C)
+                           : R * 8u * C + x * r + (j - R * C);
+    }
+    const size_t i = (size_t)tile * 64 + threadIdx.x;
+    if (i < nvec) {
+        const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+        u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+        u32x4 a = ld16<1>(s4 + i);
+        u32x4 v = ld16<1>(d4 + i);
+        st16<1>(d4 + i, vapply<float, 0>(a, v));
+    }
+}
+
 /* variant H: one-wave workgroups on a capped grid, each looping over tiles
  * (fewer workgroups for the dispatcher to launch); PIPE = 1 loads the next
  * tile before storing the current one */
@@ -316,6 +350,24 @@ int main(int argc, char **argv)
         unsigned g = (unsigned)((nv + 1023) / 1024);
         hipLaunchKernelGGL((k_reduce<float, 0, 4, 1, 256>), dim3(g), dim3(256), 0, q, d, s, (size_t)0, nv, (size_t)0);
     }, {}});
+    auto xcd = [&](int C) {
+        char buf[128];
+        snprintf(buf, sizeof(buf), "xcd-aware bs64 U1 chunk%d", C);
+        vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)((nv + 63) / 64);
+#define XC(A) if (C == A) hipLaunchKernelGGL((k_xcd<A>), dim3(g), dim3(64), 0, q, d, s, nv, g)
+            XC(0); XC(32); XC(256); XC(2048);
+#undef XC
+        }, {}});
+    };
+    if (getenv("TUNE_XCD_ONLY")) {
+        xcd(0);
+        xcd(32);
+        xcd(256);
+        xcd(2048);
+        goto run;
+    }
+    {
     auto grid_stride = [&](int U, int NT, int maxb) {
         char buf[128];
         snprintf(buf, sizeof(buf), "gridstride U%d NT%d blocks%d", U, NT, maxb);
@@ -389,7 +441,10 @@ int main(int argc, char **argv)
         osb(2, 18, 2, 64);
         osb(1, 18, 18, 64);
     }
-
+    }
+    xcd(0);
+    xcd(2048);
+run:
     /* init */
     hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, st,
                        (void*)src, 0, 1ull, n);
