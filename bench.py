@@ -150,6 +150,10 @@ def c1_loopback(ranks=4, iters=20000):
 
 
 XGMI_GBS = 7 * 153.0   # aggregate xGMI per MI355X
+# AMD's 153.6 GB/s per link counts both directions (as MI300X's 128 GB/s
+# does); a reduce-scatter's ingress into one GPU uses one direction of each
+# link, so its link roofline is 7 x 76.8 GB/s
+XGMI_DIR_GBS = 7 * 76.8
 
 
 def max_ulps(a, b):
@@ -257,7 +261,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "ag_ms": round(t_ag * 1e3, 3),
                 "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
                 "ag_busbw_gbs": round(bus / t_ag / 1e9, 1),
-                "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4)}
+                "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4),
+                "rs_frac_of_xgmi_per_direction": round(bus / t_rs / 1e9 / XGMI_DIR_GBS, 4)}
     agreed(rccl, "c4_rccl_rs_ag_4gib_fp32")
 
     def oneshot():
@@ -300,6 +305,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             rs_1gib = {"bytes": n1 * 4, "oneshot_rs_ms": round(t_rs1 * 1e3, 3),
                        "oneshot_rs_busbw_gbs": round(bus1 / t_rs1 / 1e9, 1),
                        "oneshot_rs_frac_of_xgmi": round(bus1 / t_rs1 / 1e9 / XGMI_GBS, 4),
+                       "oneshot_rs_frac_of_xgmi_per_direction":
+                           round(bus1 / t_rs1 / 1e9 / XGMI_DIR_GBS, 4),
                        "rccl_rs_ms": round(t_rccl1 * 1e3, 3),
                        "rccl_rs_busbw_gbs": round(bus1 / t_rccl1 / 1e9, 1),
                        "oneshot_bit_exact_vs_rccl_on_exact_inputs": same1}
@@ -398,6 +405,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         return {"bytes": s_bytes, "rs_ms": round(t_rs * 1e3, 3),
                 "rs_busbw_gbs": round(bus / t_rs / 1e9, 1),
                 "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4),
+                "rs_frac_of_xgmi_per_direction": round(bus / t_rs / 1e9 / XGMI_DIR_GBS, 4),
                 "rs_ag_ms": round((t_rs + t_ag) * 1e3, 3),
                 "oneshot_ag_ms": round(t_ag1 * 1e3, 3),
                 "oneshot_ag_busbw_gbs": round(bus / t_ag1 / 1e9, 1),
@@ -406,10 +414,13 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "oneshot_allreduce_ms": round(t_ar1 * 1e3, 3),
                 "oneshot_allreduce_busbw_gbs": round(2 * bus / t_ar1 / 1e9, 1),
                 "oneshot_allreduce_frac_of_xgmi": round(2 * bus / t_ar1 / 1e9 / XGMI_GBS, 4),
+                "oneshot_allreduce_frac_of_xgmi_per_direction":
+                    round(2 * bus / t_ar1 / 1e9 / XGMI_DIR_GBS, 4),
                 "oneshot_allreduce_bit_exact_vs_rccl_rs_ag": ar_same,
                 "push_rs_ms": round(t_prs * 1e3, 3),
                 "push_rs_busbw_gbs": round(bus / t_prs / 1e9, 1),
                 "push_rs_frac_of_xgmi": round(bus / t_prs / 1e9 / XGMI_GBS, 4),
+                "push_rs_frac_of_xgmi_per_direction": round(bus / t_prs / 1e9 / XGMI_DIR_GBS, 4),
                 "push_rs_bit_exact_vs_rccl": prs_same,
                 "push_allreduce_ms": round(t_par * 1e3, 3),
                 "push_allreduce_busbw_gbs": round(2 * bus / t_par / 1e9, 1),
