@@ -45,6 +45,35 @@ def main():
                "us": round(us, 2), "gbs": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
         print(row, flush=True)
         rows.append(row)
+    # the one-shot multi-operand kernel, 8 operands of 64 MiB: all in phase
+    # with dst, one operand 4 B out, every operand at its own phase
+    n8 = (64 << 20) // 4
+    bufs = [ctx.alloc(n8 * 4 + 64) for _ in range(8)]
+    out8 = ctx.alloc(n8 * 4 + 64)
+    for k, b in enumerate(bufs):
+        ctx.fill("float32", "exact", 100 + k, b, n8 + 16)
+    for name, offs in (("aligned", [0] * 8), ("one_operand_4B", [4] + [0] * 7),
+                       ("all_phases", [0, 4, 8, 12, 4, 8, 12, 0])):
+        srcs = [b.ptr + o for b, o in zip(bufs, offs)]
+        ctx.reduce_multi("sum", "float32", out8.ptr, srcs, 0, n8)
+        ctx.sync()
+        import time
+        reps = 20
+        t = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.reduce_multi("sum", "float32", out8.ptr, srcs, 0, n8)
+            ctx.sync()
+            t.append((time.perf_counter() - t0) / reps * 1e6)
+        us = sorted(t)[2]
+        gbs = 9 * n8 * 4 / (us * 1e-6) / 1e9
+        row = {"kernel": "reduce_multi", "nsrc": 8, "case": name, "variant": variant,
+               "us": round(us, 2), "gbs": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
+        print(row, flush=True)
+        rows.append(row)
+    for b in bufs + [out8]:
+        b.free()
     # spot parity on a small misaligned case vs a host restatement of fp32 sum
     m = 100_003
     a = np.random.default_rng(5).standard_normal(m).astype(np.float32)

@@ -96,6 +96,11 @@ int launch_max_blocks()
 {
     return launch_cfg().max_blocks;
 }
+
+int launch_variant()
+{
+    return launch_cfg().variant;
+}
 }  // namespace ucgdev
 
 /* dispatch tables, assembled from the per-dtype translation units */

@@ -312,6 +312,104 @@ k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
     }
 }
 
+/* bytes [r, r + 16) of the 32-B pair (lo, hi); r uniform, 0..15 */
+__device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, unsigned r)
+{
+    const unsigned rb = r & 3;
+    uint32_t w[5];
+    switch (r >> 2) {
+    case 0:  w[0] = lo[0]; w[1] = lo[1]; w[2] = lo[2]; w[3] = lo[3]; w[4] = hi[0]; break;
+    case 1:  w[0] = lo[1]; w[1] = lo[2]; w[2] = lo[3]; w[3] = hi[0]; w[4] = hi[1]; break;
+    case 2:  w[0] = lo[2]; w[1] = lo[3]; w[2] = hi[0]; w[3] = hi[1]; w[4] = hi[2]; break;
+    default: w[0] = lo[3]; w[1] = hi[0]; w[2] = hi[1]; w[3] = hi[2]; w[4] = hi[3]; break;
+    }
+    u32x4 o;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        o[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], rb);
+    }
+    return o;
+}
+
+/*
+ * k_reduce_multi when some operand disagrees with dst mod 16 B (a peer's
+ * buffer at another offset). Every operand is read in aligned 16-B vectors
+ * and realigned as in k_reduce_shift, each with its own phase (computed from
+ * its pointer: uniform per operand); an operand in phase with dst takes the
+ * plain path. All loads are issued before the first shuffle. Same
+ * association as k_reduce_multi, so the same bits.
+ */
+template <typename T, int OP, int N>
+__global__ void __launch_bounds__(kReduceBlock)
+k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
+                     size_t tail)
+{
+    constexpr int V    = 16 / sizeof(T);
+    const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+    auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<T, OP>(a, b); };
+
+    if (gtid < head || gtid < tail) {
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            size_t j;
+            if (part == 0) {
+                if (gtid >= head) continue;
+                j = gtid;
+            } else {
+                if (gtid >= tail) continue;
+                j = head + nvec * V + gtid;
+            }
+            T val[N];
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                val[m] = static_cast<const T*>(srcs.p[self ^ m])[j];
+            }
+            dst[j] = rd_tree<N>(val, fs);
+        }
+    }
+    if (nvec == 0) {
+        return;
+    }
+
+    u32x4 *d4            = reinterpret_cast<u32x4*>(dst + head);
+    const size_t i       = gtid;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    const u32x4 *a4[N];
+    unsigned r[N];
+    u32x4 val[N], ex[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        const char *p = reinterpret_cast<const char*>(
+            static_cast<const T*>(srcs.p[self ^ m]) + head);
+        r[m]  = (unsigned)((uintptr_t)p & 15);
+        a4[m] = reinterpret_cast<const u32x4*>(p - r[m]);
+        /* clamped, unmasked loads with no branch between them (see
+         * k_reduce_shift); an out-of-phase operand also needs A[nvec] */
+        const size_t lim = nvec - (r[m] == 0);
+        val[m] = ld16<1>(a4[m] + (i < lim ? i : lim));
+        ex[m]  = ld16<1>(a4[m] + (last_lane && i < lim ? i + 1 : lim));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        if (r[m]) {
+            u32x4 hi;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                hi[k] = from_next_lane<0>(val[m][k]);
+            }
+            if (last_lane) {
+                hi = ex[m];
+            }
+            val[m] = funnel16(val[m], hi, r[m]);
+        }
+    }
+    if (i < nvec) {
+        st16<1>(d4 + i, rd_tree<N>(val, fv));
+    }
+}
+
 template <typename T, int OP, int N>
 __global__ void __launch_bounds__(kBlock)
 k_reduce_multi_scalar(T *dst, SrcList srcs, unsigned self, size_t count)

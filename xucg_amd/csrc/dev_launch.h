@@ -20,6 +20,8 @@ namespace ucgdev {
 /* UCX_BUILTIN_DEV_MAX_BLOCKS: grid cap of the looping (scalar) kernels;
  * defined in dev_combine.hip */
 int launch_max_blocks();
+/* UCX_BUILTIN_DEV_VARIANT: A/B tuning knob (0 = product); defined likewise */
+int launch_variant();
 
 inline size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
 
@@ -192,7 +194,8 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
     }
     T *d = static_cast<T*>(dst);
-    if (!aligned) {
+    if (!aligned && launch_variant() == 4) {
+        /* A/B only: the element loop the realigning kernel replaced */
         const unsigned grid = grid_for(count, kBlock, launch_max_blocks());
         hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP, N>), dim3(grid),
                            dim3(kBlock), 0, st, d, srcs, self, count);
@@ -212,9 +215,21 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         for (int m = 0; m < kMaxMulti; m++) {
             sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
         }
-        const unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
-        hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
-                           st, d + off, sl, self, first ? head : 0, chunk, last ? tail : 0);
+        if (aligned) {
+            const unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
+            hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
+                               st, d + off, sl, self, first ? head : 0, chunk,
+                               last ? tail : 0);
+        } else {
+            /* some operand out of phase with dst: realigned in registers */
+            size_t items = chunk;
+            if (first && head > items) items = head;
+            if (last && tail > items) items = tail;
+            const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
+            hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N>), dim3(grid), dim3(kReduceBlock),
+                               0, st, d + off, sl, self, first ? head : 0, chunk,
+                               last ? tail : 0);
+        }
         done += chunk;
     } while (done < nvec);
     return hipGetLastError();
