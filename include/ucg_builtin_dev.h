@@ -183,8 +183,10 @@ ucs_status_t ucg_builtin_dev_reduce(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
 /* The all-gather half of a one-shot reduce-scatter + all-gather (SURVEY.md
  * 8e): dst[r * shard_bytes + i] = srcs[r][i] for r < nsrc, every source read in
  * one launch (srcs may be peer-mapped device pointers: member r's shard over
- * xGMI). A plain copy; no reference counterpart (the reference has no
- * all-gather of reduced shards). nsrc <= 16. */
+ * xGMI). A NULL source leaves its row of dst untouched (a member's own shard,
+ * already in place), so the other N-1 rows still go in one launch with every
+ * link streaming. A plain copy; no reference counterpart (the reference has
+ * no all-gather of reduced shards). nsrc <= 16, at least one source non-NULL. */
 ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                           const void *const *srcs, unsigned nsrc,
                                           size_t shard_bytes);

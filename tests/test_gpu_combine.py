@@ -323,7 +323,8 @@ def test_max_size_operands(dev_ctx, dt, count, multi):
                                                (16, 4099, 0), (3, 65536, 4), (8, 33, 1)])
 def test_gather_multi(dev_ctx, nsrc, shard, offset):
     """One-shot all-gather copy: dst[r * shard:] = srcs[r][:shard] (vector path
-    for 16-B aligned rows, byte path otherwise)."""
+    for 16-B aligned rows, byte path otherwise); then again with one row's
+    source NULL (a member's own shard), which must stay untouched."""
     srcs = [np.frombuffer(np.random.default_rng(r).bytes(shard), np.uint8) for r in range(nsrc)]
     bufs = [dev_ctx.alloc(shard + 16) for _ in range(nsrc)]
     out = dev_ctx.alloc(nsrc * shard + 16)
@@ -335,6 +336,20 @@ def test_gather_multi(dev_ctx, nsrc, shard, offset):
         dev_ctx.sync()
         got = out.download(np.uint8, nsrc * shard, offset)
         assert (got == np.concatenate(srcs)).all()
+        if nsrc > 1:
+            skip = nsrc // 2
+            out.upload(np.full(nsrc * shard, 0xA5, np.uint8), offset)
+            ptrs = [None if r == skip else b.ptr + offset for r, b in enumerate(bufs)]
+            assert dev_ctx.gather_multi(out.ptr + offset, ptrs, shard) == 0, _lib.last_error()
+            dev_ctx.sync()
+            got = out.download(np.uint8, nsrc * shard, offset).reshape(nsrc, shard)
+            for r in range(nsrc):
+                if r == skip:
+                    assert (got[r] == 0xA5).all(), "NULL row overwritten"
+                else:
+                    assert (got[r] == srcs[r]).all(), r
+        assert dev_ctx.gather_multi(out.ptr, [None] * nsrc, shard) == \
+            xucg_amd.UCS_ERR_INVALID_PARAM
     finally:
         for b in bufs:
             b.free()

@@ -501,6 +501,9 @@ k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
     const unsigned r  = blockIdx.x % nsrc;
     const size_t wg   = blockIdx.x / nsrc;
     const char *src   = static_cast<const char*>(srcs.p[r]);
+    if (src == nullptr) {
+        return;                   /* row left in place (uniform per workgroup) */
+    }
     char *out         = dst + (size_t)r * row_stride;
     const size_t nvec = nbytes / 16;
     const size_t i    = wg * kReduceBlock + threadIdx.x;
@@ -523,6 +526,9 @@ k_gather_multi_bytes(char *dst, SrcList srcs, unsigned nsrc, size_t shard_bytes)
     const size_t wg    = blockIdx.x / nsrc;
     const size_t nwg   = gridDim.x / nsrc;
     const char *src    = static_cast<const char*>(srcs.p[r]);
+    if (src == nullptr) {
+        return;
+    }
     char *out          = dst + (size_t)r * shard_bytes;
     for (size_t i = wg * kBlock + threadIdx.x; i < shard_bytes; i += nwg * kBlock) {
         out[i] = src[i];
@@ -543,14 +549,16 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
     }
     SrcList list;
     bool aligned = ((uintptr_t)dst % 16) == 0 && shard_bytes % 16 == 0;  /* rows too */
+    unsigned live = 0;
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
-        if (i < nsrc) {
-            if (srcs[i] == nullptr) {
-                return set_error(UCS_ERR_INVALID_PARAM, "gather_multi", "NULL source");
-            }
+        if (i < nsrc && srcs[i] != nullptr) {
+            live++;
             aligned = aligned && ((uintptr_t)srcs[i] % 16) == 0;
         }
+    }
+    if (live == 0) {
+        return set_error(UCS_ERR_INVALID_PARAM, "gather_multi", "every source is NULL");
     }
     char *d = static_cast<char*>(dst);
     if (!aligned) {
@@ -567,7 +575,8 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
             const size_t chunk = nvec - done < per_max ? nvec - done : per_max;
             SrcList sl = list;
             for (unsigned i = 0; i < nsrc; i++) {
-                sl.p[i] = static_cast<const char*>(list.p[i]) + done * 16;
+                sl.p[i] = list.p[i] ? static_cast<const char*>(list.p[i]) + done * 16
+                                    : nullptr;
             }
             /* the tail rides with the last dispatch */
             const size_t nbytes = (done + chunk == nvec) ? shard_bytes - done * 16
@@ -582,7 +591,7 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
     }
     HIP_TRY(hipGetLastError());
     ctx->counters[0]++;
-    ctx->counters[1] += 2 * (uint64_t)nsrc * shard_bytes;
+    ctx->counters[1] += 2 * (uint64_t)live * shard_bytes;
     return UCS_OK;
 }
 

@@ -243,19 +243,21 @@ def oneshot_all_gather(ctx, shard_peers, out_ptr, count, dt, world):
 
 
 def _gather_rows(ctx, out_ptr, ptrs, rows, count, size, world):
-    """out[shard r] = ptrs[r][0 : len(shard r)] for every r in `rows` (sorted
-    member indices), as few launches as the shard_bounds layout allows: one
-    per run of consecutive equal-sized rows."""
-    runs = []
-    for r in rows:
-        lo, hi = shard_bounds(count, size, world, r)
-        nbytes = (hi - lo) * size
-        if runs and runs[-1][1] + runs[-1][2] == r and runs[-1][3] == nbytes:
-            runs[-1][2] += 1
-        else:
-            runs.append([lo * size, r, 1, nbytes])
-    for off, first, n, nbytes in runs:
-        _lib.check(ctx.gather_multi(out_ptr + off, ptrs[first:first + n], nbytes),
+    """out[shard r] = ptrs[r][0 : len(shard r)] for every r in `rows` (member
+    indices), in as few launches as the shard_bounds layout allows: one for
+    all equal-sized rows - rows not gathered are passed as NULL and left in
+    place, so the launch still reads every peer at once - and one for an
+    unequal last row."""
+    lo0, hi0 = shard_bounds(count, size, world, 0)
+    per = (hi0 - lo0) * size
+    lo_l, hi_l = shard_bounds(count, size, world, world - 1)
+    last = (hi_l - lo_l) * size
+    nrows = world if last == per else world - 1
+    srcs = [ptrs[r] if r in rows else None for r in range(nrows)]
+    if any(p is not None for p in srcs):
+        _lib.check(ctx.gather_multi(out_ptr, srcs, per), "ucg_builtin_dev_gather_multi")
+    if nrows < world and world - 1 in rows:
+        _lib.check(ctx.gather_multi(out_ptr + lo_l * size, [ptrs[world - 1]], last),
                    "ucg_builtin_dev_gather_multi")
 
 
@@ -289,9 +291,8 @@ def oneshot_allreduce(ctx, send_peers, recv_peers, count, dt, op, rank, world, b
     if world > 1:
         shard_ptrs = [p + shard_bounds(count, size, world, r)[0] * size
                       for r, p in enumerate(recv_peers.ptrs)]
-        for rows in (list(range(rank)), list(range(rank + 1, world))):
-            if rows:
-                _gather_rows(ctx, out, shard_ptrs, rows, count, size, world)
+        _gather_rows(ctx, out, shard_ptrs, [r for r in range(world) if r != rank], count,
+                     size, world)
     barrier()
 
 
