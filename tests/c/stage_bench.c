@@ -83,6 +83,22 @@ int main(int argc, char **argv)
         t0 = now_s() - t0;
         t_cpu = t0 < t_cpu ? t0 : t_cpu;
     }
+    /* cost of the memory-kind query the dispatcher makes per step (and per
+     * whole-buffer combine): pageable host memory and device memory */
+    double mk_host_ns, mk_dev_ns;
+    {
+        void *d = ucg_builtin_dev_malloc(ctx, 4096);
+        const int k = 100000;
+        int acc = 0;
+        t0 = now_s();
+        for (i = 0; i < k; i++) acc += ucg_builtin_dev_mem_kind(dst + (i & 1023));
+        mk_host_ns = (now_s() - t0) / k * 1e9;
+        t0 = now_s();
+        for (i = 0; i < k; i++) acc += ucg_builtin_dev_mem_kind((char*)d + (i & 1023));
+        mk_dev_ns = (now_s() - t0) / k * 1e9;
+        ucg_builtin_dev_free(ctx, d);
+        if (acc < 0) return 4;
+    }
     {
         uint64_t c[4];
         ucg_builtin_dev_counters(ctx, c);
@@ -90,10 +106,11 @@ int main(int argc, char **argv)
                "\"bytes\": %zu, \"fragment_bytes\": %zu, \"fragments\": %zu, "
                "\"device_staged_ms\": %.3f, \"device_staged_gibs_n\": %.2f, "
                "\"cpu_fragmented_ms\": %.3f, \"cpu_fragmented_gibs_n\": %.2f, "
-               "\"kernel_launches_total\": %llu, \"bit_exact\": %s}\n",
+               "\"kernel_launches_total\": %llu, \"bit_exact\": %s, "
+               "\"mem_kind_ns_host\": %.1f, \"mem_kind_ns_device\": %.1f}\n",
                total, frag, (total + frag - 1) / frag, t_dev * 1e3,
                total / t_dev / 1073741824.0, t_cpu * 1e3, total / t_cpu / 1073741824.0,
-               (unsigned long long)c[0], ok ? "true" : "false");
+               (unsigned long long)c[0], ok ? "true" : "false", mk_host_ns, mk_dev_ns);
     }
     ucg_builtin_dev_ctx_destroy(ctx);
     free(src);
