@@ -50,6 +50,13 @@ def main():
                 row["gbs"].append(round(3 * b / (us * 1e-6) / 1e9, 1))
             row["frac_1gib"] = round(row["gbs"][-1] / PEAK, 4)
             row["frac_256mib"] = round(row["gbs"][-2] / PEAK, 4)
+            # src one element out of dst's 16-B phase (8 B for 16-B-phase
+            # dtypes would be the same kernel): the realigning kernel
+            if sz < 16:
+                n = (256 << 20) // sz - 1
+                ctx.profile_reduce(op, dt, dst, src.ptr + sz, n, 2)
+                us = ctx.profile_reduce(op, dt, dst, src.ptr + sz, n, 20)
+                row["shifted_256mib_frac"] = round(3 * n * sz / (us * 1e-6) / 1e9 / PEAK, 4)
             res["device"].append(row)
             print(f"{dt:9s} {op:5s} 1KiB {row['us'][0]:7.2f} us  256MiB "
                   f"{row['gbs'][-2]:7.0f} GB/s  1GiB {row['gbs'][-1]:7.0f} GB/s "

@@ -479,6 +479,35 @@ def test_random_multi_cases_against_oracle(dev_ctx):
             b.free()
 
 
+@pytest.mark.gpu
+def test_shift_kernel_every_dtype_and_op(dev_ctx):
+    """Every supported (dtype, op) pair through the realigning kernel: src one
+    element out of dst's 16-B phase, a ragged count spanning several waves,
+    all three distributions, bit-exact against the oracle."""
+    n = 64 * 16 * 3 + 5
+    bs, bd = dev_ctx.alloc(n * 8 + 64), dev_ctx.alloc(n * 8 + 64)
+    try:
+        for dt in O.DTYPES:
+            st = O.storage(dt)
+            sz = np.dtype(st).itemsize
+            for op in O.OPS:
+                if not O.is_supported(dt, op):
+                    continue
+                for dist in O.DISTS:
+                    src = O.fill(dt, dist, 31, n)
+                    dst = O.fill(dt, dist, 32, n)
+                    bs.upload(src, sz)
+                    bd.upload(dst, 0)
+                    dev_ctx.reduce_checked(op, dt, bd.ptr, bs.ptr + sz, n)
+                    dev_ctx.sync()
+                    got = bd.download(st, n)
+                    want = O.reduce(op, dt, src, dst)
+                    assert (bits(got) == bits(want)).all(), (dt, op, dist)
+    finally:
+        bs.free()
+        bd.free()
+
+
 SHIFT_COUNTS = [1, 5, 16, 17, 63 * 4 + 3, 64 * 16, 64 * 16 + 1, 65 * 16 + 7, 128 * 16, 4099,
                 64 * 64 * 16 + 9]
 
