@@ -45,8 +45,10 @@ def test_recursive_doubling_plan_over_gloo(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_oneshot_reduce_scatter_over_ipc(world):
+    """world 8 rehearses the driver's 8-GPU node: 8 processes, 7 peer
+    mappings each, the same shard bounds and gather rows (all on cuda:0)."""
     codes, outs = launch("_worker_ipc.py", world, timeout=300)
     assert codes == [0] * world, "\n".join(outs)
 
