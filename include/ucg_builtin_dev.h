@@ -32,6 +32,10 @@
  *                                      2^k ranks (builtin/plan/
  *                                      builtin_recursive.c:158-169), evaluated
  *                                      in one pass (one-shot reduce-scatter).
+ *   ucg_builtin_dev_reduce_tree()   <- the same for the tree plan's fan-in at
+ *                                      its root (builtin/plan/builtin_tree.c:
+ *                                      262-380, builtin_comp_step.inl:213-221),
+ *                                      any group size.
  *   ucg_builtin_dev_ctx_create/
  *   ucg_builtin_dev_ctx_destroy()   <- per-group state that lives in
  *                                      struct ucg_builtin_group_ctx
@@ -211,6 +215,20 @@ ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
                                           void *dst, const void *const *srcs,
                                           unsigned nsrc, unsigned self,
                                           size_t count);
+
+/* One-shot tree fan-in in the association of the reference's tree plan at
+ * its root (builtin/plan/builtin_tree.c:262-380 on one host: the root is the
+ * only parent; init_reduce seeds the root's accumulator with its own data,
+ * builtin/ops/builtin_control.c:43-47, and each child's message is reduced
+ * into it as it arrives, builtin/ops/builtin_comp_step.inl:213-221):
+ *   acc = srcs[0];  acc = srcs[m] (op) acc  for m = 1 .. nsrc-1
+ * srcs[0] is the root's contribution and srcs[1..] the children in arrival
+ * order. Any nsrc <= 16: the plan for groups that are not a power of two,
+ * and for MPI_Reduce. srcs may be peer-mapped; dst may alias any source. */
+ucs_status_t ucg_builtin_dev_reduce_tree(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
+                                         ucg_dev_dtype_t dt, void *dst,
+                                         const void *const *srcs, unsigned nsrc,
+                                         size_t count);
 
 /* ---- host-resident combine (the reduce_cb_f contract, staged) ------------*/
 /* Whole-buffer: dst_host[i] = src_host[i] (op) dst_host[i]. Host chunks are

@@ -596,3 +596,45 @@ def test_staged_runs_keep_the_accumulator_phase(dt):
         finally:
             ctx.close()
     assert max(launches.values()) <= min(launches.values()) + 2, launches
+
+
+@pytest.mark.gpu
+def test_reduce_tree_vs_oracle(dev_ctx):
+    """ucg_builtin_dev_reduce_tree: the tree plan's fan-in association for
+    every group size 1..16 (the NMAX 4, 8 and 16 kernels), with every operand
+    in dst's phase and with one out of phase (element loop), and with dst
+    aliasing the root's operand; bit-exact against the oracle's
+    tree_reduce (root 0, children in ascending order)."""
+    rng = np.random.default_rng(11)
+    pairs = [(dt, op) for dt in O.DTYPES for op in O.OPS if O.is_supported(dt, op)]
+    count = 64 * 16 * 2 + 3
+    bufs = [dev_ctx.alloc(count * 8 + 64) for _ in range(16)]
+    out = dev_ctx.alloc(count * 8 + 64)
+    try:
+        for n in range(1, 17):
+            dt, op = pairs[int(rng.integers(len(pairs)))]
+            st = O.storage(dt)
+            sz = np.dtype(st).itemsize
+            xs = [O.fill(dt, ("round", "special")[m % 2], 500 + 17 * n + m, count)
+                  for m in range(n)]
+            want = O.tree_reduce(op, dt, xs, root=0)
+            for shifted in (False, True):
+                offs = [sz if (shifted and m == n // 2) else 0 for m in range(n)]
+                for b, x, o in zip(bufs, xs, offs):
+                    b.upload(x, o)
+                srcs = [b.ptr + o for b, o in zip(bufs, offs)]
+                assert dev_ctx.reduce_tree(op, dt, out.ptr, srcs, count) == 0, _lib.last_error()
+                dev_ctx.sync()
+                got = out.download(st, count)
+                assert (bits(got) == bits(want)).all(), (n, dt, op, shifted)
+            for b, x in zip(bufs, xs):
+                b.upload(x)
+            srcs = [b.ptr for b in bufs[:n]]
+            assert dev_ctx.reduce_tree(op, dt, bufs[0].ptr, srcs, count) == 0
+            dev_ctx.sync()
+            assert (bits(bufs[0].download(st, count)) == bits(want)).all(), (n, "aliased")
+        assert dev_ctx.reduce_tree("sum", "float32", out.ptr, [b.ptr for b in bufs] * 2, 4) == \
+            xucg_amd.UCS_ERR_INVALID_PARAM
+    finally:
+        for b in bufs + [out]:
+            b.free()

@@ -45,10 +45,11 @@ def test_recursive_doubling_plan_over_gloo(world):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4, 8])
+@pytest.mark.parametrize("world", [2, 3, 4, 6, 8])
 def test_oneshot_reduce_scatter_over_ipc(world):
     """world 8 rehearses the driver's 8-GPU node: 8 processes, 7 peer
-    mappings each, the same shard bounds and gather rows (all on cuda:0)."""
+    mappings each, the same shard bounds and gather rows (all on cuda:0).
+    Worlds 3 and 6 take the tree plan's association (reduce_tree)."""
     codes, outs = launch("_worker_ipc.py", world, timeout=300)
     assert codes == [0] * world, "\n".join(outs)
 
@@ -116,6 +117,15 @@ class _SimCtx:
         self.calls.append(("reduce_multi", len(srcs), count))
         return 0
 
+    def reduce_tree(self, op, dt, dst, srcs, count):
+        from oracle import oracle as O
+        st = np.dtype(O.storage(dt))
+        xs = [self.mem[s:s + count * st.itemsize].view(st) for s in srcs]
+        out = O.tree_reduce(op, dt, xs, root=0)
+        self.mem[dst:dst + count * st.itemsize] = out.view(np.uint8)
+        self.calls.append(("reduce_tree", len(srcs), count))
+        return 0
+
     def copy_multi(self, dsts, srcs, nbytes):
         assert len(dsts) == len(srcs) <= 16
         for d, s in zip(dsts, srcs):
@@ -138,7 +148,7 @@ class _Peers:
 
 
 @pytest.mark.parametrize("variant", ["pull", "push"])
-@pytest.mark.parametrize("world", [1, 2, 4, 8, 16])
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 6, 8, 16])
 @pytest.mark.parametrize("dt,op,count", [("float32", "sum", 1001), ("int64", "prod", 4099),
                                          ("float16", "max", 7), ("float64", "sum", 1 << 14)])
 def test_oneshot_allreduce_schedule(variant, world, dt, op, count):

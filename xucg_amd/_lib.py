@@ -66,6 +66,8 @@ DEV_API = {
     "ucg_builtin_dev_reduce": (_st, [_vp, _int, _int, _vp, _vp, _sz]),
     "ucg_builtin_dev_reduce_multi": (_st, [_vp, _int, _int, _vp,
                                            ctypes.POINTER(_vp), _u, _u, _sz]),
+    "ucg_builtin_dev_reduce_tree": (_st, [_vp, _int, _int, _vp, ctypes.POINTER(_vp), _u,
+                                          _sz]),
     "ucg_builtin_dev_gather_multi": (_st, [_vp, _vp, ctypes.POINTER(_vp), _u, _sz]),
     "ucg_builtin_dev_copy_multi": (_st, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _u,
                                          _sz]),

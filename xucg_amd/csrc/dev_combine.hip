@@ -107,6 +107,7 @@ int launch_variant()
 struct Tables {
     std::array<std::array<reduce_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST> reduce;
     std::array<std::array<multi_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>  multi;
+    std::array<std::array<tree_fn_t, UCG_DEV_OP_LAST>, UCG_DEV_DT_LAST>   tree;
     std::array<fill_fn_t, UCG_DEV_DT_LAST>                                fill;
 };
 
@@ -118,6 +119,7 @@ static Tables build_tables(std::integer_sequence<int, DTS...>)
     for (int d = 0; d < UCG_DEV_DT_LAST; d++) {
         t.reduce[d] = r[d].reduce;
         t.multi[d]  = r[d].multi;
+        t.tree[d]   = r[d].tree;
         t.fill[d]   = r[d].fill;
     }
     return t;
@@ -481,6 +483,41 @@ ucs_status_t ucg_builtin_dev_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
         }
     }
     HIP_TRY(tables().multi[dt][op](dst, list, nsrc, self, count, ctx->stream));
+    ctx->counters[0]++;
+    ctx->counters[1] += (uint64_t)(nsrc + 1) * count * kDtSize[dt];
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_reduce_tree(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
+                                         ucg_dev_dtype_t dt, void *dst,
+                                         const void *const *srcs, unsigned nsrc,
+                                         size_t count)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "reduce_tree");
+    if (st != UCS_OK) {
+        return st;
+    }
+    if (nsrc == 0 || nsrc > (unsigned)kMaxMulti || srcs == nullptr ||
+        (count && dst == nullptr)) {
+        return set_error(UCS_ERR_INVALID_PARAM, "reduce_tree",
+                         "nsrc must be 1..16, srcs and dst non-NULL");
+    }
+    if (count == 0) {
+        return UCS_OK;
+    }
+    if ((uintptr_t)dst % kDtSize[dt]) {
+        return set_error(UCS_ERR_INVALID_PARAM, "reduce_tree", "misaligned dst");
+    }
+    SrcList list;
+    for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
+        list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
+        if (i < nsrc && (srcs[i] == nullptr ||
+                         ((uintptr_t)srcs[i] % kDtSize[dt]))) {
+            return set_error(UCS_ERR_INVALID_PARAM, "reduce_tree",
+                             "NULL or misaligned source");
+        }
+    }
+    HIP_TRY(tables().tree[dt][op](dst, list, nsrc, count, ctx->stream));
     ctx->counters[0]++;
     ctx->counters[1] += (uint64_t)(nsrc + 1) * count * kDtSize[dt];
     return UCS_OK;

@@ -410,6 +410,77 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
     }
 }
 
+/*
+ * One-shot tree fan-in: the association of the reference's tree plan at its
+ * root (builtin/plan/builtin_tree.c:262-380 on one host; the root's
+ * recv.buffer starts as its own send buffer, builtin_control.c:43-47, and
+ * every child's message is reduced into it as it arrives, dst = child (op)
+ * dst, builtin_comp_step.inl:213-221): acc = srcs[0]; acc = srcs[m] (op) acc
+ * for m = 1 .. n-1, srcs[0] being the root and the rest the children in
+ * arrival order. Any n <= NMAX (the plan for groups that are not a power of
+ * two, and for MPI_Reduce). Operands past n load srcs[0] again (an L2 hit,
+ * no branch between the loads) and are not combined.
+ */
+template <typename T, int OP, int NMAX>
+__global__ void __launch_bounds__(kReduceBlock)
+k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
+{
+    constexpr int V    = 16 / sizeof(T);
+    const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+
+    if (gtid < head || gtid < tail) {
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            size_t j;
+            if (part == 0) {
+                if (gtid >= head) continue;
+                j = gtid;
+            } else {
+                if (gtid >= tail) continue;
+                j = head + nvec * V + gtid;
+            }
+            T acc = static_cast<const T*>(srcs.p[0])[j];
+            for (unsigned m = 1; m < n; m++) {
+                acc = Comb<T, OP>::apply(static_cast<const T*>(srcs.p[m])[j], acc);
+            }
+            dst[j] = acc;
+        }
+    }
+
+    const size_t i = gtid;
+    if (i < nvec) {
+        u32x4 val[NMAX];
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            const void *p = srcs.p[(unsigned)m < n ? m : 0];
+            val[m] = ld16<1>(reinterpret_cast<const u32x4*>(static_cast<const T*>(p) + head) + i);
+        }
+        u32x4 acc = val[0];
+#pragma unroll
+        for (int m = 1; m < NMAX; m++) {
+            if ((unsigned)m < n) {
+                acc = vapply<T, OP>(val[m], acc);
+            }
+        }
+        st16<1>(reinterpret_cast<u32x4*>(dst + head) + i, acc);
+    }
+}
+
+/* the tree fan-in when some operand is out of dst's 16-B phase */
+template <typename T, int OP>
+__global__ void __launch_bounds__(kBlock)
+k_reduce_tree_scalar(T *dst, SrcList srcs, unsigned n, size_t count)
+{
+    const size_t nthr = (size_t)gridDim.x * kBlock;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += nthr) {
+        T acc = static_cast<const T*>(srcs.p[0])[i];
+        for (unsigned m = 1; m < n; m++) {
+            acc = Comb<T, OP>::apply(static_cast<const T*>(srcs.p[m])[i], acc);
+        }
+        dst[i] = acc;
+    }
+}
+
 template <typename T, int OP, int N>
 __global__ void __launch_bounds__(kBlock)
 k_reduce_multi_scalar(T *dst, SrcList srcs, unsigned self, size_t count)

@@ -283,10 +283,87 @@ void launch_fill(void *dst, int dist, uint64_t key, size_t count,
 
 
 
+/* ---- tree fan-in (sequential association) ------------------------------- */
+typedef hipError_t (*tree_fn_t)(void *dst, const SrcList &srcs, unsigned n,
+                                size_t count, hipStream_t st);
+
+template <typename T, int OP, int NMAX>
+void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nvec,
+                   size_t tail, hipStream_t st)
+{
+    constexpr size_t V = 16 / sizeof(T);
+    size_t done = 0;
+    do {
+        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
+        const bool first = (done == 0), last = (done + chunk == nvec);
+        const size_t off = first ? 0 : head + done * V;
+        SrcList sl;
+        for (int m = 0; m < kMaxMulti; m++) {
+            sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
+        }
+        const unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
+        hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX>), dim3(grid), dim3(kReduceBlock), 0,
+                           st, d + off, sl, n, first ? head : 0, chunk, last ? tail : 0);
+        done += chunk;
+    } while (done < nvec);
+}
+
+template <int DT, int OP>
+hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
+                       hipStream_t st)
+{
+    typedef typename DtType<DT>::T T;
+    constexpr size_t sz = sizeof(T), V = 16 / sz;
+    const uintptr_t md = (uintptr_t)dst & 15;
+    bool aligned = true;
+    for (unsigned m = 0; m < n; m++) {
+        aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
+    }
+    T *d = static_cast<T*>(dst);
+    if (!aligned) {
+        const unsigned grid = grid_for(count, kBlock, launch_max_blocks());
+        hipLaunchKernelGGL((k_reduce_tree_scalar<T, OP>), dim3(grid), dim3(kBlock), 0, st,
+                           d, srcs, n, count);
+        return hipGetLastError();
+    }
+    size_t head = md ? (16 - md) / sz : 0;
+    if (head > count) {
+        head = count;
+    }
+    const size_t rem = count - head, nvec = rem / V, tail = rem % V;
+    if (n <= 4) {
+        launch_tree_n<T, OP, 4>(d, srcs, n, head, nvec, tail, st);
+    } else if (n <= 8) {
+        launch_tree_n<T, OP, 8>(d, srcs, n, head, nvec, tail, st);
+    } else {
+        launch_tree_n<T, OP, 16>(d, srcs, n, head, nvec, tail, st);
+    }
+    return hipGetLastError();
+}
+
+template <int DT, int OP>
+constexpr tree_fn_t tree_entry()
+{
+    if constexpr (pair_supported(DT, OP)) {
+        return &launch_tree<DT, OP>;
+    } else {
+        return nullptr;
+    }
+}
+
+template <int DT, int... OPS>
+constexpr std::array<tree_fn_t, UCG_DEV_OP_LAST>
+tree_row(std::integer_sequence<int, OPS...>)
+{
+    return {tree_entry<DT, OPS>()...};
+}
+
+
 /* every launcher of one dtype */
 struct RowSet {
     std::array<reduce_fn_t, UCG_DEV_OP_LAST> reduce;
     std::array<multi_fn_t, UCG_DEV_OP_LAST>  multi;
+    std::array<tree_fn_t, UCG_DEV_OP_LAST>   tree;
     fill_fn_t                                fill;
 };
 
@@ -295,6 +372,7 @@ RowSet make_rows()
 {
     return {reduce_row<DT>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>()),
             multi_row<DT>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>()),
+            tree_row<DT>(std::make_integer_sequence<int, UCG_DEV_OP_LAST>()),
             &launch_fill<DT>};
 }
 

@@ -191,6 +191,13 @@ class DevContext:
                                                        dt_index(dt), _ptr(dst), arr,
                                                        len(srcs), self_index, count)
 
+    def reduce_tree(self, op, dt, dst, srcs, count):
+        """Tree fan-in: acc = srcs[0]; acc = srcs[m] (op) acc for m = 1.. ."""
+        arr = (ctypes.c_void_p * len(srcs))(*[_ptr(s) for s in srcs])
+        return _lib.dev().ucg_builtin_dev_reduce_tree(self.handle, op_index(op),
+                                                      dt_index(dt), _ptr(dst), arr,
+                                                      len(srcs), count)
+
     def gather_multi(self, dst, srcs, shard_bytes):
         """dst[r * shard_bytes:...] = srcs[r][:shard_bytes] in one launch."""
         arr = (ctypes.c_void_p * len(srcs))(*[_ptr(s) for s in srcs])

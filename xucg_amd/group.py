@@ -15,7 +15,11 @@ allreduce a buffer across 2^k members, all built on the same combine:
                                 association as the plan in registers
                                 (ucg_builtin_dev_reduce_multi); followed by an
                                 all-gather. Bit-exact with the plan's result
-                                on the shard owner.
+                                on the shard owner. Groups that are not a
+                                power of two get the plan the reference takes
+                                there, the tree fan-in at member 0
+                                (ucg_builtin_dev_reduce_tree), so the one-shot
+                                forms work for any size up to 16.
   recursive_halving_allreduce   reduce-scatter by recursive halving with the
                                 plan's peer order (my ^ 1, my ^ 2, ...) then
                                 all-gather by recursive doubling (SURVEY.md 8e,
@@ -212,6 +216,25 @@ class PeerBuffers:
             raise err
 
 
+def is_pow2(n):
+    return n > 0 and n & (n - 1) == 0
+
+
+def _combine_shard(ctx, op, dt, out_ptr, srcs, rank, world, n):
+    """One member's shard of a one-shot reduce-scatter, srcs in member order:
+    the recursive-doubling plan's association V(rank, log2 N) for 2^k members
+    (builtin_recursive.c:158-169), and for any other group size the plan the
+    reference takes there - the tree fan-in at member 0 with the children
+    arriving in ascending order (builtin.c:112-121, builtin_tree.c:262-380).
+    Either way every member's shard is bit-identical to what that plan leaves
+    in every member's buffer."""
+    if is_pow2(world):
+        _lib.check(ctx.reduce_multi(op, dt, out_ptr, srcs, rank, n),
+                   "ucg_builtin_dev_reduce_multi")
+    else:
+        _lib.check(ctx.reduce_tree(op, dt, out_ptr, srcs, n), "ucg_builtin_dev_reduce_tree")
+
+
 def oneshot_reduce_scatter(ctx, peers, out_ptr, count, dt, op, rank, world):
     """out[0:hi-lo] = V(rank, log2 world) over shard [lo, hi) of every member's
     buffer, read in place through `peers` (no staging copy). The caller must
@@ -220,8 +243,7 @@ def oneshot_reduce_scatter(ctx, peers, out_ptr, count, dt, op, rank, world):
     size = _lib.DTYPE_SIZE[_lib.dt_index(dt)]
     lo, hi = shard_bounds(count, size, world, rank)
     srcs = [p + lo * size for p in peers.ptrs]
-    _lib.check(ctx.reduce_multi(op, dt, out_ptr, srcs, rank, hi - lo),
-               "ucg_builtin_dev_reduce_multi")
+    _combine_shard(ctx, op, dt, out_ptr, srcs, rank, world, hi - lo)
     return lo, hi
 
 
@@ -285,8 +307,7 @@ def oneshot_allreduce(ctx, send_peers, recv_peers, count, dt, op, rank, world, b
     lo, hi = shard_bounds(count, size, world, rank)
     out = recv_peers.ptrs[rank]
     srcs = [p + lo * size for p in send_peers.ptrs]
-    _lib.check(ctx.reduce_multi(op, dt, out + lo * size, srcs, rank, hi - lo),
-               "ucg_builtin_dev_reduce_multi")
+    _combine_shard(ctx, op, dt, out + lo * size, srcs, rank, world, hi - lo)
     barrier()
     if world > 1:
         shard_ptrs = [p + shard_bounds(count, size, world, r)[0] * size
@@ -343,8 +364,7 @@ def push_reduce_scatter(ctx, x_ptr, stage_peers, out_ptr, count, dt, op, rank, w
     lo, hi = shard_bounds(count, size, world, rank)
     stage = stage_peers.ptrs[rank]
     srcs = [x_ptr + lo * size if m == rank else stage + m * slot for m in range(world)]
-    _lib.check(ctx.reduce_multi(op, dt, out_ptr, srcs, rank, hi - lo),
-               "ucg_builtin_dev_reduce_multi")
+    _combine_shard(ctx, op, dt, out_ptr, srcs, rank, world, hi - lo)
     return lo, hi
 
 
@@ -382,4 +402,7 @@ def oracle_shard(op, dt, inputs, rank, world, oracle):
     """Expected one-shot shard for tests: the plan's result on the owner."""
     size = np.dtype(inputs[0].dtype).itemsize
     lo, hi = shard_bounds(inputs[0].size, size, world, rank)
-    return lo, hi, oracle.reduce_multi(op, dt, [x[lo:hi] for x in inputs], rank)
+    shards = [x[lo:hi] for x in inputs]
+    if is_pow2(len(inputs)):
+        return lo, hi, oracle.reduce_multi(op, dt, shards, rank)
+    return lo, hi, oracle.tree_reduce(op, dt, shards, root=0)
