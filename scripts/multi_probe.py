@@ -50,6 +50,32 @@ def main():
             res.append(row)
             del srcs, out
             torch.cuda.empty_cache()
+    # the tree fan-in (groups that are not a power of two), 64 MiB operands
+    n = (64 << 20) // 4
+    for nsrc in (3, 6, 8, 12):
+        srcs = [torch.empty(n, dtype=torch.float32, device="cuda") for _ in range(nsrc)]
+        for r, s in enumerate(srcs):
+            ctx.fill("float32", "exact", 200 + r, s, n)
+        out = torch.empty(n, dtype=torch.float32, device="cuda")
+        for _ in range(3):
+            rc = ctx.reduce_tree("sum", "float32", out, srcs, n)
+            assert rc == 0, (rc, xucg_amd._lib.last_error())
+        torch.cuda.synchronize()
+        assert torch.equal(out, torch.stack(srcs).sum(0)), "tree combine mismatch"
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            ctx.reduce_tree("sum", "float32", out, srcs, n)
+        e1.record()
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / 20
+        gbs = (nsrc + 1) * n * 4 / (us * 1e-6) / 1e9
+        row = {"kernel": "reduce_tree", "nsrc": nsrc, "bytes_per_operand": n * 4,
+               "us": round(us, 2), "gbs": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
+        print(row, flush=True)
+        res.append(row)
+        del srcs, out
+        torch.cuda.empty_cache()
     ctx.close()
     if len(sys.argv) > 1:
         with open(sys.argv[1], "w") as f:
