@@ -8,6 +8,7 @@ against the oracle's simulation of the reference plan:
   allreduce       both in one operation into a recv buffer
   push forms      the same reduce-scatter and allreduce with every transfer a
                   write into a peer's buffer (stage slots, recv shards)
+  reduce          MPI_Reduce to the last member: the tree fan-in, one launch
 
 Every buffer is exported once, and all mappings are released by every
 member (PeerBuffers.close, a collective) before any member frees a buffer."""
@@ -93,6 +94,17 @@ def main():
         for r, (rlo, rhi, rwant) in enumerate(shards):
             if not (O.bits(allgot[rlo:rhi]) == O.bits(rwant)).all():
                 fail(rank, f"push allreduce {dt} {op} shard {r}")
+
+        # MPI_Reduce to the last member: the tree fan-in read in one launch
+        root = world - 1
+        ctx.fill(dt, "special", 995, full, n)
+        barrier()
+        if G.oneshot_reduce(ctx, peers, full.ptr, n, dt, op, rank, world, root):
+            ctx.sync()
+            want = O.tree_reduce(op, dt, inputs, root=root)
+            if not (O.bits(full.download(st, n)) == O.bits(want)).all():
+                fail(rank, f"reduce to root {root} {dt} {op}")
+        barrier()
 
         for p in (peers, speers, rpeers, tpeers):
             p.close()                       # collective: all mappings gone

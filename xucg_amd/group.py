@@ -317,6 +317,23 @@ def oneshot_allreduce(ctx, send_peers, recv_peers, count, dt, op, rank, world, b
     barrier()
 
 
+def oneshot_reduce(ctx, send_peers, out_ptr, count, dt, op, rank, world, root):
+    """MPI_Reduce to `root` in one launch (AGGREGATE|SINGLE_DESTINATION,
+    which the reference always runs as the tree fan-in, builtin.c:95-121):
+    the root reads every member's send buffer in place through `send_peers`
+    (all N-1 links at once) and writes the fan-in association of
+    builtin_tree.c:262-380 - its own data first, then the children in
+    ascending order - into out_ptr. The other members launch nothing; the
+    caller's barrier after the call keeps their buffers alive until the root
+    is done. Returns True on the root."""
+    if rank != root:
+        return False
+    order = [root] + [m for m in range(world) if m != root]
+    _lib.check(ctx.reduce_tree(op, dt, out_ptr, [send_peers.ptrs[m] for m in order], count),
+               "ucg_builtin_dev_reduce_tree")
+    return True
+
+
 def stage_slot_bytes(count, elem_size, world):
     """Slot size of the push reduce-scatter's stage: the largest shard (the
     last one), rounded up to 256 B."""
