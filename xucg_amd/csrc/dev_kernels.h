@@ -220,6 +220,41 @@ k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
     }
 }
 
+/* A/B variant of k_reduce_shift without the cross-lane step: every lane
+ * loads both aligned vectors A[i] and A[i+1] itself (the second load mostly
+ * hits lines the first load of the neighbouring lane brought into L2), so a
+ * lane's store waits only for its own loads. */
+template <typename T, int OP, int Q>
+__global__ void __launch_bounds__(kReduceBlock)
+k_reduce_shift2(T *dst, const T *src, size_t head, size_t nvec, size_t tail, unsigned rb)
+{
+    constexpr int V   = 16 / sizeof(T);
+    const size_t gtid = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+    if (gtid < head) {
+        dst[gtid] = Comb<T, OP>::apply(src[gtid], dst[gtid]);
+    }
+    if (gtid < tail) {
+        const size_t j = head + nvec * V + gtid;
+        dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
+    }
+    const size_t i = gtid;
+    if (i < nvec) {
+        const char *sp  = reinterpret_cast<const char*>(src + head);
+        const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
+        u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
+        const u32x4 b  = ld16<1>(d4 + i);
+        const u32x4 lo = ld16<1>(a4 + i);
+        const u32x4 hi = ld16<1>(a4 + i + 1);
+        const uint32_t w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        u32x4 sv;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
+        }
+        st16<1>(d4 + i, vapply<T, OP>(sv, b));
+    }
+}
+
 template <typename T, int OP>
 __global__ void __launch_bounds__(kBlock)
 k_reduce_scalar(T *dst, const T *src, size_t count)

@@ -127,12 +127,19 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
         /* operands disagree mod 16 B: src realigned in registers */
         const unsigned r = (unsigned)((ms + 16 - md) & 15);
         if constexpr (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM) {
-            if (variant >= 5 && variant <= 7 && r == 4) {
+            if (variant >= 5 && variant <= 8 && r == 4) {
                 /* A/B: U = 2 or 4 vectors per lane (one extra load per 64 U),
-                 * or the DPP lane shift instead of ds_bpermute */
+                 * the DPP lane shift instead of ds_bpermute, or every lane
+                 * loading both aligned vectors (no cross-lane step) */
                 if (variant == 5)      launch_shift<T, OP, 1, 2>(d, s, head, nvec, tail, 0, st);
                 else if (variant == 6) launch_shift<T, OP, 1, 4>(d, s, head, nvec, tail, 0, st);
-                else                   launch_shift<T, OP, 1, 1, 1>(d, s, head, nvec, tail, 0, st);
+                else if (variant == 7) launch_shift<T, OP, 1, 1, 1>(d, s, head, nvec, tail, 0, st);
+                else if (nvec < kMaxVecPerLaunch) {
+                    const unsigned g = grid_for(nvec > head ? nvec : head, kReduceBlock,
+                                                0x7fffffff);
+                    hipLaunchKernelGGL((k_reduce_shift2<T, OP, 1>), dim3(g), dim3(kReduceBlock),
+                                       0, st, d, s, head, nvec, tail, 0u);
+                }
                 return hipGetLastError();
             }
         }
