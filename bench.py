@@ -712,6 +712,15 @@ def main():
     # SURVEY.md 8d also asks for the median of individually timed launches
     singles = sorted(ctx.profile_reduce("sum", "float32", dst, src, n, 1) for _ in range(21))
     median_us = singles[len(singles) // 2]
+    # the box's measured ceiling beside it, same geometry and buffers: both
+    # operands read with no stores (2N bytes), and a copy (2N bytes); 5
+    # batches of 50, median batch, interleaved with the combine
+    ceil = {}
+    for kind, name in ((0, "read_only"), (1, "copy")):
+        ctx.profile_stream(kind, dst, src, n * 4, 20)
+        b = sorted(ctx.profile_stream(kind, dst, src, n * 4, 50) for _ in range(5))
+        ceil[name] = 2 * n * 4 / (b[2] * 1e-6) / 1e9
+    ctx.fill("float32", "round", 0x5EED0001 + 2 * rank, dst, n)   # the copy overwrote dst
 
     extra = {}
     if not args.no_extra and rank == 0:
@@ -801,6 +810,12 @@ def main():
                 "frac_from_median": round(bytes_per_step / (median_us * 1e-6) / 1e9
                                           / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes_per_launch": bytes_per_step,
+                "measured_ceiling_same_box": {
+                    "read_only_gbs": round(ceil["read_only"], 1),
+                    "copy_gbs": round(ceil["copy"], 1),
+                    "combine_frac_of_read_only": round(achieved / ceil["read_only"], 4),
+                    "note": "same geometry and buffers, both operands read with no "
+                            "stores / src copied to dst (ucg_builtin_dev_profile_stream)"},
             },
             "cpu_baseline": cpu,
             "extra": extra,

@@ -296,6 +296,17 @@ ucs_status_t ucg_builtin_dev_profile_reduce(ucg_builtin_dev_ctx_t *ctx,
                                             void *dst, const void *src,
                                             size_t count, unsigned iters,
                                             double *avg_us);
+
+/* Measurement reference, not part of the combine path: the same launch
+ * geometry (one wave per workgroup, one non-temporal 16-B vector per lane per
+ * stream) streaming `bytes` bytes per stream. kind 0: read two streams (src,
+ * dst) with no stores; kind 1: copy src -> dst. Average duration of one of
+ * `iters` back-to-back launches in us. It gives the box's measured ceiling
+ * beside the combine. bytes must be a multiple of 16 and both
+ * pointers 16-B aligned. */
+ucs_status_t ucg_builtin_dev_profile_stream(ucg_builtin_dev_ctx_t *ctx, int kind,
+                                            void *dst, const void *src, size_t bytes,
+                                            unsigned iters, double *avg_us);
 /* Counters since ctx creation: [0] kernel launches, [1] bytes combined on the
  * device (3N basis), [2] H2D bytes, [3] D2H bytes. */
 void         ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx, uint64_t out[4]);

@@ -257,6 +257,15 @@ class DevContext:
               "ucg_builtin_dev_profile_reduce")
         return us.value
 
+    def profile_stream(self, kind, dst, src, nbytes, iters):
+        """Measured ceiling in the combine's geometry: kind 0 reads both
+        buffers (no stores), kind 1 copies src -> dst. Average us per launch."""
+        us = ctypes.c_double()
+        check(_lib.dev().ucg_builtin_dev_profile_stream(self.handle, kind, _ptr(dst), _ptr(src),
+                                                        nbytes, iters, ctypes.byref(us)),
+              "ucg_builtin_dev_profile_stream")
+        return us.value
+
     def counters(self):
         out = (ctypes.c_uint64 * 4)()
         _lib.dev().ucg_builtin_dev_counters(self.handle, out)
