@@ -480,6 +480,42 @@ def test_random_multi_cases_against_oracle(dev_ctx):
 
 
 @pytest.mark.gpu
+def test_random_tree_cases_against_oracle(dev_ctx):
+    """Fuzz of the tree fan-in kernel: random n in 1..16, dtype/op, count and
+    per-operand element offsets (vector path when all agree mod 16 B, element
+    loop otherwise), against the oracle's tree_reduce (root first, children in
+    the given order)."""
+    rng = np.random.default_rng(8)
+    pairs = [(dt, op) for dt in O.DTYPES for op in O.OPS if O.is_supported(dt, op)]
+    cap = 20_000 * 8 + 256
+    bufs = [dev_ctx.alloc(cap) for _ in range(17)]
+    try:
+        for case in range(120):
+            dt, op = pairs[rng.integers(len(pairs))]
+            n = int(rng.integers(1, 17))
+            count = int(rng.choice([0, 1, 5, 31, 4099, int(rng.integers(1, 20_000))]))
+            st = O.storage(dt)
+            sz = np.dtype(st).itemsize
+            same_off = rng.random() < 0.5
+            base_off = int(rng.integers(16)) * sz
+            offs = [base_off if same_off else int(rng.integers(16)) * sz for _ in range(n + 1)]
+            xs = [O.fill(dt, "special" if rng.random() < 0.3 else "round", 91 * case + r, count)
+                  for r in range(n)]
+            for r in range(n):
+                bufs[r].upload(xs[r], offs[r])
+            rc = dev_ctx.reduce_tree(op, dt, bufs[16].ptr + offs[n],
+                                     [bufs[r].ptr + offs[r] for r in range(n)], count)
+            assert rc == 0, _lib.last_error()
+            dev_ctx.sync()
+            got = bufs[16].download(st, count, offs[n])
+            want = O.tree_reduce(op, dt, xs, root=0) if count else got
+            assert (O.bits(got) == O.bits(want)).all(), (case, dt, op, n, count, offs)
+    finally:
+        for b in bufs:
+            b.free()
+
+
+@pytest.mark.gpu
 def test_shift_kernel_every_dtype_and_op(dev_ctx):
     """Every supported (dtype, op) pair through the realigning kernel: src one
     element out of dst's 16-B phase, a ragged count spanning several waves,
