@@ -29,7 +29,7 @@ def main():
     out = sys.argv[1] if len(sys.argv) > 1 else None
     variant = os.environ.get("UCX_BUILTIN_DEV_VARIANT", "0")
     ctx = xucg_amd.DevContext(device=0)
-    nbytes = 256 << 20
+    nbytes = int(os.environ.get("SHIFT_PROBE_BYTES", 256 << 20))
     bs, bd = ctx.alloc(nbytes + 64), ctx.alloc(nbytes + 64)
     rows = []
     for dt, shift in CASES:

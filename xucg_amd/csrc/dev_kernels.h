@@ -134,6 +134,31 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
  * hold bytes of the operand, so they lie in its pages even where they reach
  * past its ends.
  */
+/* XCD-aware tile map for the realigning kernels. A wave of those reads one
+ * line past its own tile (the next tile's first src vector). The dispatcher
+ * deals workgroup b to XCD b % 8 (MI355X_MICROARCH.md, dispatch placement),
+ * so with the identity map that line is the next workgroup's, on another
+ * XCD, and is fetched into two L2s: PMC shows 1/16 more FETCH_SIZE than the
+ * aligned kernel, and the kernel ran 4 points slower. Here XCD x takes chunks
+ * of kXcdChunk consecutive tiles, so the neighbouring tile is processed on
+ * the same XCD one workgroup earlier or later and the line is an L2 hit.
+ * A bijection on [0, ntiles): whole rounds of 8 are remapped, a ragged last
+ * round keeps the identity. */
+constexpr unsigned kXcdChunk = 64;
+
+template <unsigned C>
+__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
+{
+    const unsigned full = ntiles & ~7u;
+    if (b >= full) {
+        return b;
+    }
+    const unsigned T8 = full >> 3, x = b & 7, j = b >> 3;
+    const unsigned R = T8 / C, r = T8 % C;   /* whole chunk rows, remainder */
+    return (j < R * C) ? (j / C) * (8u * C) + x * C + (j % C)
+                       : R * 8u * C + x * r + (j - R * C);
+}
+
 /* lane L gets lane L+1's value (lane 63: undefined, overwritten by the
  * caller). DPP=1: one v_mov_dpp wave_shl:1 (GFX9 whole-wave DPP, kept on
  * CDNA); DPP=0: ds_bpermute through the LDS crossbar. */
@@ -170,7 +195,8 @@ k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
     const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
     u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
     /* the wave's tile: U rows of 64 vectors; lane L holds column L */
-    const size_t base    = (size_t)blockIdx.x * (BS * U) + threadIdx.x;
+    const size_t base    = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * (BS * U) +
+                           threadIdx.x;
     const bool last_lane = threadIdx.x == BS - 1;
     u32x4 lo[U], b[U], ex;
     /* every load in flight before the first wait; lanes past the end load
@@ -252,6 +278,56 @@ k_reduce_shift2(T *dst, const T *src, size_t head, size_t nvec, size_t tail, uns
             sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
         }
         st16<1>(d4 + i, vapply<T, OP>(sv, b));
+    }
+}
+
+/* A/B variant of k_reduce_shift (U = 1) with other chunk sizes C of the
+ * XCD-aware tile map (see xcd_tile; C = 0: one contiguous eighth per XCD);
+ * the product uses kXcdChunk. */
+template <typename T, int OP, int Q, int C>
+__global__ void __launch_bounds__(kReduceBlock)
+k_reduce_shift_xcd(T *dst, const T *src, size_t head, size_t nvec, size_t tail, unsigned rb)
+{
+    constexpr int V   = 16 / sizeof(T);
+    const size_t gtid = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+    if (gtid < head) {
+        dst[gtid] = Comb<T, OP>::apply(src[gtid], dst[gtid]);
+    }
+    if (gtid < tail) {
+        const size_t j = head + nvec * V + gtid;
+        dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
+    }
+    /* C = 0: one contiguous eighth per XCD (a chunk of all its tiles) */
+    const unsigned tile  = C ? xcd_tile<C>(blockIdx.x, gridDim.x)
+                             : xcd_tile<0x7fffffff>(blockIdx.x, gridDim.x);
+    const size_t i       = (size_t)tile * kReduceBlock + threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    const char *sp  = reinterpret_cast<const char*>(src + head);
+    const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
+    if (nvec == 0) {
+        return;
+    }
+    const u32x4 b4 = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
+    const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
+    const u32x4 ex = ld16<1>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 hi;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        hi[k] = from_next_lane<0>(lo[k]);
+    }
+    if (last_lane) {
+        hi = ex;
+    }
+    if (i < nvec) {
+        const uint32_t w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        u32x4 sv;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
+        }
+        st16<1>(d4 + i, vapply<T, OP>(sv, b4));
     }
 }
 
@@ -408,7 +484,8 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
     }
 
     u32x4 *d4            = reinterpret_cast<u32x4*>(dst + head);
-    const size_t i       = gtid;
+    const size_t i       = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                           threadIdx.x;
     const bool last_lane = threadIdx.x == kReduceBlock - 1;
     const u32x4 *a4[N];
     unsigned r[N];

@@ -127,6 +127,24 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
         /* operands disagree mod 16 B: src realigned in registers */
         const unsigned r = (unsigned)((ms + 16 - md) & 15);
         if constexpr (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM) {
+            if (variant >= 9 && variant <= 12 && r == 4 && nvec < kMaxVecPerLaunch) {
+                /* A/B: XCD-aware tile maps for the realigning kernel */
+                const unsigned g = grid_for(nvec > head ? nvec : head, kReduceBlock,
+                                            0x7fffffff);
+                if (variant == 9)
+                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 0>), dim3(g),
+                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
+                else if (variant == 10)
+                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 2048>), dim3(g),
+                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
+                else if (variant == 11)
+                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 64>), dim3(g),
+                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
+                else
+                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 128>), dim3(g),
+                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
+                return hipGetLastError();
+            }
             if (variant >= 5 && variant <= 8 && r == 4) {
                 /* A/B: U = 2 or 4 vectors per lane (one extra load per 64 U),
                  * the DPP lane shift instead of ds_bpermute, or every lane

@@ -388,7 +388,7 @@ int main(int argc, char **argv)
         vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
             unsigned g = (unsigned)((nv + 63) / 64);
 #define XC(A) if (C == A) hipLaunchKernelGGL((k_xcd<A>), dim3(g), dim3(64), 0, q, d, s, nv, g)
-            XC(0); XC(32); XC(256); XC(2048);
+            XC(0); XC(16); XC(32); XC(64); XC(128); XC(256); XC(2048);
 #undef XC
         }, {}});
     };
@@ -408,7 +408,10 @@ int main(int argc, char **argv)
     }
     if (getenv("TUNE_XCD_ONLY")) {
         xcd(0);
+        xcd(16);
         xcd(32);
+        xcd(64);
+        xcd(128);
         xcd(256);
         xcd(2048);
         goto run;
