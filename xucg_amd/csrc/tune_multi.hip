@@ -58,6 +58,44 @@ k_multi_var(float *dst, SrcList srcs, unsigned self, size_t nvec)
     }
 }
 
+/* store policy and persistent-grid A/B: NTS = non-temporal store; G > 0:
+ * a grid of G workgroups looping over the tiles (tile b, b + G, ...) */
+template <int NTS>
+__global__ void __launch_bounds__(64)
+k_multi_loop(float *dst, SrcList srcs, unsigned self, size_t nvec, unsigned loop)
+{
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    const size_t step = loop ? (size_t)gridDim.x * 64 : nvec;
+    for (size_t i = (size_t)blockIdx.x * 64 + threadIdx.x; i < nvec; i += step) {
+        u32x4 val[N];
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            val[m] = ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ m]) + i);
+        }
+        st16<NTS>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val, fv));
+    }
+}
+
+/* ceiling probe: the same N loads, no combine and a store only where the
+ * (never true) data test passes, so the loads cannot be dropped */
+template <int BS>
+__global__ void __launch_bounds__(BS)
+k_multi_readonly(float *dst, SrcList srcs, unsigned self, size_t nvec)
+{
+    const size_t i = (size_t)blockIdx.x * BS + threadIdx.x;
+    if (i >= nvec) {
+        return;
+    }
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        acc ^= ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ m]) + i);
+    }
+    if (acc[0] == 0x7fc00123u && acc[1] == 0x7fc00321u) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, acc);
+    }
+}
+
 struct Variant {
     std::string name;
     std::function<void(float*, SrcList, size_t, hipStream_t)> run;
@@ -111,6 +149,45 @@ int main(int argc, char **argv)
     VAR(1, 64, 0, 0);
     VAR(4, 64, 1, 0);
 #undef VAR
+    vs.push_back({"temporal stores (U1 BS64)", [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_multi_loop<0>), dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, q,
+                           d, s, 0u, nv, 0u);
+    }, {}});
+    for (unsigned w : {4u, 8u, 16u, 32u}) {
+        vs.push_back({"persistent grid 256 CUs x " + std::to_string(w) + " waves, NT stores",
+                      [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+            hipLaunchKernelGGL((k_multi_loop<1>), dim3(256 * w), dim3(64), 0, q, d, s, 0u, nv, 1u);
+        }, {}});
+    }
+    /* the operands at staggered offsets inside one allocation: operand m at
+     * m * (S + pad); tests whether N streams at equal offsets of 2^k-sized
+     * buffers collide in the HBM channel/bank map */
+    std::vector<char*> stag;
+    for (size_t pad : {(size_t)4096, (size_t)65536, (size_t)(1 << 20) + 4096, (size_t)(2 << 20) + 256 * 1024 + 4096}) {
+        char *big;
+        CHECK(hipMalloc(&big, N * (n * 4 + pad)));
+        stag.push_back(big);
+        SrcList ss;
+        for (int m = 0; m < kMaxMulti; m++) {
+            ss.p[m] = nullptr;
+        }
+        for (int m = 0; m < N; m++) {
+            ss.p[m] = big + m * (n * 4 + pad);
+            CHECK(hipMemcpy(const_cast<void*>(ss.p[m]), bufs[m], n * 4, hipMemcpyDeviceToDevice));
+        }
+        vs.push_back({"product kernel, operands staggered by S+" + std::to_string(pad),
+                      [=](float *d, SrcList, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
+            hipLaunchKernelGGL((k_reduce_multi<float, 0, N>), dim3(g), dim3(kReduceBlock), 0, q,
+                               d, ss, 0u, (size_t)0, nv, (size_t)0);
+        }, {}});
+    }
+    const size_t nvariants_checked = vs.size();
+    vs.push_back({"ceiling: read the N operands, no store (N*S bytes)",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        unsigned g = (unsigned)((nv + 63) / 64);
+        hipLaunchKernelGGL((k_multi_readonly<64>), dim3(g), dim3(64), 0, q, d, s, 0u, nv);
+    }, {}});
 
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
@@ -119,7 +196,8 @@ int main(int argc, char **argv)
     CHECK(hipStreamSynchronize(st));
     std::vector<float> hr(n), ho(n);
     CHECK(hipMemcpy(hr.data(), ref, n * 4, hipMemcpyDeviceToHost));
-    for (auto &v : vs) {
+    for (size_t k = 0; k < nvariants_checked; k++) {
+        auto &v = vs[k];
         CHECK(hipMemset(out, 0, n * 4));
         v.run(out, srcs, nvec, st);
         CHECK(hipStreamSynchronize(st));
@@ -149,8 +227,9 @@ int main(int argc, char **argv)
     for (auto &v : vs) {
         std::sort(v.ms.begin(), v.ms.end());
         float med = v.ms[v.ms.size() / 2];
-        printf("%-48s median %8.2f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", v.name.c_str(),
-               med * 1e3, bytes / (med * 1e-3) / 1e9, 100.0 * bytes / (med * 1e-3) / 8e12);
+        const double b = v.name.rfind("ceiling", 0) == 0 ? bytes * N / (N + 1) : bytes;
+        printf("%-56s median %8.2f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", v.name.c_str(),
+               med * 1e3, b / (med * 1e-3) / 1e9, 100.0 * b / (med * 1e-3) / 8e12);
     }
     return 0;
 }
