@@ -2,6 +2,8 @@
 """Roofline of the combine when src and dst disagree mod 16 B: the shuffle
 kernel (k_reduce_shift, product) against the element loop it replaced
 (k_reduce_scalar, UCX_BUILTIN_DEV_VARIANT=4) and the aligned kernel, 256 MiB
+(SHIFT_PROBE_BYTES), then the 8-operand one-shot and tree fan-in kernels with
+operands in and out of dst's phase, 64 MiB
 per operand, 3N algorithmic bytes, HIP events on the context stream (20 warm
 launches, median of 5 batches of 20). Run once per variant:
 
@@ -55,23 +57,30 @@ def main():
     for name, offs in (("aligned", [0] * 8), ("one_operand_4B", [4] + [0] * 7),
                        ("all_phases", [0, 4, 8, 12, 4, 8, 12, 0])):
         srcs = [b.ptr + o for b, o in zip(bufs, offs)]
-        ctx.reduce_multi("sum", "float32", out8.ptr, srcs, 0, n8)
-        ctx.sync()
-        import time
-        reps = 20
-        t = []
-        for _ in range(5):
-            t0 = time.perf_counter()
-            for _ in range(reps):
-                ctx.reduce_multi("sum", "float32", out8.ptr, srcs, 0, n8)
+        for kernel in ("reduce_multi", "reduce_tree"):
+            if kernel == "reduce_multi":
+                def call():
+                    return ctx.reduce_multi("sum", "float32", out8.ptr, srcs, 0, n8)
+            else:
+                def call():
+                    return ctx.reduce_tree("sum", "float32", out8.ptr, srcs, n8)
+            assert call() == 0, _lib.last_error()
             ctx.sync()
-            t.append((time.perf_counter() - t0) / reps * 1e6)
-        us = sorted(t)[2]
-        gbs = 9 * n8 * 4 / (us * 1e-6) / 1e9
-        row = {"kernel": "reduce_multi", "nsrc": 8, "case": name, "variant": variant,
-               "us": round(us, 2), "gbs": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
-        print(row, flush=True)
-        rows.append(row)
+            import time
+            reps = 20
+            t = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                for _ in range(reps):
+                    call()
+                ctx.sync()
+                t.append((time.perf_counter() - t0) / reps * 1e6)
+            us = sorted(t)[2]
+            gbs = 9 * n8 * 4 / (us * 1e-6) / 1e9
+            row = {"kernel": kernel, "nsrc": 8, "case": name, "variant": variant,
+                   "us": round(us, 2), "gbs": round(gbs, 1), "frac": round(gbs / PEAK, 4)}
+            print(row, flush=True)
+            rows.append(row)
     for b in bufs + [out8]:
         b.free()
     # spot parity on a small misaligned case vs a host restatement of fp32 sum

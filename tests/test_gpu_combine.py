@@ -479,6 +479,59 @@ def test_random_multi_cases_against_oracle(dev_ctx):
             b.free()
 
 
+# vector counts (fp32, 64 vectors per tile) that reach every branch of the
+# realigning kernels' XCD-aware tile map (dev_kernels.h xcd_tile, chunks of 64
+# tiles per XCD): whole chunk rows only, chunk rows plus a remainder row, a
+# ragged last round of < 8 tiles, a ragged last tile, fewer than 8 tiles
+XCD_NVECS = [3, 7 * 64 + 5, 512 * 64, 1677 * 64 - 34, (8 * 64 * 5 + 8 * 13 + 3) * 64,
+             (8 * 64 * 2) * 64 + 1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["reduce", "multi", "tree"])
+def test_realigning_kernels_xcd_tile_map(dev_ctx, kernel):
+    """The realigning kernels (k_reduce_shift, k_reduce_multi_shift,
+    k_reduce_tree_shift) remap workgroups to tiles so that neighbouring tiles
+    share an XCD's L2. The map must be a bijection on the tiles for every grid
+    size: each count here is checked element for element against the oracle,
+    with the first operand 4 B out of dst's phase and a ragged head and tail."""
+    dt, st = "float32", np.float32
+    n_ops = {"reduce": 2, "multi": 4, "tree": 5}[kernel]
+    cap = max(XCD_NVECS) * 16 + 256
+    bufs = [dev_ctx.alloc(cap) for _ in range(n_ops + 1)]
+    try:
+        for nvec in XCD_NVECS:
+            count = nvec * 4 + 3 + 2          # dst 8 B into a vector: head 2, tail 3
+            xs = [O.fill(dt, "round", 300 + nvec % 997 + r, count) for r in range(n_ops)]
+            offs = [12] + [8] * (n_ops - 1)   # dst at 8: operand 0 out of phase
+            for r in range(n_ops):
+                bufs[r].upload(xs[r], offs[r])
+            out = bufs[n_ops]
+            if kernel == "reduce":
+                # dst is operand 1, in place
+                rc = dev_ctx.reduce("sum", dt, bufs[1].ptr + 8, bufs[0].ptr + 12, count)
+                want = O.reduce("sum", dt, xs[0], xs[1])
+                where = (bufs[1], 8)
+            elif kernel == "multi":
+                rc = dev_ctx.reduce_multi("sum", dt, out.ptr + 8,
+                                          [b.ptr + o for b, o in zip(bufs, offs)], 2, count)
+                want = O.reduce_multi("sum", dt, xs, 2)
+                where = (out, 8)
+            else:
+                rc = dev_ctx.reduce_tree("sum", dt, out.ptr + 8,
+                                         [b.ptr + o for b, o in zip(bufs, offs)], count)
+                want = O.tree_reduce("sum", dt, xs, root=0)
+                where = (out, 8)
+            assert rc == 0, _lib.last_error()
+            dev_ctx.sync()
+            got = where[0].download(st, count, where[1])
+            bad = np.flatnonzero(O.bits(got) != O.bits(want))
+            assert bad.size == 0, (kernel, nvec, bad[:8])
+    finally:
+        for b in bufs:
+            b.free()
+
+
 @pytest.mark.gpu
 def test_random_tree_cases_against_oracle(dev_ctx):
     """Fuzz of the tree fan-in kernel: random n in 1..16, dtype/op, count and

@@ -298,8 +298,7 @@ k_reduce_shift_xcd(T *dst, const T *src, size_t head, size_t nvec, size_t tail, 
         dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
     }
     /* C = 0: one contiguous eighth per XCD (a chunk of all its tiles) */
-    const unsigned tile  = C ? xcd_tile<C>(blockIdx.x, gridDim.x)
-                             : xcd_tile<0x7fffffff>(blockIdx.x, gridDim.x);
+    const unsigned tile  = xcd_tile<C ? C : 0x7fffffffu>(blockIdx.x, gridDim.x);
     const size_t i       = (size_t)tile * kReduceBlock + threadIdx.x;
     const bool last_lane = threadIdx.x == kReduceBlock - 1;
     const char *sp  = reinterpret_cast<const char*>(src + head);
@@ -578,7 +577,89 @@ k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t
     }
 }
 
-/* the tree fan-in when some operand is out of dst's 16-B phase */
+/*
+ * k_reduce_tree when some operand disagrees with dst mod 16 B (a child's
+ * fragment or buffer at another offset). Operands are read in aligned 16-B
+ * vectors and realigned in registers as in k_reduce_multi_shift, each with
+ * its own uniform phase, on the same XCD-aware tile map; the association is
+ * k_reduce_tree's (acc = srcs[m] (op) acc, m = 1 .. n-1), so the same bits.
+ * Operands past n load srcs[0] again and are not combined.
+ */
+template <typename T, int OP, int NMAX>
+__global__ void __launch_bounds__(kReduceBlock)
+k_reduce_tree_shift(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
+{
+    constexpr int V   = 16 / sizeof(T);
+    const size_t gtid = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
+
+    if (gtid < head || gtid < tail) {
+#pragma unroll
+        for (int part = 0; part < 2; part++) {
+            size_t j;
+            if (part == 0) {
+                if (gtid >= head) continue;
+                j = gtid;
+            } else {
+                if (gtid >= tail) continue;
+                j = head + nvec * V + gtid;
+            }
+            T acc = static_cast<const T*>(srcs.p[0])[j];
+            for (unsigned m = 1; m < n; m++) {
+                acc = Comb<T, OP>::apply(static_cast<const T*>(srcs.p[m])[j], acc);
+            }
+            dst[j] = acc;
+        }
+    }
+    if (nvec == 0) {
+        return;
+    }
+
+    u32x4 *d4            = reinterpret_cast<u32x4*>(dst + head);
+    const size_t i       = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                           threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    const u32x4 *a4[NMAX];
+    unsigned r[NMAX];
+    u32x4 val[NMAX], ex[NMAX];
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        const char *p = reinterpret_cast<const char*>(
+            static_cast<const T*>(srcs.p[(unsigned)m < n ? m : 0]) + head);
+        r[m]  = (unsigned)((uintptr_t)p & 15);
+        a4[m] = reinterpret_cast<const u32x4*>(p - r[m]);
+        const size_t lim = nvec - (r[m] == 0);
+        val[m] = ld16<1>(a4[m] + (i < lim ? i : lim));
+        ex[m]  = ld16<1>(a4[m] + (last_lane && i < lim ? i + 1 : lim));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < NMAX; m++) {
+        if ((unsigned)m < n && r[m]) {
+            u32x4 hi;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                hi[k] = from_next_lane<0>(val[m][k]);
+            }
+            if (last_lane) {
+                hi = ex[m];
+            }
+            val[m] = funnel16(val[m], hi, r[m]);
+        }
+    }
+    if (i < nvec) {
+        u32x4 acc = val[0];
+#pragma unroll
+        for (int m = 1; m < NMAX; m++) {
+            if ((unsigned)m < n) {
+                acc = vapply<T, OP>(val[m], acc);
+            }
+        }
+        st16<1>(d4 + i, acc);
+    }
+}
+
+/* the tree fan-in element loop (A/B variant 4 only: what k_reduce_tree_shift
+ * replaced) */
 template <typename T, int OP>
 __global__ void __launch_bounds__(kBlock)
 k_reduce_tree_scalar(T *dst, SrcList srcs, unsigned n, size_t count)

@@ -314,7 +314,7 @@ typedef hipError_t (*tree_fn_t)(void *dst, const SrcList &srcs, unsigned n,
 
 template <typename T, int OP, int NMAX>
 void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nvec,
-                   size_t tail, hipStream_t st)
+                   size_t tail, bool aligned, hipStream_t st)
 {
     constexpr size_t V = 16 / sizeof(T);
     size_t done = 0;
@@ -326,9 +326,20 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
         for (int m = 0; m < kMaxMulti; m++) {
             sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
         }
-        const unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
-        hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX>), dim3(grid), dim3(kReduceBlock), 0,
-                           st, d + off, sl, n, first ? head : 0, chunk, last ? tail : 0);
+        if (aligned) {
+            const unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
+            hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX>), dim3(grid), dim3(kReduceBlock), 0,
+                               st, d + off, sl, n, first ? head : 0, chunk, last ? tail : 0);
+        } else {
+            /* some operand out of phase with dst: realigned in registers */
+            size_t items = chunk;
+            if (first && head > items) items = head;
+            if (last && tail > items) items = tail;
+            const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
+            hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX>), dim3(grid),
+                               dim3(kReduceBlock), 0, st, d + off, sl, n, first ? head : 0,
+                               chunk, last ? tail : 0);
+        }
         done += chunk;
     } while (done < nvec);
 }
@@ -345,7 +356,8 @@ hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
         aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
     }
     T *d = static_cast<T*>(dst);
-    if (!aligned) {
+    if (!aligned && launch_variant() == 4) {
+        /* A/B only: the element loop the realigning kernel replaced */
         const unsigned grid = grid_for(count, kBlock, launch_max_blocks());
         hipLaunchKernelGGL((k_reduce_tree_scalar<T, OP>), dim3(grid), dim3(kBlock), 0, st,
                            d, srcs, n, count);
@@ -357,11 +369,11 @@ hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
     if (n <= 4) {
-        launch_tree_n<T, OP, 4>(d, srcs, n, head, nvec, tail, st);
+        launch_tree_n<T, OP, 4>(d, srcs, n, head, nvec, tail, aligned, st);
     } else if (n <= 8) {
-        launch_tree_n<T, OP, 8>(d, srcs, n, head, nvec, tail, st);
+        launch_tree_n<T, OP, 8>(d, srcs, n, head, nvec, tail, aligned, st);
     } else {
-        launch_tree_n<T, OP, 16>(d, srcs, n, head, nvec, tail, st);
+        launch_tree_n<T, OP, 16>(d, srcs, n, head, nvec, tail, aligned, st);
     }
     return hipGetLastError();
 }
