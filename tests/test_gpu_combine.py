@@ -320,10 +320,11 @@ def test_max_size_operands(dev_ctx, dt, count, multi):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nsrc,shard,offset", [(1, 4096, 0), (4, 1 << 20, 0), (8, 100_000, 0),
-                                               (16, 4099, 0), (3, 65536, 4), (8, 33, 1)])
+                                               (16, 4099, 0), (3, 65536, 4), (8, 33, 1),
+                                               (1, 4099, 0), (1, 7, 0), (1, (1 << 20) + 9, 0)])
 def test_gather_multi(dev_ctx, nsrc, shard, offset):
     """One-shot all-gather copy: dst[r * shard:] = srcs[r][:shard] (vector path
-    for 16-B aligned rows, byte path otherwise); then again with one row's
+    when every row starts on 16 B, whatever its length, byte path otherwise); then again with one row's
     source NULL (a member's own shard), which must stay untouched."""
     srcs = [np.frombuffer(np.random.default_rng(r).bytes(shard), np.uint8) for r in range(nsrc)]
     bufs = [dev_ctx.alloc(shard + 16) for _ in range(nsrc)]
@@ -358,7 +359,8 @@ def test_gather_multi(dev_ctx, nsrc, shard, offset):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,nbytes,offset", [(1, 4096, 0), (7, 1 << 20, 0), (16, 100_000, 0),
-                                             (5, 4099, 0), (3, 65536, 4), (8, 33, 1)])
+                                             (5, 4099, 0), (3, 65536, 4), (8, 33, 1),
+                                             (4, 15, 0), (2, (1 << 20) + 7, 0)])
 def test_copy_multi(dev_ctx, n, nbytes, offset):
     """n independent copies in one launch; sources repeat (pairs 0 and 1 read
     the same source, as the push all-gather's broadcast does)."""

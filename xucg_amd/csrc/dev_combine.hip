@@ -585,13 +585,18 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
         return UCS_OK;
     }
     SrcList list;
-    bool aligned = ((uintptr_t)dst % 16) == 0 && shard_bytes % 16 == 0;  /* rows too */
+    /* the vector kernel needs every live row's source and destination on a
+     * 16-B boundary; a ragged row length is fine (its tail rides with the
+     * row's first workgroup), so the last, shorter shard of a shard_bounds
+     * layout takes it too */
+    bool aligned = true;
     unsigned live = 0;
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
         if (i < nsrc && srcs[i] != nullptr) {
             live++;
-            aligned = aligned && ((uintptr_t)srcs[i] % 16) == 0;
+            aligned = aligned && ((uintptr_t)srcs[i] % 16) == 0 &&
+                      ((uintptr_t)dst + (uintptr_t)i * shard_bytes) % 16 == 0;
         }
     }
     if (live == 0) {
@@ -638,7 +643,8 @@ struct PairList {
     const void *s[kMaxMulti];
 };
 
-/* one 16-B vector per lane of pair (wg % n), as k_gather_multi */
+/* one 16-B vector per lane of pair (wg % n), as k_gather_multi; a ragged
+ * tail (< 16 B) is copied by the pair's first workgroup */
 static __global__ void __launch_bounds__(kReduceBlock)
 k_copy_multi(PairList pl, unsigned n, size_t nbytes)
 {
@@ -651,6 +657,10 @@ k_copy_multi(PairList pl, unsigned n, size_t nbytes)
     if (i < nvec) {
         st16<1>(reinterpret_cast<u32x4*>(out) + i,
                 ld16<1>(reinterpret_cast<const u32x4*>(src) + i));
+    }
+    const size_t tail = nbytes - nvec * 16;
+    if (wg == 0 && threadIdx.x < tail) {
+        out[nvec * 16 + threadIdx.x] = src[nvec * 16 + threadIdx.x];
     }
 }
 
@@ -680,7 +690,7 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
         return UCS_OK;
     }
     PairList pl;
-    bool aligned = nbytes % 16 == 0;
+    bool aligned = true;   /* pointers on 16 B; any length */
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         pl.d[i] = (i < n) ? dsts[i] : nullptr;
         pl.s[i] = (i < n) ? srcs[i] : nullptr;
@@ -708,9 +718,11 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
                 c.d[i] = static_cast<char*>(pl.d[i]) + done * 16;
                 c.s[i] = static_cast<const char*>(pl.s[i]) + done * 16;
             }
-            const size_t grid = div_up(chunk, kReduceBlock) * n;
+            /* the tail rides with the last dispatch */
+            const size_t len  = (done + chunk == nvec) ? nbytes - done * 16 : chunk * 16;
+            const size_t grid = div_up(chunk ? chunk : 1, kReduceBlock) * n;
             hipLaunchKernelGGL(k_copy_multi, dim3((unsigned)grid), dim3(kReduceBlock), 0,
-                               ctx->stream, c, n, chunk * 16);
+                               ctx->stream, c, n, len);
             done += chunk;
         } while (done < nvec);
     }
