@@ -358,9 +358,41 @@ def test_gather_multi(dev_ctx, nsrc, shard, offset):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("nsrc,shard,offset", [(2, 4099, 0), (8, 33, 5), (5, (1 << 20) + 3, 12),
+                                               (16, 100_003, 7), (3, 15, 9)])
+def test_gather_multi_phase_matched_rows(dev_ctx, nsrc, shard, offset):
+    """Rows of a ragged length, each source placed in its destination row's
+    16-B phase (the one-shot all-gather over buffers at one common offset):
+    the vector kernel with per-row byte heads and tails. Guard bytes on both
+    sides of the output must stay untouched."""
+    srcs = [np.frombuffer(np.random.default_rng(40 + r).bytes(shard), np.uint8)
+            for r in range(nsrc)]
+    phase = [(offset + r * shard) % 16 for r in range(nsrc)]
+    bufs = [dev_ctx.alloc(shard + 32) for _ in range(nsrc)]
+    out = dev_ctx.alloc(nsrc * shard + 64)
+    try:
+        for b, s_, ph in zip(bufs, srcs, phase):
+            b.upload(s_, ph)
+        out.upload(np.full(nsrc * shard + 64, 0x5A, np.uint8))
+        rc = dev_ctx.gather_multi(out.ptr + 16 + offset,
+                                  [b.ptr + ph for b, ph in zip(bufs, phase)], shard)
+        assert rc == 0, _lib.last_error()
+        dev_ctx.sync()
+        raw = out.download(np.uint8, nsrc * shard + 64)
+        got = raw[16 + offset:16 + offset + nsrc * shard]
+        assert (got == np.concatenate(srcs)).all()
+        assert (raw[:16 + offset] == 0x5A).all() and (raw[16 + offset + nsrc * shard:] == 0x5A).all()
+    finally:
+        for b in bufs:
+            b.free()
+        out.free()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,nbytes,offset", [(1, 4096, 0), (7, 1 << 20, 0), (16, 100_000, 0),
                                              (5, 4099, 0), (3, 65536, 4), (8, 33, 1),
-                                             (4, 15, 0), (2, (1 << 20) + 7, 0)])
+                                             (4, 15, 0), (2, (1 << 20) + 7, 0), (5, 4099, 7),
+                                             (3, 100_001, 13)])
 def test_copy_multi(dev_ctx, n, nbytes, offset):
     """n independent copies in one launch; sources repeat (pairs 0 and 1 read
     the same source, as the push all-gather's broadcast does)."""

@@ -524,13 +524,39 @@ ucs_status_t ucg_builtin_dev_reduce_tree(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_
 }
 
 /* ---- one-shot all-gather ------------------------------------------------ */
+/* one row (or pair) of bytes whose source and destination share a 16-B
+ * phase: the head bytes up to the first 16-B boundary of `out` and the tail
+ * (< 16 B each) by the first lanes of workgroup 0 of the row, the rest in
+ * 16-B vectors, lane i of workgroup wg taking vector wg * 64 + i */
+__device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbytes, size_t wg)
+{
+    size_t head = (16 - ((uintptr_t)out & 15)) & 15;
+    head = head < nbytes ? head : nbytes;
+    const size_t nvec = (nbytes - head) / 16;
+    const size_t i    = wg * kReduceBlock + threadIdx.x;
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(out + head) + i,
+                ld16<1>(reinterpret_cast<const u32x4*>(src + head) + i));
+    }
+    if (wg == 0) {
+        const size_t tail = nbytes - head - nvec * 16;
+        if (threadIdx.x < head) {
+            out[threadIdx.x] = src[threadIdx.x];
+        }
+        if (threadIdx.x < tail) {
+            const size_t j = head + nvec * 16 + threadIdx.x;
+            out[j] = src[j];
+        }
+    }
+}
+
 /* 16-B vectors of every source (one wave per workgroup, non-temporal, like
  * the combine). Workgroups are dealt round-robin over the sources
  * (r = wg % nsrc): the dispatcher hands out workgroup ids in order, so a
  * source-major grid (one grid row per source) would read one peer at a time
  * and keep one xGMI link busy; dealt round-robin, every link streams at once.
- * The ragged tail of a shard (< 16 B) is copied byte-wise by the first lanes
- * of the source's first workgroup. */
+ * Every live row's source shares its destination's 16-B phase (checked by the
+ * caller); ragged heads and tails are copied byte-wise (copy_row). */
 static __global__ void __launch_bounds__(kReduceBlock)
 k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
                size_t nbytes)
@@ -541,21 +567,11 @@ k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
     if (src == nullptr) {
         return;                   /* row left in place (uniform per workgroup) */
     }
-    char *out         = dst + (size_t)r * row_stride;
-    const size_t nvec = nbytes / 16;
-    const size_t i    = wg * kReduceBlock + threadIdx.x;
-    if (i < nvec) {
-        st16<1>(reinterpret_cast<u32x4*>(out) + i,
-                ld16<1>(reinterpret_cast<const u32x4*>(src) + i));
-    }
-    const size_t tail = nbytes - nvec * 16;
-    if (wg == 0 && threadIdx.x < tail) {
-        out[nvec * 16 + threadIdx.x] = src[nvec * 16 + threadIdx.x];
-    }
+    copy_row(dst + (size_t)r * row_stride, src, nbytes, wg);
 }
 
-/* unaligned sources or destinations: byte-wise, grid-stride, workgroups
- * dealt round-robin over the sources as above */
+/* a row whose source and destination disagree mod 16 B: byte-wise,
+ * grid-stride, workgroups dealt round-robin over the sources as above */
 static __global__ void __launch_bounds__(kBlock)
 k_gather_multi_bytes(char *dst, SrcList srcs, unsigned nsrc, size_t shard_bytes)
 {
@@ -585,18 +601,19 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
         return UCS_OK;
     }
     SrcList list;
-    /* the vector kernel needs every live row's source and destination on a
-     * 16-B boundary; a ragged row length is fine (its tail rides with the
-     * row's first workgroup), so the last, shorter shard of a shard_bounds
-     * layout takes it too */
+    /* the vector kernel needs every live row's source in its destination's
+     * 16-B phase (buffers at the same offset on every member, whatever the
+     * offset); ragged heads and row lengths are copied byte-wise by the
+     * row's first workgroup */
     bool aligned = true;
     unsigned live = 0;
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
         if (i < nsrc && srcs[i] != nullptr) {
             live++;
-            aligned = aligned && ((uintptr_t)srcs[i] % 16) == 0 &&
-                      ((uintptr_t)dst + (uintptr_t)i * shard_bytes) % 16 == 0;
+            aligned = aligned &&
+                      (((uintptr_t)srcs[i] ^ ((uintptr_t)dst + (uintptr_t)i * shard_bytes)) &
+                       15) == 0;
         }
     }
     if (live == 0) {
@@ -643,25 +660,13 @@ struct PairList {
     const void *s[kMaxMulti];
 };
 
-/* one 16-B vector per lane of pair (wg % n), as k_gather_multi; a ragged
- * tail (< 16 B) is copied by the pair's first workgroup */
+/* pair (wg % n) copied as a row of k_gather_multi (copy_row) */
 static __global__ void __launch_bounds__(kReduceBlock)
 k_copy_multi(PairList pl, unsigned n, size_t nbytes)
 {
-    const unsigned r  = blockIdx.x % n;
-    const size_t wg   = blockIdx.x / n;
-    const char *src   = static_cast<const char*>(pl.s[r]);
-    char *out         = static_cast<char*>(pl.d[r]);
-    const size_t nvec = nbytes / 16;
-    const size_t i    = wg * kReduceBlock + threadIdx.x;
-    if (i < nvec) {
-        st16<1>(reinterpret_cast<u32x4*>(out) + i,
-                ld16<1>(reinterpret_cast<const u32x4*>(src) + i));
-    }
-    const size_t tail = nbytes - nvec * 16;
-    if (wg == 0 && threadIdx.x < tail) {
-        out[nvec * 16 + threadIdx.x] = src[nvec * 16 + threadIdx.x];
-    }
+    const unsigned r = blockIdx.x % n;
+    copy_row(static_cast<char*>(pl.d[r]), static_cast<const char*>(pl.s[r]), nbytes,
+             blockIdx.x / n);
 }
 
 static __global__ void __launch_bounds__(kBlock)
@@ -690,7 +695,7 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
         return UCS_OK;
     }
     PairList pl;
-    bool aligned = true;   /* pointers on 16 B; any length */
+    bool aligned = true;   /* every pair in one 16-B phase; any length */
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         pl.d[i] = (i < n) ? dsts[i] : nullptr;
         pl.s[i] = (i < n) ? srcs[i] : nullptr;
@@ -698,8 +703,7 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
             if (dsts[i] == nullptr || srcs[i] == nullptr) {
                 return set_error(UCS_ERR_INVALID_PARAM, "copy_multi", "NULL pointer");
             }
-            aligned = aligned && ((uintptr_t)dsts[i] % 16) == 0 &&
-                      ((uintptr_t)srcs[i] % 16) == 0;
+            aligned = aligned && (((uintptr_t)dsts[i] ^ (uintptr_t)srcs[i]) & 15) == 0;
         }
     }
     if (!aligned) {
