@@ -389,6 +389,43 @@ def test_gather_multi_phase_matched_rows(dev_ctx, nsrc, shard, offset):
 
 
 @pytest.mark.gpu
+def test_row_copy_every_phase_pair(dev_ctx):
+    """The row copy behind gather_multi and copy_multi for every (source
+    phase, destination phase) pair mod 16 B and lengths around the head,
+    tail and wave boundaries: in phase it is the vector path with byte heads
+    and tails, out of phase the realigning path (aligned loads, next-lane
+    shuffle, funnel shift). Guard bytes around the output stay untouched;
+    the source sits flush with the end of its allocation once per case."""
+    lens = [1, 15, 16, 17, 1023, 1024 + 5, 64 * 16 * 3 + 7, 100_003]
+    cap = max(lens) + 64
+    sb, db = dev_ctx.alloc(cap), dev_ctx.alloc(cap + 64)
+    rng = np.random.default_rng(77)
+    try:
+        for nb in lens:
+            data = np.frombuffer(rng.bytes(nb), np.uint8)
+            for sp in range(16):
+                for dp in range(16):
+                    for at_end in (False, True):
+                        so = ((cap - nb - sp) // 16) * 16 + sp if at_end else sp
+                        sb.upload(data, so)
+                        db.upload(np.full(cap + 64, 0xC3, np.uint8))
+                        do = 16 + dp
+                        if (sp + dp + nb) % 2:
+                            rc = dev_ctx.gather_multi(db.ptr + do, [sb.ptr + so], nb)
+                        else:
+                            rc = dev_ctx.copy_multi([db.ptr + do], [sb.ptr + so], nb)
+                        assert rc == 0, _lib.last_error()
+                        dev_ctx.sync()
+                        raw = db.download(np.uint8, cap + 64)
+                        assert (raw[do:do + nb] == data).all(), (nb, sp, dp, at_end)
+                        assert (raw[:do] == 0xC3).all() and (raw[do + nb:] == 0xC3).all(), \
+                            (nb, sp, dp, at_end, "guard bytes overwritten")
+    finally:
+        sb.free()
+        db.free()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("n,nbytes,offset", [(1, 4096, 0), (7, 1 << 20, 0), (16, 100_000, 0),
                                              (5, 4099, 0), (3, 65536, 4), (8, 33, 1),
                                              (4, 15, 0), (2, (1 << 20) + 7, 0), (5, 4099, 7),

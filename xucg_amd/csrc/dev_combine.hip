@@ -524,19 +524,44 @@ ucs_status_t ucg_builtin_dev_reduce_tree(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_
 }
 
 /* ---- one-shot all-gather ------------------------------------------------ */
-/* one row (or pair) of bytes whose source and destination share a 16-B
- * phase: the head bytes up to the first 16-B boundary of `out` and the tail
- * (< 16 B each) by the first lanes of workgroup 0 of the row, the rest in
- * 16-B vectors, lane i of workgroup wg taking vector wg * 64 + i */
+/* one row (or pair) of bytes: the head bytes up to the first 16-B boundary
+ * of `out` and the tail (< 16 B each) by the first lanes of workgroup 0 of
+ * the row, the rest in 16-B vectors, lane i of workgroup wg taking vector
+ * wg * 64 + i. A source out of `out`'s 16-B phase (by rs bytes, uniform per
+ * row) is read in aligned vectors and realigned in registers as in
+ * k_reduce_shift: vector A[i + 1] comes from the next lane (lane 63 loads it
+ * itself), and a funnel shift extracts the bytes under out's vector i.
+ * A[nvec] holds source bytes (rs > 0), so it lies in the source's pages. */
 __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbytes, size_t wg)
 {
     size_t head = (16 - ((uintptr_t)out & 15)) & 15;
     head = head < nbytes ? head : nbytes;
-    const size_t nvec = (nbytes - head) / 16;
-    const size_t i    = wg * kReduceBlock + threadIdx.x;
-    if (i < nvec) {
-        st16<1>(reinterpret_cast<u32x4*>(out + head) + i,
-                ld16<1>(reinterpret_cast<const u32x4*>(src + head) + i));
+    const size_t nvec  = (nbytes - head) / 16;
+    const size_t i     = wg * kReduceBlock + threadIdx.x;
+    const char *sp     = src + head;
+    const unsigned rs  = (unsigned)((uintptr_t)sp & 15);
+    u32x4 *o4          = reinterpret_cast<u32x4*>(out + head);
+    if (rs == 0) {
+        if (i < nvec) {
+            st16<1>(o4 + i, ld16<1>(reinterpret_cast<const u32x4*>(sp) + i));
+        }
+    } else if (nvec != 0) {
+        /* every lane of the wave takes part in the shuffle: clamped loads */
+        const u32x4 *a4      = reinterpret_cast<const u32x4*>(sp - rs);
+        const bool last_lane = threadIdx.x == kReduceBlock - 1;
+        const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
+        const u32x4 ex = ld16<1>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
+        u32x4 hi;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            hi[k] = from_next_lane<0>(lo[k]);
+        }
+        if (last_lane) {
+            hi = ex;
+        }
+        if (i < nvec) {
+            st16<1>(o4 + i, funnel16(lo, hi, rs));
+        }
     }
     if (wg == 0) {
         const size_t tail = nbytes - head - nvec * 16;
@@ -555,8 +580,8 @@ __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbyt
  * (r = wg % nsrc): the dispatcher hands out workgroup ids in order, so a
  * source-major grid (one grid row per source) would read one peer at a time
  * and keep one xGMI link busy; dealt round-robin, every link streams at once.
- * Every live row's source shares its destination's 16-B phase (checked by the
- * caller); ragged heads and tails are copied byte-wise (copy_row). */
+ * Ragged heads and tails are copied byte-wise, and a source out of its
+ * destination's 16-B phase is realigned in registers (copy_row). */
 static __global__ void __launch_bounds__(kReduceBlock)
 k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
                size_t nbytes)
@@ -570,7 +595,7 @@ k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
     copy_row(dst + (size_t)r * row_stride, src, nbytes, wg);
 }
 
-/* a row whose source and destination disagree mod 16 B: byte-wise,
+/* the byte loop the realigning row copy replaced (A/B variant 4 only):
  * grid-stride, workgroups dealt round-robin over the sources as above */
 static __global__ void __launch_bounds__(kBlock)
 k_gather_multi_bytes(char *dst, SrcList srcs, unsigned nsrc, size_t shard_bytes)
@@ -601,10 +626,9 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
         return UCS_OK;
     }
     SrcList list;
-    /* the vector kernel needs every live row's source in its destination's
-     * 16-B phase (buffers at the same offset on every member, whatever the
-     * offset); ragged heads and row lengths are copied byte-wise by the
-     * row's first workgroup */
+    /* any row layout takes the vector kernel (copy_row: byte heads and
+     * tails, out-of-phase sources realigned in registers); the byte loop is
+     * kept as A/B variant 4 for rows out of phase */
     bool aligned = true;
     unsigned live = 0;
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
@@ -616,6 +640,7 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
                        15) == 0;
         }
     }
+    aligned = aligned || launch_variant() != 4;
     if (live == 0) {
         return set_error(UCS_ERR_INVALID_PARAM, "gather_multi", "every source is NULL");
     }
@@ -695,7 +720,7 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
         return UCS_OK;
     }
     PairList pl;
-    bool aligned = true;   /* every pair in one 16-B phase; any length */
+    bool aligned = true;   /* every pair in one 16-B phase */
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         pl.d[i] = (i < n) ? dsts[i] : nullptr;
         pl.s[i] = (i < n) ? srcs[i] : nullptr;
@@ -706,6 +731,7 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
             aligned = aligned && (((uintptr_t)dsts[i] ^ (uintptr_t)srcs[i]) & 15) == 0;
         }
     }
+    aligned = aligned || launch_variant() != 4;   /* byte loop: A/B only */
     if (!aligned) {
         const unsigned grid = grid_for(nbytes, kBlock, 1024) * n;
         hipLaunchKernelGGL(k_copy_multi_bytes, dim3(grid), dim3(kBlock), 0, ctx->stream,
