@@ -389,6 +389,68 @@ def test_gather_multi_phase_matched_rows(dev_ctx, nsrc, shard, offset):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dt", ["int8", "float16", "float32", "float64"])
+def test_line_heads(dev_ctx, dt):
+    """The ragged head runs to dst's next 128-B line (up to 127 B: more
+    lanes than one wave for int8). dst at every element offset within a
+    line, src in phase, 16-B-in-phase but not line-in-phase (the XCD-aware
+    map), and out of phase; counts shorter and longer than the head. Guard
+    bytes around dst stay untouched. Then the multi-operand and tree kernels
+    with dst off a line."""
+    st = O.storage(dt)
+    sz = np.dtype(st).itemsize
+    counts = [1, 63, 64, 65, 127, 128 // sz + 3, 1000, 64 * 64 + 17]
+    cap = max(counts) * sz + 512
+    bs, bd = dev_ctx.alloc(cap), dev_ctx.alloc(cap + 256)
+    try:
+        for count in counts:
+            nb = count * sz
+            src = O.fill(dt, "round", 500 + count, count)
+            dst = O.fill(dt, "round", 600 + count, count)
+            want = O.reduce("sum", dt, src, dst)
+            for doff in range(0, 128, sz if sz > 1 else 7):
+                for delta in (0, 16, 48, 4 * sz if sz < 4 else sz):
+                    soff = (doff + delta) % 128 + 64
+                    do = 128 + doff
+                    bd.upload(np.full(do + nb + 64, 0x3C, np.uint8))
+                    bd.upload(dst, do)
+                    bs.upload(src, soff)
+                    dev_ctx.reduce_checked("sum", dt, bd.ptr + do, bs.ptr + soff, count)
+                    dev_ctx.sync()
+                    raw = bd.download(np.uint8, do + nb + 64)
+                    got = raw[do:do + nb].view(st)
+                    assert (O.bits(got) == O.bits(want)).all(), (count, doff, delta)
+                    assert (raw[:do] == 0x3C).all() and (raw[do + nb:] == 0x3C).all(), \
+                        (count, doff, delta, "guard bytes overwritten")
+    finally:
+        bs.free()
+        bd.free()
+    # multi-operand and tree kernels, dst off a line, sources in its 16-B phase
+    count = 64 * 64 * 3 + 5
+    xs = [O.fill(dt, "round", 700 + r, count) for r in range(4)]
+    bufs = [dev_ctx.alloc(count * sz + 512) for _ in range(5)]
+    try:
+        for doff in (sz, 48, 64 + sz, 112):
+            for r in range(4):
+                bufs[r].upload(xs[r], doff + 16 * (r % 2))
+            ptrs = [bufs[r].ptr + doff + 16 * (r % 2) for r in range(4)]
+            assert dev_ctx.reduce_multi("sum", dt, bufs[4].ptr + doff, ptrs, 1, count) == 0, \
+                _lib.last_error()
+            dev_ctx.sync()
+            got = bufs[4].download(st, count, doff)
+            assert (O.bits(got) == O.bits(O.reduce_multi("sum", dt, xs, 1))).all(), ("multi", doff)
+            assert dev_ctx.reduce_tree("sum", dt, bufs[4].ptr + doff, ptrs, count) == 0, \
+                _lib.last_error()
+            dev_ctx.sync()
+            got = bufs[4].download(st, count, doff)
+            assert (O.bits(got) == O.bits(O.tree_reduce("sum", dt, xs, root=0))).all(), \
+                ("tree", doff)
+    finally:
+        for b in bufs:
+            b.free()
+
+
+@pytest.mark.gpu
 def test_row_copy_every_phase_pair(dev_ctx):
     """The row copy behind gather_multi and copy_multi for every (source
     phase, destination phase) pair mod 16 B and lengths around the head,

@@ -524,8 +524,8 @@ ucs_status_t ucg_builtin_dev_reduce_tree(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_
 }
 
 /* ---- one-shot all-gather ------------------------------------------------ */
-/* one row (or pair) of bytes: the head bytes up to the first 16-B boundary
- * of `out` and the tail (< 16 B each) by the first lanes of workgroup 0 of
+/* one row (or pair) of bytes: the head bytes up to the first 128-B line
+ * of `out` and the tail (< 16 B) by the first lanes of workgroup 0 of
  * the row, the rest in 16-B vectors, lane i of workgroup wg taking vector
  * wg * 64 + i. A source out of `out`'s 16-B phase (by rs bytes, uniform per
  * row) is read in aligned vectors and realigned in registers as in
@@ -534,7 +534,8 @@ ucs_status_t ucg_builtin_dev_reduce_tree(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_
  * A[nvec] holds source bytes (rs > 0), so it lies in the source's pages. */
 __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbytes, size_t wg)
 {
-    size_t head = (16 - ((uintptr_t)out & 15)) & 15;
+    /* the head runs to out's next 128-B line (kLine, dev_launch.h) */
+    size_t head = (kLine - ((uintptr_t)out & (kLine - 1))) & (kLine - 1);
     head = head < nbytes ? head : nbytes;
     const size_t nvec  = (nbytes - head) / 16;
     const size_t i     = wg * kReduceBlock + threadIdx.x;
@@ -565,8 +566,8 @@ __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbyt
     }
     if (wg == 0) {
         const size_t tail = nbytes - head - nvec * 16;
-        if (threadIdx.x < head) {
-            out[threadIdx.x] = src[threadIdx.x];
+        for (size_t j = threadIdx.x; j < head; j += kReduceBlock) {
+            out[j] = src[j];
         }
         if (threadIdx.x < tail) {
             const size_t j = head + nvec * 16 + threadIdx.x;

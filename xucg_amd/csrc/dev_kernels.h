@@ -73,6 +73,31 @@ __device__ __forceinline__ u32x4 vapply(u32x4 s, u32x4 d)
     return o;
 }
 
+/* XCD-aware tile map for the realigning kernels. A wave of those reads one
+ * line past its own tile (the next tile's first src vector). The dispatcher
+ * deals workgroup b to XCD b % 8 (MI355X_MICROARCH.md, dispatch placement),
+ * so with the identity map that line is the next workgroup's, on another
+ * XCD, and is fetched into two L2s: PMC shows 1/16 more FETCH_SIZE than the
+ * aligned kernel, and the kernel ran 4 points slower. Here XCD x takes chunks
+ * of kXcdChunk consecutive tiles, so the neighbouring tile is processed on
+ * the same XCD one workgroup earlier or later and the line is an L2 hit.
+ * A bijection on [0, ntiles): whole rounds of 8 are remapped, a ragged last
+ * round keeps the identity. */
+constexpr unsigned kXcdChunk = 64;
+
+template <unsigned C>
+__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
+{
+    const unsigned full = ntiles & ~7u;
+    if (b >= full) {
+        return b;
+    }
+    const unsigned T8 = full >> 3, x = b & 7, j = b >> 3;
+    const unsigned R = T8 / C, r = T8 % C;   /* whole chunk rows, remainder */
+    return (j < R * C) ? (j / C) * (8u * C) + x * C + (j % C)
+                       : R * 8u * C + x * r + (j - R * C);
+}
+
 /*
  * The streaming combine. One tile of U 16-B vectors per lane (lane stride
  * BS), no loop: the grid is sized to the data (one dispatch covers up to 2^31
@@ -84,7 +109,7 @@ __device__ __forceinline__ u32x4 vapply(u32x4 s, u32x4 d)
  * one-wave workgroups and U = 1 (profiles/r01). The ragged head
  * (until dst is 16-B aligned) and tail (< 16 B) are done by the first lanes.
  */
-template <typename T, int OP, int U, int NT, int BS>
+template <typename T, int OP, int U, int NT, int BS, int XM = 0>
 __global__ void __launch_bounds__(BS)
 k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 {
@@ -102,7 +127,10 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 
     const u32x4 *s4   = reinterpret_cast<const u32x4*>(src + head);
     u32x4 *d4         = reinterpret_cast<u32x4*>(dst + head);
-    const size_t base = (size_t)blockIdx.x * (BS * U) + threadIdx.x;
+    /* XM: the XCD-aware tile map, for a src whose vectors straddle 128-B
+     * lines (its edge lines are then shared with the neighbouring tiles) */
+    const size_t tile = XM ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t base = tile * (BS * U) + threadIdx.x;
     u32x4 a[U], b[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -134,31 +162,6 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
  * hold bytes of the operand, so they lie in its pages even where they reach
  * past its ends.
  */
-/* XCD-aware tile map for the realigning kernels. A wave of those reads one
- * line past its own tile (the next tile's first src vector). The dispatcher
- * deals workgroup b to XCD b % 8 (MI355X_MICROARCH.md, dispatch placement),
- * so with the identity map that line is the next workgroup's, on another
- * XCD, and is fetched into two L2s: PMC shows 1/16 more FETCH_SIZE than the
- * aligned kernel, and the kernel ran 4 points slower. Here XCD x takes chunks
- * of kXcdChunk consecutive tiles, so the neighbouring tile is processed on
- * the same XCD one workgroup earlier or later and the line is an L2 hit.
- * A bijection on [0, ntiles): whole rounds of 8 are remapped, a ragged last
- * round keeps the identity. */
-constexpr unsigned kXcdChunk = 64;
-
-template <unsigned C>
-__device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
-{
-    const unsigned full = ntiles & ~7u;
-    if (b >= full) {
-        return b;
-    }
-    const unsigned T8 = full >> 3, x = b & 7, j = b >> 3;
-    const unsigned R = T8 / C, r = T8 % C;   /* whole chunk rows, remainder */
-    return (j < R * C) ? (j / C) * (8u * C) + x * C + (j % C)
-                       : R * 8u * C + x * r + (j - R * C);
-}
-
 /* lane L gets lane L+1's value (lane 63: undefined, overwritten by the
  * caller). DPP=1: one v_mov_dpp wave_shl:1 (GFX9 whole-wave DPP, kept on
  * CDNA); DPP=0: ds_bpermute through the LDS crossbar. */
@@ -375,7 +378,7 @@ __device__ __forceinline__ E rd_tree(E (&val)[N], F f)
     return val[0];
 }
 
-template <typename T, int OP, int N>
+template <typename T, int OP, int N, int XM = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                size_t tail)
@@ -406,7 +409,8 @@ k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
     }
 
     u32x4 *d4 = reinterpret_cast<u32x4*>(dst + head);
-    const size_t base = (size_t)blockIdx.x * (kReduceBlock * kMultiU) + threadIdx.x;
+    const size_t tile = XM ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t base = tile * (kReduceBlock * kMultiU) + threadIdx.x;
 #pragma unroll
     for (int u = 0; u < kMultiU; u++) {
         const size_t i = base + (size_t)u * kReduceBlock;
@@ -532,7 +536,7 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
  * two, and for MPI_Reduce). Operands past n load srcs[0] again (an L2 hit,
  * no branch between the loads) and are not combined.
  */
-template <typename T, int OP, int NMAX>
+template <typename T, int OP, int NMAX, int XM = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
 {
@@ -558,7 +562,8 @@ k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t
         }
     }
 
-    const size_t i = gtid;
+    const size_t i = (XM ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x) *
+                         kReduceBlock + threadIdx.x;
     if (i < nvec) {
         u32x4 val[NMAX];
 #pragma unroll

@@ -49,7 +49,30 @@ typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
  * in the last. */
 constexpr size_t kMaxVecPerLaunch = (size_t)1 << 31;
 
-template <typename T, int OP, int U, int NT, int BS>
+/* The ragged head ends where dst reaches a 128-B line, not merely 16 B: a
+ * wave stores 64 x 16 B, and a span that starts inside a line shares its
+ * first and last lines with the neighbouring waves (on other XCDs under the
+ * identity block map), so every line at a span edge is written twice, in
+ * halves. Measured (scripts/dst_offset_probe.py): dst and src 16 B past a
+ * line, with 16-B heads, ran at 69 % of 8 TB/s against 84 % on a line. The
+ * head is at most 127 B, done by the first lanes of the grid. */
+constexpr uintptr_t kLine = 128;
+
+template <typename T>
+inline size_t line_head(const void *dst, size_t count)
+{
+    const uintptr_t ml = (uintptr_t)dst & (kLine - 1);
+    const size_t h     = ml ? (kLine - ml) / sizeof(T) : 0;
+    return h < count ? h : count;
+}
+
+/* XCD-aware tile map when a source's vectors straddle lines (see k_reduce) */
+inline bool straddles_lines(const void *p)
+{
+    return ((uintptr_t)p & (kLine - 1)) != 0;
+}
+
+template <typename T, int OP, int U, int NT, int BS, int XM = 0>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
                        hipStream_t st)
 {
@@ -59,9 +82,13 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
         const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
         const bool first = (done == 0), last = (done + chunk == nvec);
         const size_t off = first ? 0 : head + done * V;
-        /* one tile of U vectors per lane: grid sized to the chunk (no loop) */
-        const unsigned grid = grid_for(chunk, (size_t)BS * U, 0x7fffffff);
-        hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS>), dim3(grid), dim3(BS), 0, st,
+        /* one tile of U vectors per lane: grid sized to the chunk (no loop),
+         * and to the head's lanes */
+        unsigned grid = grid_for(chunk, (size_t)BS * U, 0x7fffffff);
+        if (first && div_up(head, BS) > grid) {
+            grid = (unsigned)div_up(head, BS);
+        }
+        hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS, XM>), dim3(grid), dim3(BS), 0, st,
                            d + off, s + off, first ? head : 0, chunk, last ? tail : 0);
         done += chunk;
     } while (done < nvec);
@@ -116,10 +143,7 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
                            0, st, d, s, count);
         return hipGetLastError();
     }
-    size_t head = md ? (16 - md) / sz : 0;
-    if (head > count) {
-        head = count;
-    }
+    const size_t head = line_head<T>(dst, count);
     const size_t rem  = count - head;
     const size_t nvec = rem / V, tail = rem % V;
 
@@ -177,9 +201,14 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
         case 2: launch_vec<T, OP, 1, 1, 256>(d, s, head, nvec, tail, st); break;
         case 3: launch_vec<T, OP, 1, 0, 64>(d, s, head, nvec, tail, st); break;
         default:
-            launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
+            if (straddles_lines(s + head))
+                launch_vec<T, OP, kReduceU, 1, kReduceBlock, 1>(d, s, head, nvec, tail, st);
+            else
+                launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
             break;
         }
+    } else if (straddles_lines(s + head)) {
+        launch_vec<T, OP, kReduceU, 1, kReduceBlock, 1>(d, s, head, nvec, tail, st);
     } else {
         launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
     }
@@ -226,9 +255,10 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
                            dim3(kBlock), 0, st, d, srcs, self, count);
         return hipGetLastError();
     }
-    size_t head = md ? (16 - md) / sz : 0;
-    if (head > count) {
-        head = count;
+    const size_t head = line_head<T>(dst, count);
+    bool xm = false;
+    for (int m = 0; m < N; m++) {
+        xm = xm || straddles_lines(static_cast<const T*>(srcs.p[m]) + head);
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
     size_t done = 0;
@@ -241,10 +271,18 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
         }
         if (aligned) {
-            const unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
-            hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
-                               st, d + off, sl, self, first ? head : 0, chunk,
-                               last ? tail : 0);
+            unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
+            if (first && div_up(head, kReduceBlock) > grid) {
+                grid = (unsigned)div_up(head, kReduceBlock);
+            }
+            if (xm)
+                hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1>), dim3(grid), dim3(kReduceBlock),
+                                   0, st, d + off, sl, self, first ? head : 0, chunk,
+                                   last ? tail : 0);
+            else
+                hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), 0,
+                                   st, d + off, sl, self, first ? head : 0, chunk,
+                                   last ? tail : 0);
         } else {
             /* some operand out of phase with dst: realigned in registers */
             size_t items = chunk;
@@ -314,7 +352,7 @@ typedef hipError_t (*tree_fn_t)(void *dst, const SrcList &srcs, unsigned n,
 
 template <typename T, int OP, int NMAX>
 void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nvec,
-                   size_t tail, bool aligned, hipStream_t st)
+                   size_t tail, bool aligned, bool xm, hipStream_t st)
 {
     constexpr size_t V = 16 / sizeof(T);
     size_t done = 0;
@@ -327,9 +365,18 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
         }
         if (aligned) {
-            const unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
-            hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX>), dim3(grid), dim3(kReduceBlock), 0,
-                               st, d + off, sl, n, first ? head : 0, chunk, last ? tail : 0);
+            unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
+            if (first && div_up(head, kReduceBlock) > grid) {
+                grid = (unsigned)div_up(head, kReduceBlock);
+            }
+            if (xm)
+                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1>), dim3(grid),
+                                   dim3(kReduceBlock), 0, st, d + off, sl, n, first ? head : 0,
+                                   chunk, last ? tail : 0);
+            else
+                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX>), dim3(grid), dim3(kReduceBlock),
+                                   0, st, d + off, sl, n, first ? head : 0, chunk,
+                                   last ? tail : 0);
         } else {
             /* some operand out of phase with dst: realigned in registers */
             size_t items = chunk;
@@ -363,17 +410,18 @@ hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
                            d, srcs, n, count);
         return hipGetLastError();
     }
-    size_t head = md ? (16 - md) / sz : 0;
-    if (head > count) {
-        head = count;
+    const size_t head = line_head<T>(dst, count);
+    bool xm = false;
+    for (unsigned m = 0; m < n; m++) {
+        xm = xm || straddles_lines(static_cast<const T*>(srcs.p[m]) + head);
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
     if (n <= 4) {
-        launch_tree_n<T, OP, 4>(d, srcs, n, head, nvec, tail, aligned, st);
+        launch_tree_n<T, OP, 4>(d, srcs, n, head, nvec, tail, aligned, xm, st);
     } else if (n <= 8) {
-        launch_tree_n<T, OP, 8>(d, srcs, n, head, nvec, tail, aligned, st);
+        launch_tree_n<T, OP, 8>(d, srcs, n, head, nvec, tail, aligned, xm, st);
     } else {
-        launch_tree_n<T, OP, 16>(d, srcs, n, head, nvec, tail, aligned, st);
+        launch_tree_n<T, OP, 16>(d, srcs, n, head, nvec, tail, aligned, xm, st);
     }
     return hipGetLastError();
 }
