@@ -13,7 +13,7 @@ import statistics
 import sys
 
 CASES = [(0, 0), (16, 16), (32, 32), (64, 64), (112, 112), (4, 4), (68, 68),
-         (0, 4), (16, 4), (64, 68), (4, 0)]
+         (0, 4), (16, 4), (64, 68), (4, 0), (0, 16), (0, 64), (64, 0), (48, 0)]
 PER_CASE = 120
 ALG = 3 * (256 << 20)
 

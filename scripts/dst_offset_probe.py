@@ -7,6 +7,7 @@ contiguous 1 KiB; unless dst's vector region starts on a 128-B line, the
 first and last lines of every wave's span are shared with its neighbours.
 
     python scripts/dst_offset_probe.py [out.json]
+    UCX_BUILTIN_DEV_VARIANT=14 python scripts/dst_offset_probe.py   # no XCD map
 """
 import json
 import os
@@ -30,7 +31,8 @@ def main():
     ctx.fill("float32", "round", 2, bd, n + 128)
     rows = []
     for d_off, s_off in ((0, 0), (16, 16), (32, 32), (64, 64), (112, 112), (4, 4), (68, 68),
-                         (0, 4), (16, 4), (64, 68), (4, 0)):
+                         (0, 4), (16, 4), (64, 68), (4, 0), (0, 16), (0, 64), (64, 0),
+                         (48, 0)):
         dp, sp = bd.ptr + d_off, bs.ptr + s_off
         ctx.profile_reduce("sum", "float32", dp, sp, n, 20)
         b = sorted(ctx.profile_reduce("sum", "float32", dp, sp, n, 20) for _ in range(5))

@@ -55,7 +55,8 @@ def main():
     for k, b in enumerate(bufs):
         ctx.fill("float32", "exact", 100 + k, b, n8 + 16)
     for name, offs in (("aligned", [0] * 8), ("one_operand_4B", [4] + [0] * 7),
-                       ("all_phases", [0, 4, 8, 12, 4, 8, 12, 0])):
+                       ("all_phases", [0, 4, 8, 12, 4, 8, 12, 0]),
+                       ("in_phase_off_line_16B", [16] * 8)):
         srcs = [b.ptr + o for b, o in zip(bufs, offs)]
         for kernel in ("reduce_multi", "reduce_tree"):
             if kernel == "reduce_multi":

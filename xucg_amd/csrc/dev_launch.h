@@ -66,10 +66,11 @@ inline size_t line_head(const void *dst, size_t count)
     return h < count ? h : count;
 }
 
-/* XCD-aware tile map when a source's vectors straddle lines (see k_reduce) */
+/* XCD-aware tile map when a source's vectors straddle lines (see k_reduce);
+ * A/B variant 14 keeps the identity map */
 inline bool straddles_lines(const void *p)
 {
-    return ((uintptr_t)p & (kLine - 1)) != 0;
+    return ((uintptr_t)p & (kLine - 1)) != 0 && launch_variant() != 14;
 }
 
 template <typename T, int OP, int U, int NT, int BS, int XM = 0>
