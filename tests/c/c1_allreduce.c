@@ -127,5 +127,11 @@ int main(int argc, char **argv)
     ucg_builtin_lgroup_destroy(g);
     ucg_builtin_shm_iface_close(iface);
     ucg_builtin_combine_destroy(cmb);
+    for (r = 0; r < world; r++) {
+        free(inputs[r]);
+    }
+    free(inputs);
+    free(out);
+    free(want);
     return ok ? 0 : 3;
 }

@@ -44,6 +44,33 @@ def test_c1_harness_bit_exact(max_short, world):
     assert line["bit_exact"] and line["ranks"] == world and line["bytes"] == 4096
 
 
+@pytest.mark.parametrize("world,max_short,plan,incast", [
+    (4, 256, "", ""), (3, 256, "", ""), (8, 100, "", ""),
+    (4, 256, "tree", "1"), (5, 64, "tree", "")])
+def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast):
+    """The host engine (libucg_builtin.so sources) and the C1 harness rebuilt
+    with ASan + UBSan (tests/c/Makefile, target asan): recursive and tree
+    plans, fragmenting and resend-heavy sizes, the incast fan-in. Any
+    sanitizer report (invalid access, UB, leak at exit) fails the rank."""
+    import json
+    import subprocess
+    cdir = os.path.join(os.path.dirname(__file__), "c")
+    subprocess.run(["make", "-s", "-C", cdir, "asan"], check=True)
+    exe = os.path.join(cdir, "_build", "asan", "c1_allreduce")
+    monkeypatch.setenv("ASAN_OPTIONS", "detect_leaks=1:abort_on_error=0")
+    monkeypatch.setenv("UBSAN_OPTIONS", "print_stacktrace=1")
+    if plan:
+        monkeypatch.setenv("UCX_BUILTIN_ALLREDUCE_PLAN", plan)
+    if incast:
+        monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", incast)
+    codes, outs = launch_exe(exe, world, (shm_name(), 200, max_short))
+    assert codes == [0] * world, "\n".join(outs)
+    for out in outs:
+        assert "Sanitizer" not in out and "runtime error" not in out, out
+    line = json.loads(outs[0].strip().splitlines()[-1])
+    assert line["bit_exact"] and line["ranks"] == world
+
+
 def test_plan_description_and_unsupported_sizes():
     mpi = MockMPI()
     cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
