@@ -1,0 +1,207 @@
+/*
+ * stage_fuzz.c - row f1's fragment aggregator fuzzed from C against the
+ * oracle: random dtype x op, step length, fragment size, number of
+ * interleaved senders (a fan-in step with ep_cnt > 1), arrival order, recv
+ * buffer kind (pageable host at any element offset, or device memory) and
+ * staging ring geometry (small slots and shallow rings force the flush,
+ * clash and slot-reuse paths of ucg_builtin_dev_combine).
+ *
+ * Every fragment is handed over the way the AM handler does
+ * (builtin/ops/builtin_comp_step.inl:443-449): the payload lives in a
+ * buffer that is poisoned and freed as soon as the combine returns, so a
+ * shim that kept the borrowed pointer reads garbage (or, in the sanitizer
+ * build, a freed block). The expected result applies the oracle's
+ * reduce_cb_f restatement per fragment in arrival order, so the check is
+ * bit-exact for every dtype and op, NaN payloads included.
+ *
+ *   stage_fuzz [cases] [seed]
+ *
+ * Prints one JSON line; exit 3 on the first mismatch (with its case).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "ucg_builtin_dev.h"
+#include "combine_ref.h"
+
+static uint64_t g_rng;
+
+static uint64_t rnd(void)
+{
+    g_rng += 0x9E3779B97F4A7C15ull;
+    return ucg_oracle_splitmix64(g_rng);
+}
+
+static size_t rnd_in(size_t lo, size_t hi)      /* inclusive */
+{
+    return lo + (size_t)(rnd() % (hi - lo + 1));
+}
+
+typedef struct {
+    unsigned sender;
+    size_t   off;       /* bytes into the step buffer */
+    size_t   bytes;
+} frag_t;
+
+static int run_case(ucg_builtin_dev_ctx_t *ctx, int c, int *kinds)
+{
+    int dt, op;
+    do {
+        dt = (int)rnd_in(0, UCG_DEV_DT_LAST - 1);
+        op = (int)rnd_in(0, UCG_DEV_OP_LAST - 1);
+    } while (!ucg_oracle_is_supported(dt, op));
+    const size_t sz      = ucg_oracle_dtype_size(dt);
+    const size_t count   = rnd() % 4 == 0 ? rnd_in(1, 64) : rnd_in(1, 300000 / sz);
+    const size_t bytes   = count * sz;
+    const unsigned nsend = (unsigned)rnd_in(1, 4);
+    const size_t frag    = sz * rnd_in(1, rnd() % 2 ? 64 : 16384 / sz);
+    const int dev_recv   = rnd() % 3 == 0;
+    const size_t pad     = sz * rnd_in(0, 16 / sz + 1);  /* recv offset in elements */
+    const int dist       = (int)rnd_in(0, ORA_DIST_LAST - 1);
+    const int shuffle    = rnd() % 4 == 0;  /* reorder within a sender too */
+    char **srcs = calloc(nsend, sizeof(*srcs));
+    char *host_acc = malloc(pad + bytes + 1);
+    char *want = malloc(bytes + 1);
+    char *got = malloc(bytes + 1);
+    void *dbuf = NULL;
+    size_t nfr_per = (bytes + frag - 1) / frag, nfr = nsend * nfr_per, i, k;
+    frag_t *fr = calloc(nfr, sizeof(*fr));
+    size_t *next = calloc(nsend, sizeof(*next));
+    int ok = 1;
+
+    kinds[dev_recv]++;
+    for (k = 0; k < nsend; k++) {
+        srcs[k] = malloc(bytes + 1);
+        ucg_oracle_fill(dt, dist, 0xF0220000ull + 97ull * c + k, srcs[k], count);
+    }
+    ucg_oracle_fill(dt, dist, 0xF0230000ull + c, want, count);
+    memcpy(host_acc + pad, want, bytes);
+    if (dev_recv) {
+        dbuf = ucg_builtin_dev_malloc(ctx, pad + bytes);
+        if (dbuf == NULL ||
+            ucg_builtin_dev_memcpy(ctx, (char*)dbuf + pad, want, bytes) != UCS_OK ||
+            ucg_builtin_dev_sync(ctx) != UCS_OK) {
+            fprintf(stderr, "case %d: device recv buffer: %s\n", c,
+                    ucg_builtin_dev_last_error());
+            return -1;
+        }
+    }
+
+    /* arrival order: senders interleaved at random, each sender's fragments
+     * in offset order (one ordered AM stream per peer) unless shuffled */
+    for (k = 0; k < nsend; k++) {
+        for (i = 0; i < nfr_per; i++) {
+            frag_t *f = &fr[k * nfr_per + i];
+            f->sender = (unsigned)k;
+            f->off    = i * frag;
+            f->bytes  = bytes - f->off < frag ? bytes - f->off : frag;
+        }
+    }
+    if (shuffle) {
+        for (i = nfr; i > 1; i--) {
+            size_t j = rnd() % i;
+            frag_t t = fr[i - 1];
+            fr[i - 1] = fr[j];
+            fr[j] = t;
+        }
+    } else {
+        /* merge the per-sender lists in a random interleaving */
+        frag_t *m = calloc(nfr, sizeof(*m));
+        for (i = 0; i < nfr; i++) {
+            unsigned s;
+            do {
+                s = (unsigned)rnd_in(0, nsend - 1);
+            } while (next[s] == nfr_per);
+            m[i] = fr[s * nfr_per + next[s]++];
+        }
+        free(fr);
+        fr = m;
+    }
+
+    if (ucg_builtin_dev_stage_begin(ctx, dev_recv ? (char*)dbuf + pad : host_acc + pad,
+                                    bytes) != UCS_OK) {
+        fprintf(stderr, "case %d: stage_begin: %s\n", c, ucg_builtin_dev_last_error());
+        return -1;
+    }
+    for (i = 0; i < nfr; i++) {
+        const frag_t *f = &fr[i];
+        /* the borrowed AM payload: valid for the duration of the call only */
+        char *am = malloc(f->bytes);
+        memcpy(am, srcs[f->sender] + f->off, f->bytes);
+        if (ucg_builtin_dev_combine(ctx, (ucg_dev_op_t)op, (ucg_dev_dtype_t)dt, f->off,
+                                    am, f->bytes / sz) != UCS_OK) {
+            fprintf(stderr, "case %d: combine: %s\n", c, ucg_builtin_dev_last_error());
+            return -1;
+        }
+        memset(am, 0xA5, f->bytes);
+        free(am);
+        ucg_oracle_reduce(op, dt, srcs[f->sender] + f->off, want + f->off, f->bytes / sz);
+    }
+    if (ucg_builtin_dev_stage_end(ctx) != UCS_OK) {
+        fprintf(stderr, "case %d: stage_end: %s\n", c, ucg_builtin_dev_last_error());
+        return -1;
+    }
+    if (dev_recv) {
+        if (ucg_builtin_dev_memcpy(ctx, got, (char*)dbuf + pad, bytes) != UCS_OK ||
+            ucg_builtin_dev_sync(ctx) != UCS_OK) {
+            return -1;
+        }
+        ucg_builtin_dev_free(ctx, dbuf);
+    } else {
+        memcpy(got, host_acc + pad, bytes);
+    }
+    if (memcmp(got, want, bytes) != 0) {
+        for (i = 0; i < bytes && got[i] == want[i]; i++) {
+        }
+        fprintf(stderr, "case %d MISMATCH: dt=%d op=%d count=%zu frag=%zu senders=%u "
+                "dev_recv=%d pad=%zu shuffle=%d first bad byte %zu\n", c, dt, op,
+                count, frag, nsend, dev_recv, pad, shuffle, i);
+        ok = 0;
+    }
+    for (k = 0; k < nsend; k++) {
+        free(srcs[k]);
+    }
+    free(srcs);
+    free(host_acc);
+    free(want);
+    free(got);
+    free(fr);
+    free(next);
+    return ok;
+}
+
+int main(int argc, char **argv)
+{
+    const int cases = argc > 1 ? atoi(argv[1]) : 200;
+    g_rng = argc > 2 ? strtoull(argv[2], NULL, 0) : 0x5EEDF022ull;
+    /* ring geometries: tiny slots (a fragment spans slots, runs fill
+     * quickly), a shallow ring (slot reuse waits on the stream), default */
+    const size_t slot_bytes[] = {4096, 65536, 0};
+    const unsigned slots[]    = {2, 3, 0};
+    int kinds[2] = {0, 0}, done = 0, g, c;
+
+    for (g = 0; g < 3; g++) {
+        ucg_builtin_dev_ctx_params_t prm = {0, NULL, slot_bytes[g], slots[g]};
+        ucg_builtin_dev_ctx_t *ctx;
+        if (ucg_builtin_dev_ctx_create(&prm, &ctx) != UCS_OK) {
+            fprintf(stderr, "ctx: %s\n", ucg_builtin_dev_last_error());
+            return 1;
+        }
+        for (c = g; c < cases; c += 3) {
+            int r = run_case(ctx, c, kinds);
+            if (r < 0) {
+                return 1;
+            }
+            if (r == 0) {
+                return 3;
+            }
+            done++;
+        }
+        ucg_builtin_dev_ctx_destroy(ctx);
+    }
+    printf("{\"harness\": \"stage_fuzz\", \"cases\": %d, \"host_recv\": %d, "
+           "\"device_recv\": %d, \"bit_exact\": true}\n", done, kinds[0], kinds[1]);
+    return 0;
+}

@@ -234,6 +234,26 @@ def test_stage_bench_c_harness_bit_exact():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("seed", [0x5EEDF022, 0xF022A])
+def test_stage_fuzz_c_harness_bit_exact(seed):
+    """tests/c/stage_fuzz.c: the fragment aggregator against the oracle over
+    random dtype x op, step length, fragment size, 1-4 interleaved senders,
+    arrival order, host (any element offset) or device recv buffer and ring
+    geometry; every AM payload is poisoned and freed right after its
+    combine returns (the borrowed-src contract)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "c", "_build", "stage_fuzz")
+    p = subprocess.run([exe, "150", hex(seed)], capture_output=True, text=True,
+                       timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["bit_exact"] is True and line["cases"] == 150
+    assert line["host_recv"] > 0 and line["device_recv"] > 0
+
+
+@pytest.mark.gpu
 def test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu():
     """UCX_BUILTIN_DEV_COMBINE=y (default): a host recv buffer is combined by
     reduce_cb_f (staging would cross PCIe); a device-resident one
