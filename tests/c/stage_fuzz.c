@@ -16,6 +16,10 @@
  *
  *   stage_fuzz [cases] [seed]
  *
+ * A quarter of the cases take the whole-buffer form instead
+ * (ucg_builtin_dev_combine_host): src and dst each pageable, pinned or
+ * device memory at any element offset.
+ *
  * Prints one JSON line; exit 3 on the first mismatch (with its case).
  */
 #include <stdint.h>
@@ -172,6 +176,80 @@ static int run_case(ucg_builtin_dev_ctx_t *ctx, int c, int *kinds)
     return ok;
 }
 
+/* Whole-buffer form (ucg_builtin_dev_combine_host, the reduce_cb_f call
+ * shape): src and dst each pageable, pinned or device memory, at any
+ * element offset; lengths cross the ring's chunk boundaries. */
+static int run_whole(ucg_builtin_dev_ctx_t *ctx, int c, int *kinds)
+{
+    int dt, op;
+    do {
+        dt = (int)rnd_in(0, UCG_DEV_DT_LAST - 1);
+        op = (int)rnd_in(0, UCG_DEV_OP_LAST - 1);
+    } while (!ucg_oracle_is_supported(dt, op));
+    const size_t sz    = ucg_oracle_dtype_size(dt);
+    const size_t count = rnd() % 4 == 0 ? rnd_in(1, 64) : rnd_in(1, 400000 / sz);
+    const size_t bytes = count * sz;
+    const int dist     = (int)rnd_in(0, ORA_DIST_LAST - 1);
+    const int kind[2]  = {(int)rnd_in(0, 2), (int)rnd_in(0, 2)};  /* src, dst */
+    const size_t pad[2] = {sz * rnd_in(0, 16 / sz + 1), sz * rnd_in(0, 16 / sz + 1)};
+    char *host[2], *base[2], *want = malloc(bytes + 1), *got = malloc(bytes + 1);
+    int j, ok = 1;
+
+    ucg_oracle_fill(dt, dist, 0xF0240000ull + c, want, count);   /* dst */
+    for (j = 0; j < 2; j++) {
+        host[j] = malloc(bytes + 1);
+        ucg_oracle_fill(dt, dist, j ? 0xF0240000ull + c : 0xF0250000ull + c, host[j],
+                        count);
+        kinds[kind[j]]++;
+        base[j] = kind[j] == 0 ? malloc(pad[j] + bytes)
+                : kind[j] == 1 ? ucg_builtin_dev_host_alloc(pad[j] + bytes)
+                               : ucg_builtin_dev_malloc(ctx, pad[j] + bytes);
+        if (base[j] == NULL) {
+            fprintf(stderr, "case %d: allocation: %s\n", c, ucg_builtin_dev_last_error());
+            return -1;
+        }
+        if (kind[j] == 2) {
+            if (ucg_builtin_dev_memcpy(ctx, base[j] + pad[j], host[j], bytes) != UCS_OK) {
+                return -1;
+            }
+        } else {
+            memcpy(base[j] + pad[j], host[j], bytes);
+        }
+    }
+    ucg_oracle_reduce(op, dt, host[0], want, count);
+    if (ucg_builtin_dev_combine_host(ctx, (ucg_dev_op_t)op, (ucg_dev_dtype_t)dt,
+                                     base[1] + pad[1], base[0] + pad[0], count) != UCS_OK) {
+        fprintf(stderr, "case %d: combine_host: %s\n", c, ucg_builtin_dev_last_error());
+        return -1;
+    }
+    if (kind[1] == 2) {
+        if (ucg_builtin_dev_memcpy(ctx, got, base[1] + pad[1], bytes) != UCS_OK) {
+            return -1;
+        }
+    } else {
+        memcpy(got, base[1] + pad[1], bytes);
+    }
+    if (memcmp(got, want, bytes) != 0) {
+        fprintf(stderr, "case %d MISMATCH (whole buffer): dt=%d op=%d count=%zu "
+                "src kind %d pad %zu, dst kind %d pad %zu\n", c, dt, op, count,
+                kind[0], pad[0], kind[1], pad[1]);
+        ok = 0;
+    }
+    for (j = 0; j < 2; j++) {
+        if (kind[j] == 0) {
+            free(base[j]);
+        } else if (kind[j] == 1) {
+            ucg_builtin_dev_host_free(base[j]);
+        } else {
+            ucg_builtin_dev_free(ctx, base[j]);
+        }
+        free(host[j]);
+    }
+    free(want);
+    free(got);
+    return ok;
+}
+
 int main(int argc, char **argv)
 {
     const int cases = argc > 1 ? atoi(argv[1]) : 200;
@@ -180,7 +258,7 @@ int main(int argc, char **argv)
      * quickly), a shallow ring (slot reuse waits on the stream), default */
     const size_t slot_bytes[] = {4096, 65536, 0};
     const unsigned slots[]    = {2, 3, 0};
-    int kinds[2] = {0, 0}, done = 0, g, c;
+    int kinds[2] = {0, 0}, whole_kinds[3] = {0, 0, 0}, done = 0, whole = 0, g, c;
 
     for (g = 0; g < 3; g++) {
         ucg_builtin_dev_ctx_params_t prm = {0, NULL, slot_bytes[g], slots[g]};
@@ -190,7 +268,9 @@ int main(int argc, char **argv)
             return 1;
         }
         for (c = g; c < cases; c += 3) {
-            int r = run_case(ctx, c, kinds);
+            const int w = rnd() % 4 == 0;
+            int r = w ? run_whole(ctx, c, whole_kinds) : run_case(ctx, c, kinds);
+            whole += w;
             if (r < 0) {
                 return 1;
             }
@@ -202,6 +282,8 @@ int main(int argc, char **argv)
         ucg_builtin_dev_ctx_destroy(ctx);
     }
     printf("{\"harness\": \"stage_fuzz\", \"cases\": %d, \"host_recv\": %d, "
-           "\"device_recv\": %d, \"bit_exact\": true}\n", done, kinds[0], kinds[1]);
+           "\"device_recv\": %d, \"whole_buffer\": %d, \"whole_operands\": "
+           "{\"pageable\": %d, \"pinned\": %d, \"device\": %d}, \"bit_exact\": true}\n",
+           done, kinds[0], kinds[1], whole, whole_kinds[0], whole_kinds[1], whole_kinds[2]);
     return 0;
 }

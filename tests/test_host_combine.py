@@ -240,7 +240,9 @@ def test_stage_fuzz_c_harness_bit_exact(seed):
     random dtype x op, step length, fragment size, 1-4 interleaved senders,
     arrival order, host (any element offset) or device recv buffer and ring
     geometry; every AM payload is poisoned and freed right after its
-    combine returns (the borrowed-src contract)."""
+    combine returns (the borrowed-src contract). A quarter of the cases take
+    the whole-buffer form (combine_host) with src and dst each pageable,
+    pinned or device memory at any element offset."""
     import json
     import os
     import subprocess
@@ -250,7 +252,7 @@ def test_stage_fuzz_c_harness_bit_exact(seed):
     assert p.returncode == 0, p.stdout + p.stderr
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["bit_exact"] is True and line["cases"] == 150
-    assert line["host_recv"] > 0 and line["device_recv"] > 0
+    assert line["host_recv"] > 0 and line["device_recv"] > 0 and line["whole_buffer"] > 0
 
 
 @pytest.mark.gpu
