@@ -5,6 +5,8 @@
  *
  *   RANK=r WORLD_SIZE=n c1_allreduce <shm-name> [iters] [max_short] [count]
  *
+ * C1_DEVICE_STAGING=1 forces every combine onto the GPU (staged steps).
+ *
  * The "MPI library" behind reduce_cb_f is a plain C loop with MPI's operand
  * order (inoutvec[i] = invec[i] + inoutvec[i]); inputs are exact integers so
  * its NaN handling never matters, nor does the tree plan's arrival order
@@ -67,6 +69,13 @@ int main(int argc, char **argv)
     int i, ok;
     double t0, us;
 
+    if (getenv("C1_DEVICE_STAGING")) {
+        /* every step staged on the GPU: the configuration read the way UCX
+         * reads it (UCX_BUILTIN_DEV_*), then forced on for any size */
+        ucg_builtin_combine_config_read(&cfg);
+        cfg.dev_enable    = 2;
+        cfg.dev_min_bytes = 0;
+    }
     if (ucg_builtin_combine_create(&rp, &cfg, &cmb) != UCS_OK ||
         ucg_builtin_shm_iface_open(name, world, rank, max_short, 64, &iface) != UCS_OK ||
         ucg_builtin_lgroup_create(iface, 1, world, rank, cmb, &g) != UCS_OK) {
@@ -113,15 +122,19 @@ int main(int argc, char **argv)
     ok = memcmp(out, want, count * sizeof(float)) == 0;
     ucg_builtin_shm_barrier(iface);
     if (rank == 0) {
-        uint64_t st[4];
+        uint64_t st[4], cs[6];
         ucg_builtin_lgroup_stats(g, st);
+        ucg_builtin_combine_stats(cmb, cs);
         printf("{\"config\": \"C1: %u-rank loopback allreduce, %d fp32 SUM\", "
                "\"ranks\": %u, \"bytes\": %zu, \"max_short\": %zu, "
                "\"latency_us\": %.3f, \"iters\": %d, \"bit_exact\": %s, "
-               "\"messages_sent\": %llu, \"stashed\": %llu}\n",
+               "\"messages_sent\": %llu, \"stashed\": %llu, "
+               "\"host_combines\": %llu, \"device_combines\": %llu, "
+               "\"device_staged_steps\": %llu}\n",
                world, count, world, count * sizeof(float), max_short, us, iters,
                ok ? "true" : "false", (unsigned long long)st[0],
-               (unsigned long long)st[2]);
+               (unsigned long long)st[2], (unsigned long long)cs[0],
+               (unsigned long long)cs[2], (unsigned long long)cs[4]);
     }
     ucg_builtin_lcoll_destroy(c);
     ucg_builtin_lgroup_destroy(g);

@@ -99,18 +99,50 @@ int main(int argc, char **argv)
         ucg_builtin_dev_free(ctx, d);
         if (acc < 0) return 4;
     }
+    /* small steps into a device-resident recv buffer (GPU-aware MPI): one
+     * fragment per step, stage_begin .. stage_end, mean over 2000 steps */
+    const size_t small[3] = {256, 4096, 65536};
+    double small_us[3];
+    uint64_t c[4];
+    ucg_builtin_dev_counters(ctx, c);   /* launches of the 64 MiB steps */
     {
-        uint64_t c[4];
-        ucg_builtin_dev_counters(ctx, c);
+        int j;
+        for (j = 0; j < 3; j++) {
+            const int k = 2000;
+            void *d = ucg_builtin_dev_malloc(ctx, small[j]);
+            if (d == NULL || ucg_builtin_dev_memcpy(ctx, d, dst, small[j]) != UCS_OK) {
+                return 5;
+            }
+            for (i = -50; i < k; i++) {
+                if (i == 0) {
+                    t0 = now_s();
+                }
+                if (ucg_builtin_dev_stage_begin(ctx, d, small[j]) != UCS_OK ||
+                    ucg_builtin_dev_combine(ctx, UCG_DEV_OP_SUM, UCG_DEV_DT_FLOAT32, 0,
+                                            src, small[j] / 4) != UCS_OK ||
+                    ucg_builtin_dev_stage_end(ctx) != UCS_OK) {
+                    fprintf(stderr, "small step: %s\n", ucg_builtin_dev_last_error());
+                    return 5;
+                }
+            }
+            small_us[j] = (now_s() - t0) / k * 1e6;
+            ucg_builtin_dev_free(ctx, d);
+        }
+    }
+    {
+        const char *z = getenv("UCX_BUILTIN_DEV_ZCOPY_BYTES");
         printf("{\"config\": \"f1 staged REDUCE step, fp32 SUM, pageable host buffers\", "
                "\"bytes\": %zu, \"fragment_bytes\": %zu, \"fragments\": %zu, "
                "\"device_staged_ms\": %.3f, \"device_staged_gibs_n\": %.2f, "
                "\"cpu_fragmented_ms\": %.3f, \"cpu_fragmented_gibs_n\": %.2f, "
                "\"kernel_launches_total\": %llu, \"bit_exact\": %s, "
-               "\"mem_kind_ns_host\": %.1f, \"mem_kind_ns_device\": %.1f}\n",
+               "\"mem_kind_ns_host\": %.1f, \"mem_kind_ns_device\": %.1f, "
+               "\"small_step_us_device_recv\": {\"256\": %.2f, \"4096\": %.2f, "
+               "\"65536\": %.2f}, \"zcopy_bytes\": \"%s\"}\n",
                total, frag, (total + frag - 1) / frag, t_dev * 1e3,
                total / t_dev / 1073741824.0, t_cpu * 1e3, total / t_cpu / 1073741824.0,
-               (unsigned long long)c[0], ok ? "true" : "false", mk_host_ns, mk_dev_ns);
+               (unsigned long long)c[0], ok ? "true" : "false", mk_host_ns, mk_dev_ns,
+               small_us[0], small_us[1], small_us[2], z ? z : "default");
     }
     ucg_builtin_dev_ctx_destroy(ctx);
     free(src);

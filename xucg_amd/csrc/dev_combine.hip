@@ -147,6 +147,9 @@ struct ucg_builtin_dev_ctx {
     size_t       slot_bytes;
     unsigned     nslots;
     char        *h_ring;       /* pinned host, nslots * slot_bytes */
+    char        *h_ring_dev;   /* the same memory's device address */
+    size_t       zcopy_max;    /* runs up to this many bytes are read by
+                                  the kernel from h_ring over PCIe  */
     char        *d_ring;       /* device src slots                 */
     char        *d_ring2;      /* device dst slots (host pipeline) */
     hipEvent_t  *slot_ev;      /* slot free once this completes    */
@@ -192,6 +195,7 @@ static ucs_status_t ring_init(ucg_builtin_dev_ctx_t *ctx)
     }
     const size_t total = ctx->slot_bytes * ctx->nslots;
     HIP_TRY(hipHostMalloc((void**)&ctx->h_ring, total, hipHostMallocDefault));
+    HIP_TRY(hipHostGetDevicePointer((void**)&ctx->h_ring_dev, ctx->h_ring, 0));
     HIP_TRY(hipMalloc((void**)&ctx->d_ring, total));
     HIP_TRY(hipMalloc((void**)&ctx->d_ring2, total));
     ctx->slot_ev   = new hipEvent_t[ctx->nslots];
@@ -305,6 +309,14 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
         r.active = false;
     }
     ctx->run_seq     = 0;
+    ctx->h_ring_dev  = nullptr;
+    /* small runs skip the H2D copy (UCX_BUILTIN_DEV_ZCOPY_BYTES, 0 = never):
+     * one DMA submission costs more than the kernel reading a few KiB of
+     * pinned memory over PCIe (small steps) */
+    ctx->zcopy_max   = 64u << 10;
+    if (const char *z = getenv("UCX_BUILTIN_DEV_ZCOPY_BYTES")) {
+        ctx->zcopy_max = strtoull(z, nullptr, 0);
+    }
     for (auto &c : ctx->counters) {
         c = 0;
     }
@@ -840,9 +852,17 @@ static ucs_status_t run_flush(ucg_builtin_dev_ctx_t *ctx,
     }
     r.active = false;
     const size_t sz = kDtSize[r.dt];
-    char *ds = ctx->d_ring + (size_t)r.slot * ctx->slot_bytes + r.pad;
-    HIP_TRY(hipMemcpyAsync(ds, ctx->h_ring + (size_t)r.slot * ctx->slot_bytes + r.pad,
-                           r.used, hipMemcpyHostToDevice, ctx->stream));
+    const size_t so = (size_t)r.slot * ctx->slot_bytes + r.pad;
+    const char *ds;
+    if (r.used <= ctx->zcopy_max) {
+        /* small run: the kernel reads the pinned slot itself; the slot's
+         * event (below) still orders its reuse after the kernel */
+        ds = ctx->h_ring_dev + so;
+    } else {
+        ds = ctx->d_ring + so;
+        HIP_TRY(hipMemcpyAsync(const_cast<char*>(ds), ctx->h_ring + so, r.used,
+                               hipMemcpyHostToDevice, ctx->stream));
+    }
     ucs_status_t st = reduce_on(ctx, ctx->stream, (ucg_dev_op_t)r.op,
                                 (ucg_dev_dtype_t)r.dt, ctx->acc + r.off, ds,
                                 r.used / sz);
