@@ -3,7 +3,8 @@
 # (product library), then the device shim's host code under clang ASan+UBSan
 # (tests/c/Makefile target asan-dev; host side only). Each step has its own
 # limit; a timeout or signal ends the script.
-#   usage: scripts/stage_fuzz_gpu.sh TAG
+#   usage: scripts/stage_fuzz_gpu.sh TAG   (build first, on the CPU side:
+#          make -C tests/c all asan-dev)
 set -u
 TAG=${1:-r01}
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
