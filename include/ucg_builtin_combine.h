@@ -63,6 +63,8 @@ typedef struct ucg_builtin_combine_config {
     size_t   stage_bytes;    /* UCX_BUILTIN_DEV_STAGE_BYTES  (default 16 MiB)  */
     unsigned stage_slots;    /* UCX_BUILTIN_DEV_STAGE_SLOTS  (default 4)       */
     int      device;         /* UCX_BUILTIN_DEV_DEVICE       (default -1)      */
+    size_t   zcopy_bytes;    /* UCX_BUILTIN_DEV_ZCOPY_BYTES  (default 64k;
+                                0, n, never: UCG_BUILTIN_DEV_ZCOPY_NEVER)      */
 } ucg_builtin_combine_config_t;
 
 typedef struct ucg_builtin_combine ucg_builtin_combine_t;

@@ -147,7 +147,14 @@ typedef struct ucg_builtin_dev_ctx_params {
                               (so the legacy null stream cannot be chosen) */
     size_t   stage_bytes;  /* pinned staging slot size; 0 = 16 MiB */
     unsigned stage_slots;  /* staging ring depth; 0 = 4 */
+    size_t   zcopy_bytes;  /* staged runs of at most this many bytes are read
+                              by the kernel from the pinned slot over PCIe,
+                              with no H2D copy; 0 = 64 KiB,
+                              UCG_BUILTIN_DEV_ZCOPY_NEVER = always copy */
 } ucg_builtin_dev_ctx_params_t;
+
+#define UCG_BUILTIN_DEV_ZCOPY_DEFAULT ((size_t)64 << 10)
+#define UCG_BUILTIN_DEV_ZCOPY_NEVER   ((size_t)-1)
 
 /* ---- introspection (no GPU needed) ---------------------------------------*/
 size_t      ucg_builtin_dev_dtype_size(ucg_dev_dtype_t dt);
@@ -308,8 +315,12 @@ ucs_status_t ucg_builtin_dev_profile_stream(ucg_builtin_dev_ctx_t *ctx, int kind
                                             void *dst, const void *src, size_t bytes,
                                             unsigned iters, double *avg_us);
 /* Counters since ctx creation: [0] kernel launches, [1] bytes combined on the
- * device (3N basis), [2] H2D bytes, [3] D2H bytes. */
-void         ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx, uint64_t out[4]);
+ * device (3N basis), [2] H2D bytes copied by DMA (hipMemcpyAsync), [3] D2H
+ * bytes, [4] staged bytes the kernel read from pinned host memory in place
+ * (zero-copy runs, no DMA). */
+#define UCG_BUILTIN_DEV_NCOUNTERS 5
+void         ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx,
+                                      uint64_t out[UCG_BUILTIN_DEV_NCOUNTERS]);
 
 #ifdef __cplusplus
 }

@@ -255,19 +255,28 @@ int main(int argc, char **argv)
     const int cases = argc > 1 ? atoi(argv[1]) : 200;
     g_rng = argc > 2 ? strtoull(argv[2], NULL, 0) : 0x5EEDF022ull;
     /* ring geometries: tiny slots (a fragment spans slots, runs fill
-     * quickly), a shallow ring (slot reuse waits on the stream), default */
-    const size_t slot_bytes[] = {4096, 65536, 0};
-    const unsigned slots[]    = {2, 3, 0};
+     * quickly), a shallow ring (slot reuse waits on the stream), default;
+     * each with the default zero-copy threshold (runs <= 64 KiB are read by
+     * the kernel from the pinned slot: every run of the 4 KiB and 64 KiB
+     * geometries) and again with zero-copy off (every run copied H2D), so
+     * both flush paths see the clash and slot-reuse orderings */
+    const size_t slot_bytes[] = {4096, 65536, 0, 4096, 65536, 0};
+    const unsigned slots[]    = {2, 3, 0, 2, 3, 0};
+    const size_t zcopy[]      = {0, 0, 0, UCG_BUILTIN_DEV_ZCOPY_NEVER,
+                                 UCG_BUILTIN_DEV_ZCOPY_NEVER, UCG_BUILTIN_DEV_ZCOPY_NEVER};
+    const int ngeo = 6;
     int kinds[2] = {0, 0}, whole_kinds[3] = {0, 0, 0}, done = 0, whole = 0, g, c;
+    int by_path[2] = {0, 0};
+    uint64_t zc_bytes = 0, dma_bytes = 0;
 
-    for (g = 0; g < 3; g++) {
-        ucg_builtin_dev_ctx_params_t prm = {0, NULL, slot_bytes[g], slots[g]};
+    for (g = 0; g < ngeo; g++) {
+        ucg_builtin_dev_ctx_params_t prm = {0, NULL, slot_bytes[g], slots[g], zcopy[g]};
         ucg_builtin_dev_ctx_t *ctx;
         if (ucg_builtin_dev_ctx_create(&prm, &ctx) != UCS_OK) {
             fprintf(stderr, "ctx: %s\n", ucg_builtin_dev_last_error());
             return 1;
         }
-        for (c = g; c < cases; c += 3) {
+        for (c = g; c < cases; c += ngeo) {
             const int w = rnd() % 4 == 0;
             int r = w ? run_whole(ctx, c, whole_kinds) : run_case(ctx, c, kinds);
             whole += w;
@@ -278,12 +287,28 @@ int main(int argc, char **argv)
                 return 3;
             }
             done++;
+            by_path[zcopy[g] == UCG_BUILTIN_DEV_ZCOPY_NEVER]++;
+        }
+        {
+            uint64_t cnt[UCG_BUILTIN_DEV_NCOUNTERS];
+            ucg_builtin_dev_counters(ctx, cnt);
+            dma_bytes += cnt[2];
+            zc_bytes  += cnt[4];
+            if (zcopy[g] == UCG_BUILTIN_DEV_ZCOPY_NEVER && cnt[4] != 0) {
+                fprintf(stderr, "geometry %d: zero-copy off but %llu bytes read in "
+                        "place\n", g, (unsigned long long)cnt[4]);
+                return 3;
+            }
         }
         ucg_builtin_dev_ctx_destroy(ctx);
     }
     printf("{\"harness\": \"stage_fuzz\", \"cases\": %d, \"host_recv\": %d, "
            "\"device_recv\": %d, \"whole_buffer\": %d, \"whole_operands\": "
-           "{\"pageable\": %d, \"pinned\": %d, \"device\": %d}, \"bit_exact\": true}\n",
-           done, kinds[0], kinds[1], whole, whole_kinds[0], whole_kinds[1], whole_kinds[2]);
+           "{\"pageable\": %d, \"pinned\": %d, \"device\": %d}, "
+           "\"cases_zcopy_default\": %d, \"cases_zcopy_off\": %d, "
+           "\"h2d_dma_bytes\": %llu, \"zcopy_read_bytes\": %llu, \"bit_exact\": true}\n",
+           done, kinds[0], kinds[1], whole, whole_kinds[0], whole_kinds[1], whole_kinds[2],
+           by_path[0], by_path[1], (unsigned long long)dma_bytes,
+           (unsigned long long)zc_bytes);
     return 0;
 }

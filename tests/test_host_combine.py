@@ -35,6 +35,20 @@ def test_config_from_environment(monkeypatch):
     assert c.dev_enable == 1 and c.dev_min_bytes == 1 << 20 and c.stage_bytes == 16 << 20
 
 
+def test_zcopy_threshold_parsed_as_memory_units(monkeypatch):
+    """UCX_BUILTIN_DEV_ZCOPY_BYTES goes through the same unit parser as the
+    other size knobs: '64k' is 65536, not 64; '0' and 'never' turn it off;
+    unset is the 64 KiB default."""
+    from xucg_amd import _lib
+    monkeypatch.delenv("UCX_BUILTIN_DEV_ZCOPY_BYTES", raising=False)
+    assert host.read_config().zcopy_bytes == 64 << 10
+    for text, want in (("64k", 64 << 10), ("1m", 1 << 20), ("4096", 4096),
+                       ("010", 10), ("0", _lib.ZCOPY_NEVER),
+                       ("never", _lib.ZCOPY_NEVER), ("off", _lib.ZCOPY_NEVER)):
+        monkeypatch.setenv("UCX_BUILTIN_DEV_ZCOPY_BYTES", text)
+        assert host.read_config().zcopy_bytes == want, text
+
+
 def test_classification_through_api_callbacks():
     mpi = MockMPI()
     cmb = host_only_combine(mpi)

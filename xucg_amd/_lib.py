@@ -48,7 +48,12 @@ _st = ctypes.c_int
 
 class DevCtxParams(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("stream", ctypes.c_void_p),
-                ("stage_bytes", ctypes.c_size_t), ("stage_slots", ctypes.c_uint)]
+                ("stage_bytes", ctypes.c_size_t), ("stage_slots", ctypes.c_uint),
+                ("zcopy_bytes", ctypes.c_size_t)]
+
+
+ZCOPY_NEVER = (1 << 64) - 1   # UCG_BUILTIN_DEV_ZCOPY_NEVER
+NCOUNTERS = 5                 # UCG_BUILTIN_DEV_NCOUNTERS
 
 
 DEV_API = {

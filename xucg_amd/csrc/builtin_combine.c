@@ -96,6 +96,16 @@ void ucg_builtin_combine_config_read(ucg_builtin_combine_config_t *cfg)
     cfg->stage_slots   = (unsigned)parse_memunits(
                                         getenv("UCX_BUILTIN_DEV_STAGE_SLOTS"), 4);
     cfg->device        = dev ? atoi(dev) : -1;
+    {
+        /* "0" (and n/no/off/never) turns zero-copy runs off; the field uses
+         * the device params' convention (0 = default, NEVER = off) */
+        const char *z = getenv("UCX_BUILTIN_DEV_ZCOPY_BYTES");
+        if (z && (!strcasecmp(z, "never") || parse_bool(z, 1) == 0)) {
+            cfg->zcopy_bytes = UCG_BUILTIN_DEV_ZCOPY_NEVER;
+        } else {
+            cfg->zcopy_bytes = parse_memunits(z, UCG_BUILTIN_DEV_ZCOPY_DEFAULT);
+        }
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -126,7 +136,8 @@ ucs_status_t ucg_builtin_combine_create(const ucg_builtin_reduce_params_t *param
             .device      = cmb->cfg.device,
             .stream      = NULL,
             .stage_bytes = cmb->cfg.stage_bytes,
-            .stage_slots = cmb->cfg.stage_slots
+            .stage_slots = cmb->cfg.stage_slots,
+            .zcopy_bytes = cmb->cfg.zcopy_bytes
         };
         /* a device that fails to initialise is an error, not a silent
          * downgrade: the caller asked for the device path */

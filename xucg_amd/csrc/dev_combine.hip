@@ -179,7 +179,7 @@ struct ucg_builtin_dev_ctx {
     unsigned     max_runs;
     uint64_t     run_seq;
 
-    std::atomic<uint64_t> counters[4];
+    std::atomic<uint64_t> counters[UCG_BUILTIN_DEV_NCOUNTERS];
 };
 
 static ucs_status_t set_device(ucg_builtin_dev_ctx_t *ctx)
@@ -310,13 +310,11 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
     }
     ctx->run_seq     = 0;
     ctx->h_ring_dev  = nullptr;
-    /* small runs skip the H2D copy (UCX_BUILTIN_DEV_ZCOPY_BYTES, 0 = never):
-     * one DMA submission costs more than the kernel reading a few KiB of
-     * pinned memory over PCIe (small steps) */
-    ctx->zcopy_max   = 64u << 10;
-    if (const char *z = getenv("UCX_BUILTIN_DEV_ZCOPY_BYTES")) {
-        ctx->zcopy_max = strtoull(z, nullptr, 0);
-    }
+    /* small runs skip the H2D copy: one DMA submission costs more than the
+     * kernel reading a few KiB of pinned memory over PCIe.
+     * The threshold comes from params->zcopy_bytes, which the host layer
+     * reads from UCX_BUILTIN_DEV_ZCOPY_BYTES (ucg_builtin_combine_config_read) */
+    ctx->zcopy_max   = UCG_BUILTIN_DEV_ZCOPY_DEFAULT;
     for (auto &c : ctx->counters) {
         c = 0;
     }
@@ -329,6 +327,11 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
         }
         if (params->stage_slots) {
             ctx->nslots = params->stage_slots < 2 ? 2 : params->stage_slots;
+        }
+        if (params->zcopy_bytes == UCG_BUILTIN_DEV_ZCOPY_NEVER) {
+            ctx->zcopy_max = 0;
+        } else if (params->zcopy_bytes) {
+            ctx->zcopy_max = params->zcopy_bytes;
         }
     }
     ctx->max_runs = ctx->nslots - 1 < 4 ? ctx->nslots - 1 : 4;
@@ -858,10 +861,12 @@ static ucs_status_t run_flush(ucg_builtin_dev_ctx_t *ctx,
         /* small run: the kernel reads the pinned slot itself; the slot's
          * event (below) still orders its reuse after the kernel */
         ds = ctx->h_ring_dev + so;
+        ctx->counters[4] += r.used;
     } else {
         ds = ctx->d_ring + so;
         HIP_TRY(hipMemcpyAsync(const_cast<char*>(ds), ctx->h_ring + so, r.used,
                                hipMemcpyHostToDevice, ctx->stream));
+        ctx->counters[2] += r.used;
     }
     ucs_status_t st = reduce_on(ctx, ctx->stream, (ucg_dev_op_t)r.op,
                                 (ucg_dev_dtype_t)r.dt, ctx->acc + r.off, ds,
@@ -870,7 +875,6 @@ static ucs_status_t run_flush(ucg_builtin_dev_ctx_t *ctx,
         return st;
     }
     HIP_TRY(hipEventRecord(ctx->slot_ev[r.slot], ctx->stream));
-    ctx->counters[2] += r.used;
     return UCS_OK;
 }
 
@@ -1308,9 +1312,10 @@ ucs_status_t ucg_builtin_dev_profile_stream(ucg_builtin_dev_ctx_t *ctx, int kind
     return UCS_OK;
 }
 
-void ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx, uint64_t out[4])
+void ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx,
+                              uint64_t out[UCG_BUILTIN_DEV_NCOUNTERS])
 {
-    for (int i = 0; i < 4; i++) {
+    for (int i = 0; i < UCG_BUILTIN_DEV_NCOUNTERS; i++) {
         out[i] = ctx ? ctx->counters[i].load() : 0;
     }
 }

@@ -115,7 +115,8 @@ class DevContext:
     """Per-group device context: one HIP stream, a pinned staging ring and the
     per-step device accumulator."""
 
-    def __init__(self, device=-1, stream=None, stage_bytes=0, stage_slots=0):
+    def __init__(self, device=-1, stream=None, stage_bytes=0, stage_slots=0,
+                 zcopy_bytes=0):
         if stream is not None and stream == 0:
             # the C ABI reads NULL as "create a stream": the legacy null stream
             # cannot be shared, and a private non-blocking stream would not be
@@ -123,7 +124,9 @@ class DevContext:
             raise ValueError("stream 0 (the null stream) cannot be shared; use "
                              "DevContext.on_torch_stream()")
         L = _lib.dev()
-        p = _lib.DevCtxParams(device, stream, stage_bytes, stage_slots)
+        # zcopy_bytes: 0 = the library default (64 KiB), None = never
+        zc = _lib.ZCOPY_NEVER if zcopy_bytes is None else zcopy_bytes
+        p = _lib.DevCtxParams(device, stream, stage_bytes, stage_slots, zc)
         h = ctypes.c_void_p()
         check(L.ucg_builtin_dev_ctx_create(ctypes.byref(p), ctypes.byref(h)),
               "ucg_builtin_dev_ctx_create")
@@ -267,7 +270,7 @@ class DevContext:
         return us.value
 
     def counters(self):
-        out = (ctypes.c_uint64 * 4)()
+        out = (ctypes.c_uint64 * _lib.NCOUNTERS)()
         _lib.dev().ucg_builtin_dev_counters(self.handle, out)
         return {"launches": out[0], "combined_bytes": out[1], "h2d_bytes": out[2],
-                "d2h_bytes": out[3]}
+                "d2h_bytes": out[3], "zcopy_bytes": out[4]}
