@@ -211,6 +211,41 @@ int main(int argc, char **argv)
             }
         }
     }
+    /* where the small-step floor goes, same process: (a) an empty step
+     * (stage_begin + stage_end: one stream sync with nothing queued), (b) one
+     * device-resident 4 KiB combine + sync (launch + completion wait), each
+     * the median of 7 reps of 400 */
+    double floor_sync_us, floor_launch_us;
+    {
+        void *d = ucg_builtin_dev_malloc(ctx[ZC], 8192);
+        double v[2][7];
+        int r, k;
+        if (d == NULL) {
+            return 5;
+        }
+        for (r = 0; r < 7; r++) {
+            for (k = -20; k < 400; k++) {
+                if (k == 0) t0 = now_s();
+                if (ucg_builtin_dev_stage_begin(ctx[ZC], d, 4096) != UCS_OK ||
+                    ucg_builtin_dev_stage_end(ctx[ZC]) != UCS_OK) {
+                    return 5;
+                }
+            }
+            v[0][r] = (now_s() - t0) / 400 * 1e6;
+            for (k = -20; k < 400; k++) {
+                if (k == 0) t0 = now_s();
+                if (ucg_builtin_dev_reduce(ctx[ZC], UCG_DEV_OP_SUM, UCG_DEV_DT_FLOAT32, d,
+                                           (char*)d + 4096, 1024) != UCS_OK ||
+                    ucg_builtin_dev_sync(ctx[ZC]) != UCS_OK) {
+                    return 5;
+                }
+            }
+            v[1][r] = (now_s() - t0) / 400 * 1e6;
+        }
+        floor_sync_us   = median(v[0], 7);
+        floor_launch_us = median(v[1], 7);
+        ucg_builtin_dev_free(ctx[ZC], d);
+    }
     {
         double lo[2], hi[2], md[2], cpu_md;
         for (c = 0; c < 2; c++) {
@@ -239,7 +274,8 @@ int main(int argc, char **argv)
                "\"small_step_us_range\": {\"zcopy\": [[%.2f, %.2f], [%.2f, %.2f], "
                "[%.2f, %.2f]], \"copy\": [[%.2f, %.2f], [%.2f, %.2f], [%.2f, %.2f]]}, "
                "\"small_step_timing\": \"median of %d alternating reps of 400 steps "
-               "per context, one process\"}\n",
+               "per context, one process\", \"floor_empty_step_us\": %.2f, "
+               "\"floor_device_reduce_4k_plus_sync_us\": %.2f}\n",
                total, frag, (total + frag - 1) / frag, reps,
                md[ZC] * 1e3, total / md[ZC] / 1073741824.0, lo[ZC] * 1e3, hi[ZC] * 1e3,
                md[COPY] * 1e3, lo[COPY] * 1e3, hi[COPY] * 1e3,
@@ -252,7 +288,8 @@ int main(int argc, char **argv)
                small_lo[ZC][0], small_hi[ZC][0], small_lo[ZC][1], small_hi[ZC][1],
                small_lo[ZC][2], small_hi[ZC][2],
                small_lo[COPY][0], small_hi[COPY][0], small_lo[COPY][1], small_hi[COPY][1],
-               small_lo[COPY][2], small_hi[COPY][2], sreps);
+               small_lo[COPY][2], small_hi[COPY][2], sreps, floor_sync_us,
+               floor_launch_us);
     }
     for (c = 0; c < 2; c++) {
         ucg_builtin_dev_ctx_destroy(ctx[c]);

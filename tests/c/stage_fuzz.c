@@ -288,6 +288,9 @@ int main(int argc, char **argv)
             }
             done++;
             by_path[zcopy[g] == UCG_BUILTIN_DEV_ZCOPY_NEVER]++;
+            if (done % 250 == 0) {   /* progress for long runs */
+                fprintf(stderr, "stage_fuzz: %d cases bit-exact\n", done);
+            }
         }
         {
             uint64_t cnt[UCG_BUILTIN_DEV_NCOUNTERS];

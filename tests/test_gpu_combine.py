@@ -227,6 +227,38 @@ def test_staged_fragments_like_the_am_handler(dt, op):
         ctx.close()
 
 
+@pytest.mark.parametrize("zcopy", [0, None, 1 << 20])
+def test_staged_runs_zero_copy_and_dma_counters(zcopy):
+    """Both flush paths of the fragment aggregator give the same bits, and the
+    counters tell them apart: runs of at most the zero-copy threshold are read
+    by the kernel from the pinned slot (counter 4, no DMA), larger ones are
+    copied H2D (counter 2, which also holds stage_begin's mirror copy).
+    zcopy: 0 = default 64 KiB, None = never, 1 MiB = every run."""
+    ctx = xucg_amd.DevContext(device=0, stage_bytes=64 << 10, stage_slots=3,
+                              zcopy_bytes=zcopy)
+    try:
+        n = 50_000 + 1          # 200 KiB: four 64 KiB slots, the last ragged
+        acc = O.fill("float32", "round", 5, n)
+        src = O.fill("float32", "round", 6, n)
+        host = acc.copy()
+        assert ctx.stage_begin(host, host.nbytes) == 0
+        frag = O.frag_length(256, 4)
+        for off in range(0, n * 4, frag):
+            cnt = min(frag, n * 4 - off) // 4
+            assert ctx.combine("sum", "float32", off, src[off // 4: off // 4 + cnt],
+                               cnt) == 0, _lib.last_error()
+        assert ctx.stage_end() == 0, _lib.last_error()
+        assert (bits(host) == bits(O.reduce("sum", "float32", src, acc))).all()
+        c = ctx.counters()
+        if zcopy is None:
+            assert c["zcopy_bytes"] == 0 and c["h2d_bytes"] == 2 * n * 4
+        else:
+            assert c["zcopy_bytes"] == n * 4 and c["h2d_bytes"] == n * 4
+        assert c["d2h_bytes"] == n * 4
+    finally:
+        ctx.close()
+
+
 def test_staged_contiguous_fragments_one_launch_per_slot():
     ctx = xucg_amd.DevContext(device=0, stage_bytes=1 << 20, stage_slots=2)
     try:
