@@ -13,9 +13,9 @@ cd "$ROOT"
     --showcomputepartition --showmemorypartition -c -P -t 2>/dev/null || true) \
     > "$OUT/smi_idle.txt"
 # clocks sampled while the ceiling probes stream 1 GiB operands
-( sleep 3; rocm-smi -c -P 2>/dev/null > "$OUT/smi_load.txt" || true ) &
+( sleep 1.5; rocm-smi -c -P 2>/dev/null > "$OUT/smi_load.txt" || true ) &
 sampler=$!
-TUNE_CEILING=1 timeout -k 10 120 ./tools/tune_combine 28 5 > "$OUT/tune_ceiling_1GiB.txt" 2>&1
+TUNE_CEILING=1 timeout -k 10 120 ./tools/tune_combine 28 40 > "$OUT/tune_ceiling_1GiB.txt" 2>&1
 rc=$?
 wait "$sampler"
 grep -E "Card SKU|Card Series|vendor|Max Graphics|Performance Level|sclk|mclk|fclk|Power \(W\)" \
