@@ -73,6 +73,28 @@ k_combine_flag(float *dst, const float *src, size_t nvec, unsigned *counter,
     }
 }
 
+/* a one-workgroup kernel queued behind any stream work (a combine, a D2H
+ * copy): stream order means everything before it has completed; the
+ * system-scope release makes the pinned word the host's completion signal */
+__global__ void __launch_bounds__(64) k_signal(unsigned *host_flag, unsigned seq)
+{
+    if (threadIdx.x == 0) {
+        __hip_atomic_store(host_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+static void spin_flag(volatile unsigned *flag, unsigned s, hipStream_t st, const char *who)
+{
+    long spins = 0;
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != s) {
+        if (++spins == (1L << 28)) {   /* seconds, not microseconds */
+            fprintf(stderr, "%s: flag %u never arrived\n", who, s);
+            (void)hipStreamSynchronize(st);
+            exit(2);
+        }
+    }
+}
+
 static double now_us()
 {
     return std::chrono::duration<double, std::micro>(
@@ -102,6 +124,8 @@ int main(int argc, char **argv)
     CHECK(hipMemset(counter, 0, sizeof(unsigned)));
     CHECK(hipHostMalloc((void**)&flag, sizeof(unsigned), hipHostMallocDefault));
     *flag = 0;
+    void *hbuf;
+    CHECK(hipHostMalloc(&hbuf, 256, hipHostMallocDefault));
     hipStream_t st;
     CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     hipEvent_t ev;
@@ -146,6 +170,30 @@ int main(int argc, char **argv)
                 exit(2);
             }
         }
+    }, {}});
+    ms.push_back({"sig    (launch + 1-WG signal kernel + spin on word)", [&]() {
+        const unsigned s = ++seq;
+        launch();
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, flag, s);
+        spin_flag(flag, s, st, "sig");
+    }, {}});
+    ms.push_back({"wv32   (launch + hipStreamWriteValue32 + spin on word)", [&]() {
+        const unsigned s = ++seq;
+        launch();
+        CHECK(hipStreamWriteValue32(st, flag, s, 0));
+        spin_flag(flag, s, st, "wv32");
+    }, {}});
+    ms.push_back({"d2hsig (launch + 256-B D2H + signal kernel + spin)", [&]() {
+        const unsigned s = ++seq;
+        launch();
+        CHECK(hipMemcpyAsync(hbuf, dst, 256, hipMemcpyDeviceToHost, st));
+        hipLaunchKernelGGL(k_signal, dim3(1), dim3(64), 0, st, flag, s);
+        spin_flag(flag, s, st, "d2hsig");
+    }, {}});
+    ms.push_back({"d2hsyn (launch + 256-B D2H + hipStreamSynchronize)", [&]() {
+        launch();
+        CHECK(hipMemcpyAsync(hbuf, dst, 256, hipMemcpyDeviceToHost, st));
+        CHECK(hipStreamSynchronize(st));
     }, {}});
     ms.push_back({"graph  (hipGraphLaunch + hipStreamSynchronize)", [&]() {
         CHECK(hipGraphLaunch(gexec, st));
