@@ -65,6 +65,8 @@ typedef struct ucg_builtin_combine_config {
     int      device;         /* UCX_BUILTIN_DEV_DEVICE       (default -1)      */
     size_t   zcopy_bytes;    /* UCX_BUILTIN_DEV_ZCOPY_BYTES  (default 64k;
                                 0, n, never: UCG_BUILTIN_DEV_ZCOPY_NEVER)      */
+    int      completion;     /* UCX_BUILTIN_DEV_COMPLETION   signal|sync (default
+                                signal: UCG_BUILTIN_DEV_COMPLETION_*)          */
 } ucg_builtin_combine_config_t;
 
 typedef struct ucg_builtin_combine ucg_builtin_combine_t;

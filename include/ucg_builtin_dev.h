@@ -151,10 +151,24 @@ typedef struct ucg_builtin_dev_ctx_params {
                               by the kernel from the pinned slot over PCIe,
                               with no H2D copy; 0 = 64 KiB,
                               UCG_BUILTIN_DEV_ZCOPY_NEVER = always copy */
+    int      completion;   /* how stage_end waits for the step's last launch
+                              (UCG_BUILTIN_DEV_COMPLETION_*; 0 = SIGNAL) */
 } ucg_builtin_dev_ctx_params_t;
 
 #define UCG_BUILTIN_DEV_ZCOPY_DEFAULT ((size_t)64 << 10)
 #define UCG_BUILTIN_DEV_ZCOPY_NEVER   ((size_t)-1)
+
+/* Completion wait of a staged step (ucg_builtin_dev_stage_end) whose result
+ * is in device memory or pinned host memory:
+ *   SIGNAL  a one-workgroup kernel queued behind the step publishes a sequence
+ *           number to a pinned host word with a system-scope release store;
+ *           the host spins on it (then blocks in hipStreamSynchronize if the
+ *           step runs longer than 200 us). 8.8-9.7 us per small step against
+ *           11.5-11.8 us (tools/tune_latency, profiles/r02/r02d).
+ *   SYNC    hipStreamSynchronize.
+ * A result copied back into pageable host memory always takes SYNC. */
+#define UCG_BUILTIN_DEV_COMPLETION_SIGNAL 1
+#define UCG_BUILTIN_DEV_COMPLETION_SYNC   2
 
 /* ---- introspection (no GPU needed) ---------------------------------------*/
 size_t      ucg_builtin_dev_dtype_size(ucg_dev_dtype_t dt);
@@ -317,8 +331,8 @@ ucs_status_t ucg_builtin_dev_profile_stream(ucg_builtin_dev_ctx_t *ctx, int kind
 /* Counters since ctx creation: [0] kernel launches, [1] bytes combined on the
  * device (3N basis), [2] H2D bytes copied by DMA (hipMemcpyAsync), [3] D2H
  * bytes, [4] staged bytes the kernel read from pinned host memory in place
- * (zero-copy runs, no DMA). */
-#define UCG_BUILTIN_DEV_NCOUNTERS 5
+ * (zero-copy runs, no DMA), [5] completion waits on the signal word. */
+#define UCG_BUILTIN_DEV_NCOUNTERS 6
 void         ucg_builtin_dev_counters(ucg_builtin_dev_ctx_t *ctx,
                                       uint64_t out[UCG_BUILTIN_DEV_NCOUNTERS]);
 

@@ -9,11 +9,13 @@
  *
  *   stage_bench [total_bytes] [frag_bytes] [reps]
  *
- * Two device contexts run side by side in one process: one with the default
- * zero-copy threshold (staged runs <= 64 KiB are read by the kernel from the
- * pinned slot) and one that always copies H2D. Every measurement alternates
- * between them rep by rep and reports the median of each, so the A/B is not
- * confounded by box phases (one run per setting is noise).
+ * Three device contexts run side by side in one process: the defaults
+ * (staged runs <= 64 KiB are read by the kernel from the pinned slot, and
+ * stage_end waits on the pinned completion word), one that always copies
+ * H2D, and one that waits with hipStreamSynchronize. Every measurement
+ * alternates between them rep by rep and reports the median of each, so the
+ * A/B is not confounded by box phases (one run per setting is
+ * noise).
  *
  * Prints one JSON line; exit 3 if a staged result differs from the oracle.
  */
@@ -85,7 +87,9 @@ static double small_steps(ucg_builtin_dev_ctx_t *ctx, void *d, const float *src,
 }
 
 #define MAXREPS 64
-enum { ZC = 0, COPY = 1 };   /* context index: zero-copy default / always copy */
+/* context index: defaults (zero-copy, completion word) / always copy /
+ * hipStreamSynchronize completion */
+enum { ZC = 0, COPY = 1, SYNC = 2, NCTX = 3 };
 
 int main(int argc, char **argv)
 {
@@ -93,7 +97,7 @@ int main(int argc, char **argv)
     size_t frag  = argc > 2 ? (size_t)atol(argv[2]) : 8184;
     int reps     = argc > 3 ? atoi(argv[3]) : 5;
     size_t n     = total / 4;
-    ucg_builtin_dev_ctx_t *ctx[2];
+    ucg_builtin_dev_ctx_t *ctx[NCTX];
     float *src, *dst, *want, *ref;
     double t0, t_step[2][MAXREPS], t_cpu[MAXREPS];
     int i, c, ok = 1;
@@ -101,9 +105,11 @@ int main(int argc, char **argv)
     reps = reps < 1 ? 1 : (reps > MAXREPS ? MAXREPS : reps);
     total = n * 4;
     frag -= frag % 4;
-    for (c = 0; c < 2; c++) {
+    for (c = 0; c < NCTX; c++) {
         ucg_builtin_dev_ctx_params_t prm = {0, NULL, 0, 0,
-                                            c == ZC ? 0 : UCG_BUILTIN_DEV_ZCOPY_NEVER};
+                                            c == COPY ? UCG_BUILTIN_DEV_ZCOPY_NEVER : 0,
+                                            c == SYNC ? UCG_BUILTIN_DEV_COMPLETION_SYNC :
+                                                        UCG_BUILTIN_DEV_COMPLETION_SIGNAL};
         if (ucg_builtin_dev_ctx_create(&prm, &ctx[c]) != UCS_OK) {
             fprintf(stderr, "ctx: %s\n", ucg_builtin_dev_last_error());
             return 1;
@@ -162,28 +168,28 @@ int main(int argc, char **argv)
      * context, plus a parity check of the last small step of each */
     const size_t small[3] = {256, 4096, 65536};
     const int sreps = 7;
-    double small_us[2][3], small_lo[2][3], small_hi[2][3];
+    double small_us[NCTX][3], small_lo[NCTX][3], small_hi[NCTX][3];
     {
         int j, r;
         for (j = 0; j < 3; j++) {
-            double v[2][7];
-            void *d[2];
-            for (c = 0; c < 2; c++) {
+            double v[NCTX][7];
+            void *d[NCTX];
+            for (c = 0; c < NCTX; c++) {
                 d[c] = ucg_builtin_dev_malloc(ctx[c], small[j]);
                 if (d[c] == NULL) {
                     return 5;
                 }
             }
             for (r = 0; r < sreps; r++) {
-                for (c = 0; c < 2; c++) {
-                    const int k = (r & 1) ? 1 - c : c;
+                for (c = 0; c < NCTX; c++) {
+                    const int k = (c + r) % NCTX;   /* rotate which goes first */
                     v[k][r] = small_steps(ctx[k], d[k], src, small[j], 400);
                     if (v[k][r] < 0) {
                         return 5;
                     }
                 }
             }
-            for (c = 0; c < 2; c++) {
+            for (c = 0; c < NCTX; c++) {
                 /* d[c] = ref + 421 steps of src (exact: counts of a float
                  * added to itself are compared against the oracle below) */
                 float *h = malloc(small[j]), *w = malloc(small[j]);
@@ -271,8 +277,11 @@ int main(int argc, char **argv)
                "\"65536\": %.2f}, "
                "\"small_step_us_device_recv_always_copy\": {\"256\": %.2f, "
                "\"4096\": %.2f, \"65536\": %.2f}, "
+               "\"small_step_us_device_recv_sync_completion\": {\"256\": %.2f, "
+               "\"4096\": %.2f, \"65536\": %.2f}, "
                "\"small_step_us_range\": {\"zcopy\": [[%.2f, %.2f], [%.2f, %.2f], "
-               "[%.2f, %.2f]], \"copy\": [[%.2f, %.2f], [%.2f, %.2f], [%.2f, %.2f]]}, "
+               "[%.2f, %.2f]], \"copy\": [[%.2f, %.2f], [%.2f, %.2f], [%.2f, %.2f]], "
+               "\"sync\": [[%.2f, %.2f], [%.2f, %.2f], [%.2f, %.2f]]}, "
                "\"small_step_timing\": \"median of %d alternating reps of 400 steps "
                "per context, one process\", \"floor_empty_step_us\": %.2f, "
                "\"floor_device_reduce_4k_plus_sync_us\": %.2f}\n",
@@ -285,13 +294,16 @@ int main(int argc, char **argv)
                mk_host_ns, mk_dev_ns,
                small_us[ZC][0], small_us[ZC][1], small_us[ZC][2],
                small_us[COPY][0], small_us[COPY][1], small_us[COPY][2],
+               small_us[SYNC][0], small_us[SYNC][1], small_us[SYNC][2],
                small_lo[ZC][0], small_hi[ZC][0], small_lo[ZC][1], small_hi[ZC][1],
                small_lo[ZC][2], small_hi[ZC][2],
                small_lo[COPY][0], small_hi[COPY][0], small_lo[COPY][1], small_hi[COPY][1],
-               small_lo[COPY][2], small_hi[COPY][2], sreps, floor_sync_us,
+               small_lo[COPY][2], small_hi[COPY][2],
+               small_lo[SYNC][0], small_hi[SYNC][0], small_lo[SYNC][1], small_hi[SYNC][1],
+               small_lo[SYNC][2], small_hi[SYNC][2], sreps, floor_sync_us,
                floor_launch_us);
     }
-    for (c = 0; c < 2; c++) {
+    for (c = 0; c < NCTX; c++) {
         ucg_builtin_dev_ctx_destroy(ctx[c]);
     }
     free(src);

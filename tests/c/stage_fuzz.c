@@ -2,7 +2,8 @@
  * stage_fuzz.c - row f1's fragment aggregator fuzzed from C against the
  * oracle: random dtype x op, step length, fragment size, number of
  * interleaved senders (a fan-in step with ep_cnt > 1), arrival order, recv
- * buffer kind (pageable host at any element offset, or device memory) and
+ * buffer kind (pageable or pinned host memory at any element offset, or
+ * device memory; the last two end their step on the completion word) and
  * staging ring geometry (small slots and shallow rings force the flush,
  * clash and slot-reuse paths of ucg_builtin_dev_combine).
  *
@@ -61,12 +62,14 @@ static int run_case(ucg_builtin_dev_ctx_t *ctx, int c, int *kinds)
     const size_t bytes   = count * sz;
     const unsigned nsend = (unsigned)rnd_in(1, 4);
     const size_t frag    = sz * rnd_in(1, rnd() % 2 ? 64 : 16384 / sz);
-    const int dev_recv   = rnd() % 3 == 0;
+    const int recv_kind  = (int)(rnd() % 3);   /* 0 pageable, 1 device, 2 pinned */
+    const int dev_recv   = recv_kind == 1;
     const size_t pad     = sz * rnd_in(0, 16 / sz + 1);  /* recv offset in elements */
     const int dist       = (int)rnd_in(0, ORA_DIST_LAST - 1);
     const int shuffle    = rnd() % 4 == 0;  /* reorder within a sender too */
     char **srcs = calloc(nsend, sizeof(*srcs));
-    char *host_acc = malloc(pad + bytes + 1);
+    char *host_acc = recv_kind == 2 ? ucg_builtin_dev_host_alloc(pad + bytes + 1)
+                                    : malloc(pad + bytes + 1);
     char *want = malloc(bytes + 1);
     char *got = malloc(bytes + 1);
     void *dbuf = NULL;
@@ -75,7 +78,11 @@ static int run_case(ucg_builtin_dev_ctx_t *ctx, int c, int *kinds)
     size_t *next = calloc(nsend, sizeof(*next));
     int ok = 1;
 
-    kinds[dev_recv]++;
+    if (host_acc == NULL) {
+        fprintf(stderr, "case %d: recv buffer: %s\n", c, ucg_builtin_dev_last_error());
+        return -1;
+    }
+    kinds[recv_kind]++;
     for (k = 0; k < nsend; k++) {
         srcs[k] = malloc(bytes + 1);
         ucg_oracle_fill(dt, dist, 0xF0220000ull + 97ull * c + k, srcs[k], count);
@@ -160,15 +167,19 @@ static int run_case(ucg_builtin_dev_ctx_t *ctx, int c, int *kinds)
         for (i = 0; i < bytes && got[i] == want[i]; i++) {
         }
         fprintf(stderr, "case %d MISMATCH: dt=%d op=%d count=%zu frag=%zu senders=%u "
-                "dev_recv=%d pad=%zu shuffle=%d first bad byte %zu\n", c, dt, op,
-                count, frag, nsend, dev_recv, pad, shuffle, i);
+                "recv_kind=%d pad=%zu shuffle=%d first bad byte %zu\n", c, dt, op,
+                count, frag, nsend, recv_kind, pad, shuffle, i);
         ok = 0;
     }
     for (k = 0; k < nsend; k++) {
         free(srcs[k]);
     }
     free(srcs);
-    free(host_acc);
+    if (recv_kind == 2) {
+        ucg_builtin_dev_host_free(host_acc);
+    } else {
+        free(host_acc);
+    }
     free(want);
     free(got);
     free(fr);
@@ -265,12 +276,16 @@ int main(int argc, char **argv)
     const size_t zcopy[]      = {0, 0, 0, UCG_BUILTIN_DEV_ZCOPY_NEVER,
                                  UCG_BUILTIN_DEV_ZCOPY_NEVER, UCG_BUILTIN_DEV_ZCOPY_NEVER};
     const int ngeo = 6;
-    int kinds[2] = {0, 0}, whole_kinds[3] = {0, 0, 0}, done = 0, whole = 0, g, c;
+    int kinds[3] = {0, 0, 0}, whole_kinds[3] = {0, 0, 0}, done = 0, whole = 0, g, c;
     int by_path[2] = {0, 0};
-    uint64_t zc_bytes = 0, dma_bytes = 0;
+    uint64_t zc_bytes = 0, dma_bytes = 0, signal_waits = 0;
 
     for (g = 0; g < ngeo; g++) {
-        ucg_builtin_dev_ctx_params_t prm = {0, NULL, slot_bytes[g], slots[g], zcopy[g]};
+        /* odd geometries wait with hipStreamSynchronize, even ones on the
+         * completion word: both stage_end paths are fuzzed */
+        ucg_builtin_dev_ctx_params_t prm = {0, NULL, slot_bytes[g], slots[g], zcopy[g],
+                                            (g & 1) ? UCG_BUILTIN_DEV_COMPLETION_SYNC :
+                                                      UCG_BUILTIN_DEV_COMPLETION_SIGNAL};
         ucg_builtin_dev_ctx_t *ctx;
         if (ucg_builtin_dev_ctx_create(&prm, &ctx) != UCS_OK) {
             fprintf(stderr, "ctx: %s\n", ucg_builtin_dev_last_error());
@@ -297,6 +312,12 @@ int main(int argc, char **argv)
             ucg_builtin_dev_counters(ctx, cnt);
             dma_bytes += cnt[2];
             zc_bytes  += cnt[4];
+            signal_waits += cnt[5];
+            if ((g & 1) && cnt[5] != 0) {
+                fprintf(stderr, "geometry %d: sync completion but %llu signal waits\n", g,
+                        (unsigned long long)cnt[5]);
+                return 3;
+            }
             if (zcopy[g] == UCG_BUILTIN_DEV_ZCOPY_NEVER && cnt[4] != 0) {
                 fprintf(stderr, "geometry %d: zero-copy off but %llu bytes read in "
                         "place\n", g, (unsigned long long)cnt[4]);
@@ -306,12 +327,13 @@ int main(int argc, char **argv)
         ucg_builtin_dev_ctx_destroy(ctx);
     }
     printf("{\"harness\": \"stage_fuzz\", \"cases\": %d, \"host_recv\": %d, "
-           "\"device_recv\": %d, \"whole_buffer\": %d, \"whole_operands\": "
+           "\"device_recv\": %d, \"pinned_recv\": %d, \"whole_buffer\": %d, \"whole_operands\": "
            "{\"pageable\": %d, \"pinned\": %d, \"device\": %d}, "
            "\"cases_zcopy_default\": %d, \"cases_zcopy_off\": %d, "
-           "\"h2d_dma_bytes\": %llu, \"zcopy_read_bytes\": %llu, \"bit_exact\": true}\n",
-           done, kinds[0], kinds[1], whole, whole_kinds[0], whole_kinds[1], whole_kinds[2],
+           "\"h2d_dma_bytes\": %llu, \"zcopy_read_bytes\": %llu, "
+           "\"stage_end_signal_waits\": %llu, \"bit_exact\": true}\n",
+           done, kinds[0], kinds[1], kinds[2], whole, whole_kinds[0], whole_kinds[1], whole_kinds[2],
            by_path[0], by_path[1], (unsigned long long)dma_bytes,
-           (unsigned long long)zc_bytes);
+           (unsigned long long)zc_bytes, (unsigned long long)signal_waits);
     return 0;
 }

@@ -259,6 +259,108 @@ def test_staged_runs_zero_copy_and_dma_counters(zcopy):
         ctx.close()
 
 
+@pytest.mark.parametrize("completion", ["signal", "sync"])
+@pytest.mark.parametrize("recv", ["device", "pinned", "pageable"])
+def test_stage_end_completion_word(completion, recv):
+    """stage_end's two completion waits give the same bits for every recv
+    buffer kind. With "signal" a device or pinned result is waited for on the
+    pinned completion word (counter 5 counts the waits); a pageable result is
+    always waited for by the runtime (its D2H may end in a host-side copy).
+    Steps of one fragment (the small-step floor) and of many, 3 steps each so
+    the sequence number advances and a stale word never passes for a new one."""
+    ctx = xucg_amd.DevContext(device=0, stage_bytes=64 << 10, stage_slots=3,
+                              completion=completion)
+    try:
+        for n in (64, 30_001):
+            acc = O.fill("float64", "round", 21, n)
+            srcs = [O.fill("float64", "round", 22 + k, n) for k in range(3)]
+            want = acc.copy()
+            hb = db = None
+            if recv == "device":
+                db = ctx.alloc(n * 8)
+                db.upload(acc)
+                target = db.ptr
+            elif recv == "pinned":
+                hb = xucg_amd.HostBuffer(n * 8)
+                hv = hb.view(np.float64, n)
+                hv[:] = acc
+                target = hb.ptr
+            else:
+                hv = acc.copy()
+                target = hv
+            before = ctx.counters()["signal_waits"]
+            frag = O.frag_length(8192, 8)
+            for src in srcs:
+                assert ctx.stage_begin(target, n * 8) == 0, _lib.last_error()
+                for off in range(0, n * 8, frag):
+                    cnt = min(frag, n * 8 - off) // 8
+                    piece = np.ascontiguousarray(src[off // 8: off // 8 + cnt])
+                    assert ctx.combine("sum", "float64", off, piece, cnt) == 0
+                assert ctx.stage_end() == 0, _lib.last_error()
+                want = O.reduce("sum", "float64", src, want)
+                got = db.download(np.float64, n) if db else hv.copy()
+                assert (bits(got) == bits(want)).all(), (n, recv, completion)
+            waits = ctx.counters()["signal_waits"] - before
+            expect = 3 if completion == "signal" and recv != "pageable" else 0
+            assert waits == expect, (waits, expect)
+            if hb:
+                hb.free()
+            if db:
+                db.free()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("completion", ["signal", "sync"])
+def test_whole_buffer_combine_inside_a_staged_step(completion):
+    """Another op of the group combines a whole host buffer (the per-fragment
+    path of a step that found the staging busy, builtin_ops.c) while a staged
+    step holds a pending run in a ring slot. The whole-buffer combine takes
+    ring slots and frees them all at its end; the staged run must have been
+    flushed first, or the step's next run lands in its slot and overwrites it."""
+    ctx = xucg_amd.DevContext(device=0, stage_bytes=4096, stage_slots=3,
+                              completion=completion)
+    try:
+        n = 2048
+        acc = O.fill("float32", "round", 31, n)
+        a = O.fill("float32", "round", 32, 256)
+        b = O.fill("float32", "round", 33, 256)
+        host = acc.copy()
+        assert ctx.stage_begin(host, host.nbytes) == 0
+        assert ctx.combine("sum", "float32", 0, a, 256) == 0          # run in slot 0
+        hs, hd0 = O.fill("float32", "round", 34, n), O.fill("float32", "round", 35, n)
+        hd = hd0.copy()
+        assert ctx.combine_host("sum", "float32", hd, hs, n) == 0, _lib.last_error()
+        assert ctx.combine("sum", "float32", 4096, b, 256) == 0       # a new run
+        assert ctx.stage_end() == 0, _lib.last_error()
+        want = acc.copy()
+        want[:256] = O.reduce("sum", "float32", a, want[:256])
+        want[1024:1280] = O.reduce("sum", "float32", b, want[1024:1280])
+        assert (bits(host) == bits(want)).all()
+        assert (bits(hd) == bits(O.reduce("sum", "float32", hs, hd0))).all()
+    finally:
+        ctx.close()
+
+
+def test_empty_staged_step_waits_for_nothing(dev_ctx):
+    """A step with no fragment queues nothing, and its stage_end returns at
+    once in either completion mode (no signal launch)."""
+    b = dev_ctx.alloc(4096)
+    before = dev_ctx.counters()["signal_waits"]
+    for _ in range(3):
+        assert dev_ctx.stage_begin(b, 4096) == 0
+        assert dev_ctx.stage_end() == 0
+    assert dev_ctx.counters()["signal_waits"] == before
+
+
+def test_completion_mode_rejects_unknown():
+    p = _lib.DevCtxParams(0, None, 0, 0, 0, 7)
+    import ctypes
+    h = ctypes.c_void_p()
+    assert _lib.dev().ucg_builtin_dev_ctx_create(ctypes.byref(p), ctypes.byref(h)) == \
+        xucg_amd.UCS_ERR_INVALID_PARAM
+
+
 def test_staged_contiguous_fragments_one_launch_per_slot():
     ctx = xucg_amd.DevContext(device=0, stage_bytes=1 << 20, stage_slots=2)
     try:

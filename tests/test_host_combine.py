@@ -49,6 +49,17 @@ def test_zcopy_threshold_parsed_as_memory_units(monkeypatch):
         assert host.read_config().zcopy_bytes == want, text
 
 
+def test_completion_mode_from_environment(monkeypatch):
+    """UCX_BUILTIN_DEV_COMPLETION: 'sync' selects hipStreamSynchronize in
+    stage_end; unset (or anything else) the completion word."""
+    from xucg_amd import _lib
+    monkeypatch.delenv("UCX_BUILTIN_DEV_COMPLETION", raising=False)
+    assert host.read_config().completion == _lib.COMPLETION["signal"]
+    for text, want in (("sync", "sync"), ("SYNC", "sync"), ("signal", "signal")):
+        monkeypatch.setenv("UCX_BUILTIN_DEV_COMPLETION", text)
+        assert host.read_config().completion == _lib.COMPLETION[want], text
+
+
 def test_classification_through_api_callbacks():
     mpi = MockMPI()
     cmb = host_only_combine(mpi)

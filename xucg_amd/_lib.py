@@ -49,11 +49,12 @@ _st = ctypes.c_int
 class DevCtxParams(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int), ("stream", ctypes.c_void_p),
                 ("stage_bytes", ctypes.c_size_t), ("stage_slots", ctypes.c_uint),
-                ("zcopy_bytes", ctypes.c_size_t)]
+                ("zcopy_bytes", ctypes.c_size_t), ("completion", ctypes.c_int)]
 
 
 ZCOPY_NEVER = (1 << 64) - 1   # UCG_BUILTIN_DEV_ZCOPY_NEVER
-NCOUNTERS = 5                 # UCG_BUILTIN_DEV_NCOUNTERS
+NCOUNTERS = 6                 # UCG_BUILTIN_DEV_NCOUNTERS
+COMPLETION = {"signal": 1, "sync": 2}   # UCG_BUILTIN_DEV_COMPLETION_*
 
 
 DEV_API = {

@@ -106,6 +106,12 @@ void ucg_builtin_combine_config_read(ucg_builtin_combine_config_t *cfg)
             cfg->zcopy_bytes = parse_memunits(z, UCG_BUILTIN_DEV_ZCOPY_DEFAULT);
         }
     }
+    {
+        /* how a staged step waits for its last launch (ucg_builtin_dev.h) */
+        const char *c = getenv("UCX_BUILTIN_DEV_COMPLETION");
+        cfg->completion = (c && !strcasecmp(c, "sync")) ? UCG_BUILTIN_DEV_COMPLETION_SYNC :
+                                                          UCG_BUILTIN_DEV_COMPLETION_SIGNAL;
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -137,7 +143,8 @@ ucs_status_t ucg_builtin_combine_create(const ucg_builtin_reduce_params_t *param
             .stream      = NULL,
             .stage_bytes = cmb->cfg.stage_bytes,
             .stage_slots = cmb->cfg.stage_slots,
-            .zcopy_bytes = cmb->cfg.zcopy_bytes
+            .zcopy_bytes = cmb->cfg.zcopy_bytes,
+            .completion  = cmb->cfg.completion
         };
         /* a device that fails to initialise is an error, not a silent
          * downgrade: the caller asked for the device path */

@@ -116,7 +116,7 @@ class DevContext:
     per-step device accumulator."""
 
     def __init__(self, device=-1, stream=None, stage_bytes=0, stage_slots=0,
-                 zcopy_bytes=0):
+                 zcopy_bytes=0, completion="signal"):
         if stream is not None and stream == 0:
             # the C ABI reads NULL as "create a stream": the legacy null stream
             # cannot be shared, and a private non-blocking stream would not be
@@ -126,7 +126,10 @@ class DevContext:
         L = _lib.dev()
         # zcopy_bytes: 0 = the library default (64 KiB), None = never
         zc = _lib.ZCOPY_NEVER if zcopy_bytes is None else zcopy_bytes
-        p = _lib.DevCtxParams(device, stream, stage_bytes, stage_slots, zc)
+        # completion: how stage_end waits ("signal": pinned completion word,
+        # "sync": hipStreamSynchronize)
+        p = _lib.DevCtxParams(device, stream, stage_bytes, stage_slots, zc,
+                              _lib.COMPLETION[completion])
         h = ctypes.c_void_p()
         check(L.ucg_builtin_dev_ctx_create(ctypes.byref(p), ctypes.byref(h)),
               "ucg_builtin_dev_ctx_create")
@@ -273,4 +276,4 @@ class DevContext:
         out = (ctypes.c_uint64 * _lib.NCOUNTERS)()
         _lib.dev().ucg_builtin_dev_counters(self.handle, out)
         return {"launches": out[0], "combined_bytes": out[1], "h2d_bytes": out[2],
-                "d2h_bytes": out[3], "zcopy_bytes": out[4]}
+                "d2h_bytes": out[3], "zcopy_bytes": out[4], "signal_waits": out[5]}

@@ -38,10 +38,12 @@ def read_config():
 
 
 def make_config(dev_enable=1, dev_min_bytes=1 << 20, stage_bytes=8 << 20,
-                stage_slots=4, device=-1, zcopy_bytes=0):
-    """zcopy_bytes: 0 = the device library's default (64 KiB), None = never"""
+                stage_slots=4, device=-1, zcopy_bytes=0, completion="signal"):
+    """zcopy_bytes: 0 = the device library's default (64 KiB), None = never;
+    completion: "signal" (pinned completion word) or "sync" (stage_end)"""
     zc = _lib.ZCOPY_NEVER if zcopy_bytes is None else zcopy_bytes
-    return CombineConfig(dev_enable, dev_min_bytes, stage_bytes, stage_slots, device, zc)
+    return CombineConfig(dev_enable, dev_min_bytes, stage_bytes, stage_slots, device, zc,
+                         _lib.COMPLETION[completion])
 
 
 class BuiltinCombine:
