@@ -90,6 +90,40 @@ void         ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *iface);
 typedef struct ucg_builtin_lgroup ucg_builtin_lgroup_t;
 typedef struct ucg_builtin_lcoll  ucg_builtin_lcoll_t;
 
+/* Member distances, the values of enum ucg_group_member_distance
+ * (api/ucg.h:253-264). */
+#define UCG_BUILTIN_DISTANCE_SELF   0
+#define UCG_BUILTIN_DISTANCE_CACHE  1
+#define UCG_BUILTIN_DISTANCE_SOCKET 7
+#define UCG_BUILTIN_DISTANCE_HOST   15
+#define UCG_BUILTIN_DISTANCE_NET    253
+
+/* The group's placement and the planner's tree/recursive knobs
+ * (ucg_group_params_t.distance, api/ucg.h:304-324; the BUILTIN_TREE_ and
+ * BUILTIN_RECURSIVE_ config tables, builtin/builtin.c:33-39,
+ * builtin/plan/builtin_tree.c:18-29, builtin_recursive.c:13-18).
+ *   distance    member_count entries as seen by this member (distance[my] =
+ *               SELF), NULL = every other member at HOST (one host). Members
+ *               of a host carry consecutive indices and every host the same
+ *               number of them (the reference's "by node" allocation,
+ *               builtin_tree.c:397-405); other layouts are UCS_ERR_UNSUPPORTED.
+ *               The transport stays the shared-memory one: a NET distance
+ *               changes the plan, not the wire, so multi-host plans run on
+ *               one machine.
+ *   tree_radix  UCX_BUILTIN_TREE_RADIX (0 = environment, else 8): fan-out of
+ *               the inter-host tree
+ *   sock_thresh UCX_BUILTIN_TREE_SOCKET_LEVEL_PPN_THRESH (0 = environment,
+ *               else 16): from this many members per host on, SOCKET
+ *               distances make a second intra-host tree level
+ *   recursive_factor UCX_BUILTIN_RECURSIVE_FACTOR (0 = environment, else 2):
+ *               the K of recursive K-ing */
+typedef struct ucg_builtin_lgroup_params {
+    const uint8_t *distance;
+    unsigned       tree_radix;
+    unsigned       sock_thresh;
+    unsigned       recursive_factor;
+} ucg_builtin_lgroup_params_t;
+
 /* group_id must be non-zero (builtin_control.c:645); `combine` is the
  * per-group combine state and stays owned by the caller. */
 ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
@@ -97,23 +131,41 @@ ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
                                        unsigned my_index,
                                        ucg_builtin_combine_t *combine,
                                        ucg_builtin_lgroup_t **group_p);
+/* The same with a placement and planner knobs (NULL params = the call
+ * above). */
+ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
+                                          uint16_t group_id, unsigned member_count,
+                                          unsigned my_index,
+                                          ucg_builtin_combine_t *combine,
+                                          const ucg_builtin_lgroup_params_t *params,
+                                          ucg_builtin_lgroup_t **group_p);
 void         ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *group);
 /* Progress the transport and any pending resends of this group's ops. */
 unsigned     ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *group);
 
-/* MPI_Allreduce (modifiers AGGREGATE|BROADCAST, api/ucg_mpi.h:53-54):
- * recursive doubling when member_count is a power of two, otherwise the tree
- * fan-in to member 0 followed by its fan-out (ucg_builtin_choose_topology,
- * builtin/builtin.c:112-121; UCX_BUILTIN_ALLREDUCE_PLAN=tree|recursive
- * overrides, a knob of this build). sbuf == rbuf means in place. The op is
- * reusable (persistent). */
+/* MPI_Allreduce (modifiers AGGREGATE|BROADCAST, api/ucg_mpi.h:53-54), the
+ * plan ucg_builtin_choose_topology picks (builtin/builtin.c:112-121):
+ *  - member_count a power of two: the recursive plan (builtin_recursive.c:
+ *    20-228): recursive K-ing over the hosts' masters (peers my^... for K=2,
+ *    K-1 peers per step otherwise), wrapped in an intra-host fan-in/fan-out
+ *    when a host has several members; one host whose size is not a power of
+ *    K falls back to the intra-host tree; several hosts whose number is not
+ *    a power of K are UCS_ERR_UNSUPPORTED (:77-88).
+ *  - otherwise the tree (builtin_tree.c:441-523): intra-host fan-in to each
+ *    host's master (two levels from sock_thresh members per host), the
+ *    inter-host tree of `tree_radix` over the masters, and the fan-out back.
+ * UCX_BUILTIN_ALLREDUCE_PLAN=tree|recursive overrides the choice (a knob of
+ * this build). sbuf == rbuf means in place. The op is reusable (persistent). */
 ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *group,
                                          const void *sbuf, void *rbuf,
                                          int count, void *dtype, void *op,
                                          ucg_builtin_lcoll_t **coll_p);
-/* MPI_Reduce (AGGREGATE|SINGLE_DESTINATION, api/ucg_mpi.h:41-42, 156): fan-in to
- * `root`, whose rbuf receives the result; rbuf is not touched (may be NULL)
- * on the other members. */
+/* MPI_Reduce (AGGREGATE|SINGLE_DESTINATION, api/ucg_mpi.h:41-42, 156): the
+ * tree's fan-in to `root`, whose rbuf receives the result; rbuf is not
+ * touched (may be NULL) on the other members - a member that combines on
+ * the way (a host master, a waypoint) uses a buffer of the op's own. A root
+ * other than 0 takes the tree built for root 0 with its host moved to the
+ * front and the root to the front of its host. */
 ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *group,
                                       const void *sbuf, void *rbuf,
                                       int count, void *dtype, void *op,

@@ -1,0 +1,157 @@
+"""One member of a multi-process collective on a placement (hosts, sockets)
+through the builtin operation engine: the plan the engine builds is checked
+against the oracle's restatement (oracle/plans.py), then allreduce and
+reduce to several roots run and are checked against the oracle's simulation
+of every member's plan.
+
+    _worker_topo.py <shm-name> <mode: host|dev> <max_short> <n:ppn:socket:radix:factor:thresh>
+
+socket = 0 means no socket level. The transport is the shared-memory one
+for every member: a NET distance changes the plan, not the wire.
+
+Checks:
+  - the plan: every step's method, step index, send and receive peers (in
+    order) equal the oracle's; a layout the oracle rejects is
+    UCS_ERR_UNSUPPORTED at create;
+  - integer types, every op, and fp SUM of exact integers: bit-exact against
+    the oracle's simulation (arrival order does not change these results);
+  - fp SUM of rounded values: within the SURVEY 8c-style relative bound of
+    the fp64 sum, and "digest" lines so the test can check that every member
+    of an allreduce holds identical bits."""
+import hashlib
+import os
+import re
+import sys
+
+import numpy as np
+
+from oracle import oracle as O
+from oracle import plans as P
+from xucg_amd import host, ops
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from mock_mpi import MockMPI, OPS, DTYPES, op_classifier, dt_classifier  # noqa: E402
+
+UCS_ERR_UNSUPPORTED = -22
+CASES = [("int32", "sum", 3001), ("uint8", "bxor", 777), ("int64", "max", 257),
+         ("float64", "sum", 1500), ("uint32", "sum", 64), ("int16", "prod", 33)]
+STEP_RE = re.compile(r"Step #\d+ \(step_idx (\d+)\): (\w+)"
+                     r"(?:, send (?:send|recv)\.buffer to ([\d ]+))?"
+                     r"(?:, receive from ([\d ]+))?"
+                     r"(?:, then send recv\.buffer to ([\d ]+))?")
+
+
+def parse(text):
+    out = []
+    for m in STEP_RE.finditer(text):
+        step, method, s1, r, s2 = m.groups()
+        send = s1 or s2 or ""
+        out.append((method, int(step), [int(x) for x in send.split()],
+                    [int(x) for x in (r or "").split()]))
+    return out
+
+
+def digest(a):
+    return hashlib.sha1(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()[:16]
+
+
+def main():
+    name, mode, max_short = sys.argv[1], sys.argv[2], int(sys.argv[3])
+    n, ppn, socket, radix, factor, thresh = map(int, sys.argv[4].split(":"))
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    assert world == n
+    mpi = MockMPI()
+    cfg = (host.make_config(dev_enable=2, dev_min_bytes=0, stage_bytes=1 << 16)
+           if mode == "dev" else host.make_config(dev_enable=0))
+    cmb = host.BuiltinCombine(mpi.callbacks(), cfg, op_classifier=op_classifier,
+                              dt_classifier=dt_classifier)
+    if mode == "dev" and not cmb.has_device:
+        print("no device", flush=True)
+        sys.exit(2)
+    iface = ops.ShmIface(name, n, rank, max_short=max_short, ring_cells=16)
+    dist = ops.layout_distances(n, rank, ppn, socket or None)
+    assert dist == P.layout(n, rank, ppn, socket or None)
+    group = ops.Group(iface, 5, n, rank, cmb, distance=dist, radix=radix,
+                      sock_thresh=thresh, factor=factor)
+    cfgkw = dict(ppn=ppn, socket=socket or None, radix=radix, factor=factor,
+                 sock_thresh=thresh)
+    rc = 0
+
+    def fail(msg):
+        nonlocal rc
+        print(f"rank {rank}: MISMATCH {msg}", flush=True)
+        rc = 1
+
+    kinds = [("allreduce", 0)] + [("reduce", r) for r in sorted({0, n - 1, n // 2})]
+    for ci, (dt, op, count) in enumerate(CASES):
+        dist_kind = "exact" if dt.startswith("float") else "round"
+        inputs = [O.fill(dt, dist_kind, 5000 + 31 * ci + m, count) for m in range(n)]
+        for kind, root in kinds:
+            try:
+                want = P.simulate(kind, op, dt, inputs, root=root, **cfgkw)
+                oplan = P.plan(kind, n, rank, root=root, **cfgkw)
+            except P.Unsupported:
+                want = oplan = None
+            sbuf = inputs[rank].copy()
+            rbuf = np.zeros_like(sbuf) if (kind == "allreduce" or rank == root) else None
+            coll = (group.allreduce(sbuf, rbuf, count, DTYPES[dt], OPS[op]) if kind == "allreduce"
+                    else group.reduce(sbuf, rbuf, count, DTYPES[dt], OPS[op], root))
+            if oplan is None:
+                if coll.status != UCS_ERR_UNSUPPORTED:
+                    fail(f"{kind} root={root}: oracle rejects the layout, create gave "
+                         f"{coll.status}")
+                coll.close()
+                continue
+            if coll.status != 0:
+                fail(f"{kind} root={root}: create failed {coll.status}")
+                continue
+            if ci == 0:
+                text = coll.describe()
+                got = parse(text)
+                exp = [(p["method"], p["step"], p["send"], p["recv"]) for p in oplan[2]]
+                if got != exp:
+                    fail(f"{kind} root={root} plan\n engine {got}\n oracle {exp}\n{text}")
+                if kind == "allreduce" or root == n - 1:
+                    print(f"describe {kind} root={root}:\n{text}", flush=True)
+            st = coll.run()
+            if st != 0:
+                fail(f"{kind} {dt} {op} root={root} status={st}")
+            elif rbuf is not None and not (O.bits(rbuf) == O.bits(want[rank])).all():
+                fail(f"{kind} {dt} {op} n={count} root={root}")
+            if not (O.bits(sbuf) == O.bits(inputs[rank])).all():
+                fail(f"{kind} {dt} {op}: send buffer modified")
+            coll.close()
+
+    # rounded fp32: tolerance against the fp64 sum, digests for identity
+    for ci, count in enumerate((4096, 1000)):
+        xs = [O.fill("float32", "round", 7000 + 11 * ci + m, count) for m in range(n)]
+        f64 = np.sum([x.astype(np.float64) for x in xs], axis=0)
+        scale = np.sum([np.abs(x.astype(np.float64)) for x in xs], axis=0)
+        rbuf = np.zeros(count, np.float32)
+        sbuf = xs[rank].copy()           # the op keeps the address: keep it alive
+        coll = group.allreduce(sbuf, rbuf, count, DTYPES["float32"], OPS["sum"])
+        if coll.status == UCS_ERR_UNSUPPORTED:
+            coll.close()
+            continue
+        st = coll.run()
+        tol = 2 * (n - 1) * 2.0 ** -24 * scale + 1e-30
+        err = np.abs(rbuf.astype(np.float64) - f64)
+        if st != 0 or not (err <= tol).all():
+            i = int(np.argmax(err / tol))
+            fail(f"allreduce float32 round n={count} status={st}: element {i} "
+                 f"{rbuf[i]!r} vs {f64[i]!r} (error {err[i] / tol[i]:.3g} x the bound)")
+        print(f"digest r{ci} {digest(rbuf)}", flush=True)
+        coll.close()
+    if rank == 0:
+        print(f"stats {group.stats()} combine {cmb.stats()}", flush=True)
+    group.close()
+    iface.close()
+    cmb.close()
+    if rc == 0:
+        print(f"rank {rank}: ok", flush=True)
+    sys.exit(rc)
+
+
+if __name__ == "__main__":
+    main()

@@ -6,6 +6,9 @@
  *   RANK=r WORLD_SIZE=n c1_allreduce <shm-name> [iters] [max_short] [count]
  *
  * C1_DEVICE_STAGING=1 forces every combine onto the GPU (staged steps).
+ * C1_PPN=p [C1_SOCKET=s] places the members on hosts of p consecutive
+ * members (sockets of s) through ucg_builtin_lgroup_create_ex; the planner
+ * knobs come from the environment (UCX_BUILTIN_TREE_RADIX, ...).
  *
  * The "MPI library" behind reduce_cb_f is a plain C loop with MPI's operand
  * order (inoutvec[i] = invec[i] + inoutvec[i]); inputs are exact integers so
@@ -66,7 +69,9 @@ int main(int argc, char **argv)
     ucg_builtin_lcoll_t *c;
     float **inputs, *out, *want;
     unsigned r;
-    int i, ok;
+    int i, ok, placed;
+    uint8_t dist[UCG_BUILTIN_OPS_MAX_MEMBERS];
+    ucg_builtin_lgroup_params_t gp = {NULL, 0, 0, 0};
     double t0, us;
 
     if (getenv("C1_DEVICE_STAGING")) {
@@ -76,9 +81,21 @@ int main(int argc, char **argv)
         cfg.dev_enable    = 2;
         cfg.dev_min_bytes = 0;
     }
+    {
+        const char *pp = getenv("C1_PPN"), *ps = getenv("C1_SOCKET");
+        unsigned ppn = pp ? (unsigned)atoi(pp) : world, sock = ps ? (unsigned)atoi(ps) : 0;
+        for (r = 0; r < world && r < UCG_BUILTIN_OPS_MAX_MEMBERS; r++) {
+            dist[r] = (r == rank) ? UCG_BUILTIN_DISTANCE_SELF :
+                      (r / ppn != rank / ppn) ? UCG_BUILTIN_DISTANCE_NET :
+                      (sock && r / sock != rank / sock) ? UCG_BUILTIN_DISTANCE_HOST :
+                      sock ? UCG_BUILTIN_DISTANCE_SOCKET : UCG_BUILTIN_DISTANCE_HOST;
+        }
+        placed = (pp != NULL || ps != NULL);
+    }
+    gp.distance = placed ? dist : NULL;
     if (ucg_builtin_combine_create(&rp, &cfg, &cmb) != UCS_OK ||
         ucg_builtin_shm_iface_open(name, world, rank, max_short, 64, &iface) != UCS_OK ||
-        ucg_builtin_lgroup_create(iface, 1, world, rank, cmb, &g) != UCS_OK) {
+        ucg_builtin_lgroup_create_ex(iface, 1, world, rank, cmb, &gp, &g) != UCS_OK) {
         fprintf(stderr, "rank %u: set-up failed\n", rank);
         return 1;
     }
@@ -89,10 +106,11 @@ int main(int argc, char **argv)
     }
     out  = calloc(count, sizeof(float));
     want = calloc(count, sizeof(float));
-    if ((world & (world - 1)) == 0 && !getenv("UCX_BUILTIN_ALLREDUCE_PLAN")) {
+    if ((world & (world - 1)) == 0 && !getenv("UCX_BUILTIN_ALLREDUCE_PLAN") && !placed) {
         ucg_oracle_reduce_multi(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
                                 world, rank, count);
-    } else {   /* tree plan; exact inputs make the arrival order irrelevant */
+    } else {   /* tree or multi-level plans; exact inputs make the
+                * association (and arrival order) irrelevant */
         ucg_oracle_tree_reduce(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
                                world, 0, NULL, count);
     }

@@ -44,10 +44,11 @@ def test_c1_harness_bit_exact(max_short, world):
     assert line["bit_exact"] and line["ranks"] == world and line["bytes"] == 4096
 
 
-@pytest.mark.parametrize("world,max_short,plan,incast", [
-    (4, 256, "", ""), (3, 256, "", ""), (8, 100, "", ""),
-    (4, 256, "tree", "1"), (5, 64, "tree", "")])
-def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast):
+@pytest.mark.parametrize("world,max_short,plan,incast,place", [
+    (4, 256, "", "", ""), (3, 256, "", "", ""), (8, 100, "", "", ""),
+    (4, 256, "tree", "1", ""), (5, 64, "tree", "", ""),
+    (8, 256, "", "", "4"), (12, 100, "", "", "3"), (8, 256, "tree", "1", "8:4")])
+def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast, place):
     """The host engine (libucg_builtin.so sources) and the C1 harness rebuilt
     with ASan + UBSan (tests/c/Makefile, target asan): recursive and tree
     plans, fragmenting and resend-heavy sizes, the incast fan-in. Any
@@ -63,6 +64,16 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast)
         monkeypatch.setenv("UCX_BUILTIN_ALLREDUCE_PLAN", plan)
     if incast:
         monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", incast)
+    if place:
+        # placements (test_topology.py): hosts of C1_PPN, sockets of
+        # C1_SOCKET; radix 2 so 4 hosts of 3 have an inter-host waypoint, and
+        # a socket level from 4 members per host on
+        ppn, _, sock = place.partition(":")
+        monkeypatch.setenv("C1_PPN", ppn)
+        if sock:
+            monkeypatch.setenv("C1_SOCKET", sock)
+        monkeypatch.setenv("UCX_BUILTIN_TREE_RADIX", "2")
+        monkeypatch.setenv("UCX_BUILTIN_TREE_SOCKET_LEVEL_PPN_THRESH", "4")
     codes, outs = launch_exe(exe, world, (shm_name(), 200, max_short))
     assert codes == [0] * world, "\n".join(outs)
     for out in outs:

@@ -1,0 +1,151 @@
+"""Placements (hosts, sockets) and the planner's knobs: the reference's tree
+and recursive plans beyond one flat host, built by
+the operation engine and checked against the oracle's restatement
+(oracle/plans.py) and its simulation of every member's plan."""
+import os
+import uuid
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle import plans as P
+from xucg_amd import host, ops
+from _launch import launch
+from mock_mpi import MockMPI, OPS, DTYPES
+
+
+def shm_name():
+    return f"ucg_topo_{os.getpid()}_{uuid.uuid4().hex[:8]}"
+
+
+def test_oracle_plans_fit_together():
+    """Every member's restated plan sends exactly what its peers expect, and
+    the simulation of all of them yields the full reduction, over hosts of
+    every size dividing the group, 0-2 socket levels, radix 2/3/8 and
+    factors 2/3/4. The only layouts without a plan are the reference's:
+    several hosts whose number is not a power of the factor
+    (builtin_recursive.c:83-87) and two-level host trees of more than two
+    sockets (builtin_tree.c:336-351)."""
+    done = rejected = 0
+    for n in range(2, 25):
+        for ppn in [p for p in range(1, n + 1) if n % p == 0]:
+            for socket in [None] + [s for s in (2, 4) if ppn % s == 0 and s < ppn]:
+                for radix, factor in ((2, 2), (3, 3), (8, 4), (8, 2)):
+                    for kind, root in (("allreduce", 0), ("reduce", 0), ("reduce", n - 1)):
+                        xs = [O.fill("int64", "round", 31 * m + n, 5) for m in range(n)]
+                        try:
+                            out = P.simulate(kind, "sum", "int64", xs, root=root, ppn=ppn,
+                                             socket=socket, radix=radix, factor=factor,
+                                             sock_thresh=4)
+                        except P.Unsupported as e:
+                            rejected += 1
+                            hosts_bad = "power of the factor" in str(e)
+                            sockets_bad = socket and ppn >= 4 and ppn // socket > 2
+                            assert hosts_bad or sockets_bad, (n, ppn, socket, kind, str(e))
+                            continue
+                        want = np.sum(np.array(xs, dtype=np.int64), axis=0)  # wraps like int64
+                        for m, o in enumerate(out):
+                            if o is not None:
+                                assert (o == want).all(), (n, ppn, socket, radix, factor,
+                                                           kind, root, m)
+                        done += 1
+    assert done > 1000 and rejected > 50, (done, rejected)
+
+
+def test_oracle_restates_reference_examples():
+    """Hand-checked plans: 2 hosts of 4 (recursive doubling between the
+    masters 0 and 4 inside the host fan-in/fan-out), and 4 hosts of 3 with
+    radix 2 (member 6 is a waypoint of the inter-host tree)."""
+    name, _, ph = P.plan("allreduce", 8, 4, ppn=4)
+    assert name == "recursive"
+    assert [(p["method"], p["step"], p["send"], p["recv"]) for p in ph] == [
+        ("REDUCE_TERMINAL", 1, [], [5, 6, 7]),
+        ("REDUCE_RECURSIVE", 2, [0], [0]),
+        ("SEND_TERMINAL", 5, [5, 6, 7], [])]
+    name, _, ph = P.plan("allreduce", 8, 6, ppn=4)
+    assert [(p["method"], p["step"]) for p in ph] == [("SEND_TO_SM_ROOT", 1),
+                                                      ("RECV_TERMINAL", 5)]
+    _, _, ph = P.plan("allreduce", 12, 6, ppn=3, radix=2)
+    assert [(p["method"], p["step"], p["send"], p["recv"]) for p in ph] == [
+        ("REDUCE_TERMINAL", 1, [], [7, 8]),
+        ("REDUCE_WAYPOINT", 2, [0], [9]),
+        ("BCAST_WAYPOINT", 3, [9], [0]),
+        ("SEND_TERMINAL", 4, [7, 8], [])]
+    # K-ing with K = 4 on 16 members of one host: peers my + j * 4^k
+    _, _, ph = P.plan("allreduce", 16, 5, factor=4)
+    assert [p["send"] for p in ph] == [[6, 7, 4], [9, 13, 1]]
+
+
+# n:ppn:socket:radix:factor:sock_thresh
+LAYOUTS = [
+    "8:4:0:8:2:16",     # 2 hosts: host fan-in, recursive doubling of masters, fan-out
+    "12:3:0:2:2:16",    # 4 hosts, radix 2: an inter-host waypoint (REDUCE/BCAST)
+    "6:2:0:8:2:16",     # 3 hosts: inter-host tree (non-power-of-two allreduce)
+    "8:8:4:8:2:4",      # one host, two sockets: socket masters are waypoints
+    "16:16:0:8:4:16",   # recursive K-ing, K = 4, 2 steps of 3 peers
+    "16:4:0:8:4:16",    # 4 hosts, K = 4 over the masters
+    "8:4:0:8:4:16",     # 2 hosts, K = 4: UCS_ERR_UNSUPPORTED (the reference's rule)
+    "12:12:4:8:2:4",    # 3 sockets at two levels: UCS_ERR_UNSUPPORTED
+    "5:1:0:2:2:16",     # every member its own host, radix 2: a 3-level tree
+]
+
+
+def _digests(outs):
+    return [sorted(ln for ln in out.splitlines() if ln.startswith("digest")) for out in outs]
+
+
+@pytest.mark.parametrize("spec", LAYOUTS)
+def test_engine_placements_host(spec):
+    """Every member's plan equals the oracle's, results equal the oracle's
+    simulation (bit-exact for integers and exact floats), rounded fp32 sums
+    are within the bound. Trees end with the root's bits everywhere and
+    recursive doubling pairs the same operands on both sides, so every member
+    holds identical bits; recursive K-ing with K > 2 combines the K-1
+    incoming messages in each member's own arrival order, so its members may
+    differ in the last bits (as in the reference) and only the bound holds."""
+    n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "host", 256, spec),
+                         timeout=300)
+    assert codes == [0] * n, "\n".join(outs)
+    d = _digests(outs)
+    if factor == 2:
+        assert all(x == d[0] for x in d), d
+
+
+def test_engine_rejects_bad_distance_arrays():
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    iface = ops.ShmIface(shm_name(), 1, 0, max_short=256)
+    with pytest.raises(Exception):
+        ops.Group(iface, 3, 1, 0, cmb, distance=[15])      # distance[my] must be SELF
+    with pytest.raises(Exception):
+        ops.Group(iface, 3, 1, 0, cmb, distance=[254])     # FAULT is not a placement
+    g = ops.Group(iface, 3, 1, 0, cmb, distance=[0], factor=4)
+    x = np.arange(16, dtype=np.int32)
+    y = np.zeros_like(x)
+    c = g.allreduce(x, y, 16, DTYPES["int32"], OPS["sum"])
+    assert c.status == 0 and c.run() == 0 and (y == x).all()
+    c.close()
+    g.close()
+    iface.close()
+    cmb.close()
+
+
+def test_layout_distances_match_oracle():
+    for n, ppn, socket in ((8, 4, None), (16, 8, 4), (6, 3, None), (4, 4, 2)):
+        for m in range(n):
+            assert ops.layout_distances(n, m, ppn, socket) == P.layout(n, m, ppn, socket)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec", ["12:3:0:2:2:16", "8:8:4:8:2:4", "8:4:0:8:2:16"])
+def test_engine_placements_device_staging(spec):
+    """The same plans with every REDUCE step (waypoints included) staged on
+    the GPU."""
+    n = int(spec.split(":")[0])   # factor 2 in every layout here: identical bits
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "dev", 256, spec),
+                         timeout=300)
+    assert codes == [0] * n, "\n".join(outs)
+    d = _digests(outs)
+    assert all(x == d[0] for x in d), d

@@ -403,16 +403,20 @@ typedef union {
 
 _Static_assert(sizeof(ops_header_t) == 8, "wire header is 8 bytes");
 
-#define OPS_MAX_STEPS 8
+#define OPS_MAX_STEPS 12
 
-/* the plan methods this engine runs (builtin/plan/builtin_plan.h), and the
- * aggregation each receive applies (builtin_control.c:960-972) */
+/* the plan methods this engine runs (builtin/plan/builtin_plan.h:28-44), and
+ * the aggregation each receive applies (builtin_control.c:960-972) */
 typedef enum {
-    M_REDUCE_RECURSIVE,   /* send to the partner, then receive and reduce */
+    M_REDUCE_RECURSIVE,   /* send to the step's peers, receive and reduce */
     M_REDUCE_TERMINAL,    /* tree root: receive from every child and reduce */
     M_SEND_TO_SM_ROOT,    /* tree leaf, fan-in (ppn > 2) */
     M_SEND_TERMINAL,      /* tree leaf fan-in at ppn == 2, root fan-out */
-    M_RECV_TERMINAL       /* tree leaf, fan-out: receive the result */
+    M_RECV_TERMINAL,      /* tree leaf, fan-out: receive the result */
+    M_REDUCE_WAYPOINT,    /* receive from the children and reduce, then send
+                             the accumulator to the parent */
+    M_BCAST_WAYPOINT      /* receive from the parent, then send to the
+                             children */
 } op_method_t;
 
 typedef enum { AGG_NOP, AGG_REDUCE, AGG_WRITE } op_aggregation_t;
@@ -424,7 +428,7 @@ static const char *const packer_name[] = {"copy", "reducing", "atomic"};
 
 static const char *const method_name[] = {
     "REDUCE_RECURSIVE", "REDUCE_TERMINAL", "SEND_TO_SM_ROOT", "SEND_TERMINAL",
-    "RECV_TERMINAL"
+    "RECV_TERMINAL", "REDUCE_WAYPOINT", "BCAST_WAYPOINT"
 };
 
 typedef struct {
@@ -436,6 +440,10 @@ typedef struct {
     unsigned    recv_cnt;         /* endpoints received from */
     unsigned    recv_peers[UCG_BUILTIN_OPS_MAX_MEMBERS];  /* describe only */
     int         send_recv_buffer; /* 0: send.buffer, 1: recv.buffer */
+    int         recv_first;       /* *_WAYPOINT: every receive of the step
+                                     before its sends (RECV_BEFORE_SEND1 /
+                                     RECV1_BEFORE_SEND, builtin_control.c:
+                                     379-389) */
     int         incast;           /* sends / receives go through the incast */
     uint8_t     packer;           /* op_packer_t of an incast send */
     unsigned    incast_expected;  /* children packing each incast message */
@@ -460,6 +468,11 @@ struct ucg_builtin_lgroup {
     uint8_t                  next_coll_id;
     int                      incast;   /* UCX_BUILTIN_SM_INCAST */
     uint64_t                 stats[4];
+    /* placement and planner knobs (ucg_builtin_lgroup_params_t) */
+    uint8_t                  distance[UCG_BUILTIN_OPS_MAX_MEMBERS];
+    unsigned                 radix;
+    unsigned                 sock_thresh;
+    unsigned                 factor;
 };
 
 struct ucg_builtin_lcoll {
@@ -471,8 +484,11 @@ struct ucg_builtin_lcoll {
     void        *op;
     size_t       dt_len;
     size_t       length;
-    const char  *plan;            /* "recursive doubling" / "tree" */
+    const char  *plan;            /* "recursive doubling" / "tree" / ... */
     int          kind;            /* 0 allreduce, 1 reduce */
+    char        *scratch;         /* accumulator of a non-root member that
+                                     combines in a reduce (rbuf then points
+                                     here) */
     unsigned     root;
     int          init_reduce;     /* ucg_builtin_init_reduce on start */
     op_step_t    steps[OPS_MAX_STEPS];
@@ -487,6 +503,7 @@ struct ucg_builtin_lcoll {
     int          step_started;
     int          step_open;       /* a combine step is open */
     int          send_pending;
+    int          recv_done;       /* a recv_first step has all its data */
     unsigned     iter_ep;
     size_t       iter_offset;
 };
@@ -656,17 +673,76 @@ static ucs_status_t send_one(ucg_builtin_lcoll_t *c, const op_step_t *s,
     return (st == UCS_OK) ? a.status : st;
 }
 
-/* ucg_builtin_step_execute, builtin_data.c:411-668: send every fragment to
- * every endpoint of the step (endpoint-major, resumable at iter_ep /
- * iter_offset after UCS_ERR_NO_RESOURCE, :470-517 and ucg_builtin_step_
- * am_short_max :83-137), then either complete (no receive: comp_criteria
- * SEND, builtin_control.c:1000-1002) or drain what is already stashed for
- * this step (builtin_comp_step.inl:403-462) */
-static void step_execute(ucg_builtin_lcoll_t *c)
+/* the send half of a step: every fragment to every endpoint of the step
+ * (endpoint-major, resumable at iter_ep / iter_offset after
+ * UCS_ERR_NO_RESOURCE, builtin_data.c:470-517 and ucg_builtin_step_
+ * am_short_max :83-137). Returns 1 when every message went out, 0 when it
+ * has to be resumed (send_pending) or the op failed. */
+static int step_send(ucg_builtin_lcoll_t *c)
 {
     ucg_builtin_lgroup_t *g = c->g;
     op_step_t *s = &c->steps[c->cur];
     const char *sbuf = s->send_recv_buffer ? c->rbuf : c->sbuf;
+    ops_header_t h;
+    ucs_status_t st;
+
+    h.header   = 0;
+    h.group_id = g->group_id;
+    h.coll_id  = c->coll_id;
+    h.step_idx = s->step_idx;
+    for (; c->iter_ep < s->send_cnt; c->iter_ep++) {
+        unsigned peer = s->send_peers[c->iter_ep];
+        if (s->frag_len == 0) {
+            if (c->iter_offset == 0) {
+                h.remote_offset = 0;
+                st = send_one(c, s, peer, h.header, sbuf, c->length);
+                if (st == UCS_ERR_NO_RESOURCE) {
+                    c->send_pending = 1;  /* ucg_builtin_req_enqueue_resend */
+                    return 0;
+                }
+                if (st != UCS_OK) {
+                    finish(c, st);
+                    return 0;
+                }
+                g->stats[0]++;
+            }
+        } else {
+            while (c->iter_offset < c->length) {
+                size_t n = c->length - c->iter_offset;
+                if (n > s->frag_len) {
+                    n = s->frag_len;
+                }
+                h.remote_offset = (uint32_t)c->iter_offset;
+                st = send_one(c, s, peer, h.header, sbuf + c->iter_offset, n);
+                if (st == UCS_ERR_NO_RESOURCE) {
+                    c->send_pending = 1;
+                    return 0;
+                }
+                if (st != UCS_OK) {
+                    finish(c, st);
+                    return 0;
+                }
+                g->stats[0]++;
+                c->iter_offset += n;
+            }
+        }
+        c->iter_offset = 0;   /* next endpoint starts from the first byte */
+    }
+    c->send_pending = 0;
+    return 1;
+}
+
+/* ucg_builtin_step_execute, builtin_data.c:411-668. A step sends first and
+ * then either completes (no receive: comp_criteria SEND, builtin_control.c:
+ * 1000-1002) or drains what is already stashed for it (builtin_comp_step.inl:
+ * 403-462). A *_WAYPOINT step (recv_first) receives first - from its
+ * children, reducing, or from its parent - and sends once the data is
+ * complete (comp_action SEND, builtin_control.c:1003-1007): recv_cb comes
+ * back here with recv_done set. */
+static void step_execute(ucg_builtin_lcoll_t *c)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    op_step_t *s = &c->steps[c->cur];
     ops_header_t h;
     ucs_status_t st;
 
@@ -684,6 +760,7 @@ static void step_execute(ucg_builtin_lcoll_t *c)
              * this step combines each fragment on its own (recv_cb) */
         }
         c->step_started = 1;
+        c->recv_done    = 0;
         c->pending      = s->fragments_total;
         c->iter_ep      = 0;
         c->iter_offset  = 0;
@@ -692,55 +769,23 @@ static void step_execute(ucg_builtin_lcoll_t *c)
     h.group_id = g->group_id;
     h.coll_id  = c->coll_id;
     h.step_idx = s->step_idx;
-    for (; c->iter_ep < s->send_cnt; c->iter_ep++) {
-        unsigned peer = s->send_peers[c->iter_ep];
-        if (s->frag_len == 0) {
-            if (c->iter_offset == 0) {
-                h.remote_offset = 0;
-                st = send_one(c, s, peer, h.header, sbuf, c->length);
-                if (st == UCS_ERR_NO_RESOURCE) {
-                    c->send_pending = 1;  /* ucg_builtin_req_enqueue_resend */
-                    return;
-                }
-                if (st != UCS_OK) {
-                    finish(c, st);
-                    return;
-                }
-                g->stats[0]++;
-            }
-        } else {
-            while (c->iter_offset < c->length) {
-                size_t n = c->length - c->iter_offset;
-                if (n > s->frag_len) {
-                    n = s->frag_len;
-                }
-                h.remote_offset = (uint32_t)c->iter_offset;
-                st = send_one(c, s, peer, h.header, sbuf + c->iter_offset, n);
-                if (st == UCS_ERR_NO_RESOURCE) {
-                    c->send_pending = 1;
-                    return;
-                }
-                if (st != UCS_OK) {
-                    finish(c, st);
-                    return;
-                }
-                g->stats[0]++;
-                c->iter_offset += n;
-            }
-        }
-        c->iter_offset = 0;   /* next endpoint starts from the first byte */
+    if (s->recv_first && !c->recv_done) {
+        check_pending(c, h.local_id);
+        return;
     }
-    c->send_pending = 0;
-    if (s->recv_cnt == 0) {
+    if (!step_send(c)) {
+        return;
+    }
+    if (s->recv_first || s->recv_cnt == 0) {
         step_complete(c);
         return;
     }
-    h.remote_offset = 0;
     check_pending(c, h.local_id);
 }
 
 /* ucg_builtin_step_recv_cb -> recv_handle_chunk + handle_comp,
- * builtin_comp_step.inl:184-232, 314-401; returns 1 when the step is done */
+ * builtin_comp_step.inl:184-232, 314-401; returns 1 when the step's receives
+ * are done */
 static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
                    size_t length)
 {
@@ -765,6 +810,21 @@ static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
     }
     if (--c->pending != 0) {
         return 0;
+    }
+    if (s->recv_first) {
+        /* the accumulator goes out next: its device mirror back to
+         * recv.buffer first, as before any send of it */
+        if (c->step_open) {
+            st = ucg_builtin_combine_step_end(c->g->cmb);
+            c->step_open = 0;
+            if (st != UCS_OK) {
+                finish(c, st);
+                return 1;
+            }
+        }
+        c->recv_done = 1;
+        step_execute(c);
+        return 1;
     }
     step_complete(c);
     return 1;
@@ -803,18 +863,36 @@ static ucs_status_t am_handler(void *arg, void *data, size_t length)
     return UCS_OK;
 }
 
-ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
-                                       uint16_t group_id, unsigned member_count,
-                                       unsigned my_index,
-                                       ucg_builtin_combine_t *combine,
-                                       ucg_builtin_lgroup_t **group_p)
+static unsigned env_uint(const char *name, unsigned dflt)
+{
+    const char *e = getenv(name);
+    return (e && *e) ? (unsigned)strtoul(e, NULL, 0) : dflt;
+}
+
+ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
+                                          uint16_t group_id, unsigned member_count,
+                                          unsigned my_index,
+                                          ucg_builtin_combine_t *combine,
+                                          const ucg_builtin_lgroup_params_t *params,
+                                          ucg_builtin_lgroup_t **group_p)
 {
     ucg_builtin_lgroup_t *g;
     stash_t **pp;
+    unsigned m;
 
     if (iface == NULL || group_p == NULL || combine == NULL || group_id == 0 ||
         member_count != iface->members || my_index != iface->my) {
         return UCS_ERR_INVALID_PARAM;
+    }
+    if (params && params->distance) {
+        for (m = 0; m < member_count; m++) {
+            /* distance[my] = SELF and no other member at SELF; FAULT and
+             * LAST are not placements */
+            if ((params->distance[m] == UCG_BUILTIN_DISTANCE_SELF) != (m == my_index) ||
+                params->distance[m] > UCG_BUILTIN_DISTANCE_NET) {
+                return UCS_ERR_INVALID_PARAM;
+            }
+        }
     }
     if (iface->groups[group_id % UNEXP_GROUPS] != NULL) {
         return UCS_ERR_BUSY;
@@ -832,6 +910,17 @@ ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
         const char *e = getenv("UCX_BUILTIN_SM_INCAST");
         g->incast = e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1');
     }
+    for (m = 0; m < member_count; m++) {
+        g->distance[m] = (params && params->distance) ? params->distance[m] :
+                         (m == my_index) ? UCG_BUILTIN_DISTANCE_SELF : UCG_BUILTIN_DISTANCE_HOST;
+    }
+    /* builtin/plan/builtin_tree.c:18-29, builtin_recursive.c:13-18 */
+    g->radix       = (params && params->tree_radix) ? params->tree_radix :
+                     env_uint("UCX_BUILTIN_TREE_RADIX", 8);
+    g->sock_thresh = (params && params->sock_thresh) ? params->sock_thresh :
+                     env_uint("UCX_BUILTIN_TREE_SOCKET_LEVEL_PPN_THRESH", 16);
+    g->factor      = (params && params->recursive_factor) ? params->recursive_factor :
+                     env_uint("UCX_BUILTIN_RECURSIVE_FACTOR", 2);
     iface->groups[group_id % UNEXP_GROUPS] = g;
     /* adopt messages that arrived before the group existed (builtin.c:
      * 424-446) */
@@ -840,16 +929,26 @@ ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
         ops_header_t h;
         h.header = (*pp)->header;
         if (h.group_id == group_id) {
-            stash_t *m = *pp;
-            *pp = m->next;
-            m->next = NULL;
-            stash_append(&g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT].msgs, m);
+            stash_t *msg = *pp;
+            *pp = msg->next;
+            msg->next = NULL;
+            stash_append(&g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT].msgs, msg);
         } else {
             pp = &(*pp)->next;
         }
     }
     *group_p = g;
     return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
+                                       uint16_t group_id, unsigned member_count,
+                                       unsigned my_index,
+                                       ucg_builtin_combine_t *combine,
+                                       ucg_builtin_lgroup_t **group_p)
+{
+    return ucg_builtin_lgroup_create_ex(iface, group_id, member_count, my_index,
+                                        combine, NULL, group_p);
 }
 
 void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
@@ -911,125 +1010,430 @@ static ucs_status_t step_fragments(ucg_builtin_lcoll_t *c, op_step_t *s)
     return UCS_OK;
 }
 
-/* Recursive doubling, factor 2 (builtin_recursive.c:20-228): step k sends to
- * and reduces from my ^ 2^(k-1); step 1 sends the send buffer, later steps
- * the accumulator (builtin_control.c:825-857). */
-static ucs_status_t plan_recursive(ucg_builtin_lcoll_t *c)
+/* ---- plan construction (builtin/plan) ------------------------------------
+ * The reference builds every tree for root 0 (builtin_tree.c:544-551) and a
+ * non-zero root through ucg_builtin_topo_tree_set_root, which reads tree
+ * parameters out of a plan phase (:590-592). Here a plan is built in a
+ * virtual numbering in which the root is member 0: the root's host moves to
+ * the front and the root to the front of its host, so hosts stay runs of
+ * consecutive indices; v2r maps a virtual member back. */
+#define TREE_MAX_RADIX 128   /* UCG_BUILTIN_TREE_MAX_RADIX, builtin_plan.h:98 */
+#define PM               UCG_BUILTIN_OPS_MAX_MEMBERS
+
+typedef struct {
+    unsigned n, my;              /* group size, my virtual index */
+    uint8_t  d[PM];               /* my distances, virtual order */
+    unsigned v2r[PM];
+    unsigned radix, sock_thresh, factor;
+} plan_ctx_t;
+
+enum {
+    D_SELF = UCG_BUILTIN_DISTANCE_SELF, D_SOCKET = UCG_BUILTIN_DISTANCE_SOCKET,
+    D_HOST = UCG_BUILTIN_DISTANCE_HOST, D_NET = UCG_BUILTIN_DISTANCE_NET,
+    D_LAST = 255                 /* UCG_GROUP_MEMBER_DISTANCE_LAST */
+};
+
+/* The virtual numbering for `root`. Hosts are runs of ppn consecutive
+ * members (the "by node" allocation builtin_tree.c:397-405 assumes); a layout
+ * that is not, as seen from this member, is UCS_ERR_UNSUPPORTED. */
+static ucs_status_t plan_ctx_init(ucg_builtin_lgroup_t *g, unsigned root, plan_ctx_t *pc)
 {
-    ucg_builtin_lgroup_t *g = c->g;
-    unsigned steps = ucg_builtin_recursive_steps(g->size, 2), k;
-    if (steps > OPS_MAX_STEPS) {
+    unsigned m, ppn = 0, H, hr, lr, r2v_my = 0;
+    for (m = 0; m < g->size; m++) {
+        ppn += g->distance[m] <= D_HOST;
+    }
+    if (ppn == 0 || g->size % ppn) {
         return UCS_ERR_UNSUPPORTED;
     }
-    c->plan        = "recursive doubling";
-    c->nsteps      = steps;
-    c->init_reduce = 1;
-    for (k = 0; k < steps; k++) {
-        op_step_t *s  = &c->steps[k];
-        unsigned peer = (unsigned)ucg_builtin_recursive_peer(g->my, k + 1, 2, 1);
-        s->method           = M_REDUCE_RECURSIVE;
-        s->aggregation      = AGG_REDUCE;
-        s->step_idx         = (uint8_t)(k + 1);
-        s->send_cnt         = 1;
-        s->send_peers[0]    = peer;
-        s->recv_cnt         = 1;
-        s->recv_peers[0]    = peer;
-        s->send_recv_buffer = (k != 0);
-        if (step_fragments(c, s) != UCS_OK) {
+    for (m = 0; m < g->size; m++) {
+        if ((g->distance[m] <= D_HOST) != (m / ppn == g->my / ppn)) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+    }
+    H  = g->size / ppn;
+    hr = root / ppn;
+    lr = root % ppn;
+    pc->n           = g->size;
+    pc->radix       = g->radix;
+    pc->sock_thresh = g->sock_thresh;
+    pc->factor      = g->factor;
+    for (m = 0; m < g->size; m++) {
+        unsigned vb = m / ppn, vi = m % ppn, li;
+        li = (vb != 0) ? vi : (vi == 0) ? lr : (vi <= lr ? vi - 1 : vi);
+        pc->v2r[m] = ((vb + hr) % H) * ppn + li;
+        if (pc->v2r[m] == g->my) {
+            r2v_my = m;
+        }
+    }
+    pc->my = r2v_my;
+    for (m = 0; m < g->size; m++) {
+        uint8_t d = g->distance[pc->v2r[m]];
+        /* with the root moved to the front of its host, sockets are no
+         * longer runs of the virtual numbering: one intra-host level */
+        pc->d[m] = (root != 0 && d == D_SOCKET) ? D_HOST : d;
+    }
+    return UCS_OK;
+}
+
+/* ucg_builtin_tree_add_intra, builtin_tree.c:262-380 (root 0): my parent is
+ * the first member before me at the smallest distance; my children are the
+ * members after me at a distance above the last one taken and within my
+ * master phase - the first of each new distance moved to the front - and
+ * the members at the distance of my first child. Below sock_thresh members
+ * per host SOCKET counts as HOST (one level). */
+static ucs_status_t tree_add_intra(const plan_ctx_t *pc, unsigned *ppn, unsigned *up,
+                                   unsigned *up_cnt, unsigned *down, unsigned *down_cnt,
+                                   unsigned *master_phase)
+{
+    unsigned m, up_distance = D_LAST, down_distance = D_SELF, first_distance = D_SELF;
+    int single;
+    *ppn = *up_cnt = *down_cnt = 0;
+    *master_phase = D_NET;
+    for (m = 0; m < pc->n; m++) {
+        *ppn += pc->d[m] <= D_HOST;
+    }
+    single = *ppn < pc->sock_thresh;
+    for (m = 0; m < pc->my; m++) {
+        unsigned d = (single && pc->d[m] == D_SOCKET) ? D_HOST : pc->d[m];
+        if (up_distance > d) {
+            up_distance   = d;
+            *master_phase = d - 1;
+            up[0]         = m;
+            *up_cnt       = 1;
+        }
+    }
+    for (m = pc->my + 1; m < pc->n; m++) {
+        unsigned d = (single && pc->d[m] == D_SOCKET) ? D_HOST : pc->d[m];
+        if (d > down_distance && d <= *master_phase && d < D_NET) {
+            down_distance  = d;
+            first_distance = (first_distance == D_SELF) ? d : D_LAST;
+            if (*down_cnt) {
+                down[(*down_cnt)++] = down[0];
+            } else {
+                (*down_cnt)++;
+            }
+            down[0] = m;
+        } else if (d == first_distance) {
+            down[(*down_cnt)++] = m;
+        }
+        if (*down_cnt == TREE_MAX_RADIX) {
             return UCS_ERR_UNSUPPORTED;
         }
     }
     return UCS_OK;
 }
 
-/* Single-host tree (builtin_tree.c): every member of a shm iface is at
- * UCG_GROUP_MEMBER_DISTANCE_HOST from every other, so ucg_builtin_tree_add_
- * intra (:262-380) makes the root the parent of all other members (children
- * in member order) and no member a waypoint; with ppn == member_count there
- * is no inter-host phase (:486-495). ucg_builtin_tree_connect (:86-260,
- * step_offset 1) then gives
- *   fan-in,  step_idx 1: root REDUCE_TERMINAL from all children (init_reduce:
- *            recv <- send first); each child SEND_TO_SM_ROOT (SEND_TERMINAL
- *            when ppn == 2) of its send buffer to the root;
- *   fan-out, step_idx 4 (allreduce only, BROADCAST modifier): root
- *            SEND_TERMINAL of recv.buffer to all children; each child
- *            RECV_TERMINAL into recv.buffer with WRITE aggregation.
- * The root receives the children's messages in arrival order and reduces each
- * one into recv.buffer as it comes (MULTIPLE_MESSAGES criteria,
- * builtin_control.c:974-996): for a floating-point op the association follows
- * arrival, as in the reference; every member ends with the root's bits.
- * The reference builds root != 0 through ucg_builtin_topo_tree_set_root, which
- * reads tree parameters out of a plan phase (builtin_tree.c:590-592); here the
- * same flat tree is simply rooted at `root`. */
-static ucs_status_t plan_tree(ucg_builtin_lcoll_t *c, int fanout)
+/* The intra-host trees tree_add_intra cannot build: the host master takes
+ * the first other socket's master as a child and no later one
+ * (first_distance turns LAST, builtin_tree.c:336-351), so on a host of more
+ * than two sockets (or with a CACHE level inside a socket) some masters send
+ * to a parent that never expects them. UCS_ERR_UNSUPPORTED instead of a hang
+ * (DESIGN.md 7). */
+static ucs_status_t check_host_tree(const plan_ctx_t *pc)
 {
-    ucg_builtin_lgroup_t *g = c->g;
-    unsigned ppn = g->size, m, nchild = 0;
-    unsigned children[UCG_BUILTIN_OPS_MAX_MEMBERS];
-    int is_root = (g->my == c->root);
-    op_step_t *s;
-
-    for (m = 0; m < g->size; m++) {
-        if (m != c->root) {
-            children[nchild++] = m;
+    unsigned m, ppn = 0, sock = 0;
+    int has_socket = 0;
+    for (m = 0; m < pc->n; m++) {
+        if (pc->d[m] == UCG_BUILTIN_DISTANCE_CACHE) {
+            return UCS_ERR_UNSUPPORTED;
         }
+        ppn        += pc->d[m] <= D_HOST;
+        sock       += pc->d[m] <= D_SOCKET;
+        has_socket |= pc->d[m] == D_SOCKET;
     }
-    c->plan   = "tree";
-    c->nsteps = 0;
-    /* fan-in */
-    s = &c->steps[c->nsteps++];
-    s->step_idx = 1;
-    if (is_root) {
-        s->method      = M_REDUCE_TERMINAL;
-        s->aggregation = AGG_REDUCE;
-        s->recv_cnt    = nchild;
-        memcpy(s->recv_peers, children, nchild * sizeof(unsigned));
-        s->send_cnt    = 0;
-        c->init_reduce = 1;
-    } else {
-        s->method        = (ppn == 2) ? M_SEND_TERMINAL : M_SEND_TO_SM_ROOT;
-        s->aggregation   = AGG_NOP;
-        s->send_cnt      = 1;
-        s->send_peers[0] = c->root;
-        s->recv_cnt      = 0;
-    }
-    s->send_recv_buffer = 0;
-    if (step_fragments(c, s) != UCS_OK) {
+    if (ppn >= pc->sock_thresh && has_socket && (ppn % sock || ppn / sock > 2)) {
         return UCS_ERR_UNSUPPORTED;
     }
-    /* SM-root reduce (is_sm_reduce, builtin_control.c:535-537): with the
-     * incast transport the children pack into one message per fragment */
-    if (g->incast && ppn > 2) {
-        s->incast = 1;
-        if (is_root) {
-            s->fragments_total = s->frags;
-        } else {
-            s->incast_expected = nchild;
-            s->packer = ucg_builtin_combine_atomic_sum_length(g->cmb, c->op, c->dtype)
-                        ? PACK_ATOMIC : PACK_REDUCING;
+    return UCS_OK;
+}
+
+/* ucg_builtin_tree_add_inter, builtin_tree.c:382-438: the hosts' masters
+ * (every ppn-th member) form a tree of the given radix, root 0 */
+static ucs_status_t tree_add_inter(const plan_ctx_t *pc, unsigned ppn, unsigned *up,
+                                   unsigned *up_cnt, unsigned *down, unsigned *down_cnt)
+{
+    const unsigned long limit = pc->n, radix = pc->radix < 2 ? 2 : pc->radix;
+    unsigned long inner_range = ppn, outer_range = (unsigned long)ppn * radix;
+    unsigned long outer, inner, root;
+    *up_cnt = *down_cnt = 0;
+    do {
+        for (outer = 0; outer < limit; outer += outer_range) {
+            root = (outer_range < limit) ? outer : 0;
+            for (inner = outer; inner < outer + outer_range && inner < limit;
+                 inner += inner_range) {
+                if (pc->my == inner) {
+                    if (pc->my == root) {
+                        continue;
+                    }
+                    up[(*up_cnt)++] = (unsigned)root;
+                    if (*up_cnt == TREE_MAX_RADIX) {
+                        return UCS_ERR_UNSUPPORTED;
+                    }
+                } else if (pc->my == root) {
+                    down[(*down_cnt)++] = (unsigned)inner;
+                    if (*down_cnt == TREE_MAX_RADIX) {
+                        return UCS_ERR_UNSUPPORTED;
+                    }
+                }
+            }
+        }
+        inner_range *= radix;
+        outer_range *= radix;
+    } while (outer_range < limit * radix);
+    return UCS_OK;
+}
+
+/* one phase: who the step sends to and receives from, by method
+ * (builtin_control.c:375-396 for the order, :960-972 for the aggregation) */
+static ucs_status_t add_phase(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc,
+                              op_method_t method, unsigned step_idx,
+                              const unsigned *peers, unsigned npeers)
+{
+    op_step_t *s;
+    unsigned i, first_send = 0, send_cnt = 0, recv_cnt = 0;
+    if (c->nsteps == OPS_MAX_STEPS || npeers == 0 || npeers > PM || step_idx > 255) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    s = &c->steps[c->nsteps++];
+    memset(s, 0, sizeof(*s));
+    s->method   = (uint8_t)method;
+    s->step_idx = (uint8_t)step_idx;
+    switch (method) {
+    case M_SEND_TERMINAL:
+    case M_SEND_TO_SM_ROOT:
+        send_cnt = npeers;
+        break;
+    case M_REDUCE_TERMINAL:
+        recv_cnt       = npeers;
+        s->aggregation = AGG_REDUCE;
+        break;
+    case M_RECV_TERMINAL:
+        recv_cnt       = npeers;
+        s->aggregation = AGG_WRITE;
+        break;
+    case M_REDUCE_RECURSIVE:
+        send_cnt = recv_cnt = npeers;
+        s->aggregation = AGG_REDUCE;
+        break;
+    case M_REDUCE_WAYPOINT:      /* children first, the parent last */
+        if (npeers < 2) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+        recv_cnt       = npeers - 1;
+        first_send     = npeers - 1;
+        send_cnt       = 1;
+        s->aggregation = AGG_REDUCE;
+        s->recv_first  = 1;
+        break;
+    case M_BCAST_WAYPOINT:       /* the parent first, then the children */
+        if (npeers < 2) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+        recv_cnt       = 1;
+        first_send     = 1;
+        send_cnt       = npeers - 1;
+        s->aggregation = AGG_WRITE;
+        s->recv_first  = 1;
+        break;
+    }
+    s->send_cnt = send_cnt;
+    s->recv_cnt = recv_cnt;
+    for (i = 0; i < send_cnt; i++) {
+        s->send_peers[i] = pc->v2r[peers[first_send + i]];
+    }
+    for (i = 0; i < recv_cnt; i++) {
+        s->recv_peers[i] = pc->v2r[peers[i]];
+    }
+    return UCS_OK;
+}
+
+/* ucg_builtin_tree_connect, builtin_tree.c:86-260, for the aggregating
+ * collectives (AGGREGATE; BROADCAST for the fan-out of an allreduce): the
+ * host fan-in at step_offset, the network fan-in at +1, the network fan-out
+ * at +2 and the host fan-out at +3. A fan-in sends to the parent appended
+ * after the children; a fan-out hears from the parent listed first. */
+static ucs_status_t tree_connect(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc, int fanin,
+                                 int fanout, unsigned step_offset, unsigned ppn,
+                                 const unsigned *host_up, unsigned host_up_cnt,
+                                 const unsigned *net_up, unsigned net_up_cnt,
+                                 const unsigned *net_down, unsigned net_down_cnt,
+                                 const unsigned *host_down, unsigned host_down_cnt)
+{
+    unsigned peers[2 * PM + 2], n, i;
+    ucs_status_t st = UCS_OK;
+    op_method_t method;
+    if (fanin && host_up_cnt + host_down_cnt) {
+        method = host_down_cnt ? (host_up_cnt ? M_REDUCE_WAYPOINT : M_REDUCE_TERMINAL) :
+                 (ppn == 2) ? M_SEND_TERMINAL : M_SEND_TO_SM_ROOT;
+        for (n = 0, i = 0; i < host_down_cnt; i++) peers[n++] = host_down[i];
+        if (host_up_cnt) peers[n++] = host_up[0];
+        st = add_phase(c, pc, method, step_offset, peers, n);
+    }
+    if (st == UCS_OK && fanin && net_up_cnt + net_down_cnt) {
+        method = net_down_cnt ? (net_up_cnt ? M_REDUCE_WAYPOINT : M_REDUCE_TERMINAL) :
+                 M_SEND_TERMINAL;
+        for (n = 0, i = 0; i < net_down_cnt; i++) peers[n++] = net_down[i];
+        if (net_up_cnt) peers[n++] = net_up[0];
+        st = add_phase(c, pc, method, step_offset + 1, peers, n);
+    }
+    if (st == UCS_OK && fanout && net_up_cnt + net_down_cnt) {
+        method = net_down_cnt ? (net_up_cnt ? M_BCAST_WAYPOINT : M_SEND_TERMINAL) :
+                 M_RECV_TERMINAL;
+        for (n = 0, i = 0; i < net_up_cnt; i++) peers[n++] = net_up[i];
+        for (i = 0; i < net_down_cnt; i++) peers[n++] = net_down[i];
+        st = add_phase(c, pc, method, step_offset + 2, peers, n);
+    }
+    if (st == UCS_OK && fanout && host_up_cnt + host_down_cnt) {
+        method = host_down_cnt ? (host_up_cnt ? M_BCAST_WAYPOINT : M_SEND_TERMINAL) :
+                 M_RECV_TERMINAL;
+        for (n = 0, i = 0; i < host_up_cnt; i++) peers[n++] = host_up[i];
+        for (i = 0; i < host_down_cnt; i++) peers[n++] = host_down[i];
+        st = add_phase(c, pc, method, step_offset + 3, peers, n);
+    }
+    return st;
+}
+
+/* ucg_builtin_tree_create / _build, builtin_tree.c:441-561: the intra-host
+ * tree, and for a host master of a multi-host group the inter-host tree (its
+ * parent "of index 0" from the intra-host pass dropped, :488-497) */
+static ucs_status_t plan_tree(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc, int fanout,
+                              unsigned *ppn)
+{
+    unsigned host_up[PM], host_down[PM], net_up[TREE_MAX_RADIX], net_down[TREE_MAX_RADIX];
+    unsigned hu, hd, nu = 0, nd = 0, mp;
+    ucs_status_t st = check_host_tree(pc);
+    if (st != UCS_OK || (st = tree_add_intra(pc, ppn, host_up, &hu, host_down, &hd,
+                                             &mp)) != UCS_OK) {
+        return st;
+    }
+    if (mp >= D_HOST && *ppn < pc->n) {
+        hu = 0;
+        if ((st = tree_add_inter(pc, *ppn, net_up, &nu, net_down, &nd)) != UCS_OK) {
+            return st;
         }
     }
-    if (!fanout) {
-        return UCS_OK;
+    c->plan = "tree";
+    return tree_connect(c, pc, 1, fanout, 1, *ppn, host_up, hu, net_up, nu, net_down, nd,
+                        host_down, hd);
+}
+
+/* ucg_builtin_recursive_create, builtin_recursive.c:20-228: recursive K-ing
+ * (K = factor) over the hosts' masters - step k's peers are
+ *   base + ((my - base + step_size * j) % (step_size * K)),  j = 1 .. K-1,
+ *   base = my - my % (step_size * K), step_size = ppn * K^(k-1)
+ * (:158-197) - wrapped in the intra-host fan-in and fan-out when hosts hold
+ * several members. One host whose size is not a power of K runs the
+ * intra-host tree alone (:78-82); several hosts whose number is not one are
+ * UCS_ERR_UNSUPPORTED (:83-87). */
+static ucs_status_t plan_recursive(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc,
+                                   unsigned *ppn_out)
+{
+    unsigned host_up[PM], host_down[PM], peers[PM];
+    unsigned ppn, hu, hd, mp, steps = 0, k, j, idx;
+    unsigned long proc_count, step_size = 1;
+    ucs_status_t st = tree_add_intra(pc, &ppn, host_up, &hu, host_down, &hd, &mp);
+    if (st != UCS_OK) {
+        return st;
     }
-    /* fan-out */
-    s = &c->steps[c->nsteps++];
-    s->step_idx = 4;
-    if (is_root) {
-        s->method      = M_SEND_TERMINAL;
-        s->aggregation = AGG_NOP;
-        s->send_cnt    = nchild;
-        memcpy(s->send_peers, children, nchild * sizeof(unsigned));
-        s->recv_cnt    = 0;
+    *ppn_out = ppn;
+    /* a host's master drops its parent from the intra-host pass (a member
+     * of another host). The reference tests master_phase == HOST (:55),
+     * which no NET parent produces; >= HOST is the intent */
+    if (mp >= D_HOST) {
+        hu = 0;
+    }
+    if (pc->factor < 2) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    proc_count = (pc->n == ppn) ? ppn : pc->n / ppn + (pc->n % ppn > 0);
+    while (step_size < proc_count) {
+        step_size *= pc->factor;
+        steps++;
+    }
+    if (step_size != proc_count) {
+        if (pc->n != ppn) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+        steps = 0;               /* one host: the intra-host tree */
+    }
+    if (pc->n == ppn && steps) {
+        hu = hd = 0;             /* one host, recursive among all members */
+        ppn = 1;
+    } else if ((st = check_host_tree(pc)) != UCS_OK) {
+        return st;
+    }
+    if (steps == 0) {
+        c->plan = "tree";
+    } else if (hu || hd) {
+        c->plan = pc->factor == 2 ? "host fan-in, recursive doubling over host masters, fan-out" :
+                                    "host fan-in, recursive K-ing over host masters, fan-out";
     } else {
-        s->method        = M_RECV_TERMINAL;
-        s->aggregation   = AGG_WRITE;
-        s->send_cnt      = 0;
-        s->recv_cnt      = 1;
-        s->recv_peers[0] = c->root;
+        c->plan = pc->factor == 2 ? "recursive doubling" : "recursive K-ing";
     }
-    s->send_recv_buffer = 1;
-    return step_fragments(c, s);
+    if ((hu || hd) &&
+        (st = tree_connect(c, pc, 1, 0, 1, ppn, host_up, hu, NULL, 0, NULL, 0,
+                           host_down, hd)) != UCS_OK) {
+        return st;
+    }
+    if (!hu) {
+        idx = c->nsteps + 1;
+        step_size = ppn;
+        for (k = 0; k < steps; k++, step_size *= pc->factor) {
+            unsigned long base = pc->my - pc->my % (step_size * pc->factor);
+            for (j = 1; j < pc->factor; j++) {
+                peers[j - 1] = (unsigned)(base + ((pc->my - base + step_size * j) %
+                                                  (step_size * pc->factor)));
+            }
+            if ((st = add_phase(c, pc, M_REDUCE_RECURSIVE, idx + k, peers,
+                                pc->factor - 1)) != UCS_OK) {
+                return st;
+            }
+        }
+    }
+    if (hu || hd) {
+        st = tree_connect(c, pc, 0, 1, steps + 1, ppn, host_up, hu, NULL, 0, NULL, 0,
+                          host_down, hd);
+    }
+    return st;
+}
+
+/* what every step of the member's plan sends and how much it receives:
+ * the send buffer is recv.buffer once anything was received into it
+ * (builtin_control.c:673-683; a waypoint sends what it received), the
+ * accumulator is seeded (ucg_builtin_init_reduce) when the member reduces,
+ * and the SM-root children of a one-level host fan-in may pack into one
+ * incast cell at their master (builtin_control.c:535-537) */
+static ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    int received = 0;
+    unsigned k;
+    c->init_reduce = 0;
+    for (k = 0; k < c->nsteps; k++) {
+        op_step_t *s = &c->steps[k];
+        s->send_recv_buffer = received || s->recv_first;
+        if (s->recv_cnt) {
+            received = 1;
+        }
+        if (s->aggregation == AGG_REDUCE) {
+            c->init_reduce = 1;
+        }
+        if (step_fragments(c, s) != UCS_OK) {
+            return UCS_ERR_UNSUPPORTED;
+        }
+        if (g->incast && s->step_idx == 1 && ppn > 2 && ppn < g->sock_thresh) {
+            if (s->method == M_REDUCE_TERMINAL) {
+                s->incast          = 1;
+                s->fragments_total = s->frags;
+            } else if (s->method == M_SEND_TO_SM_ROOT) {
+                s->incast          = 1;
+                s->incast_expected = ppn - 1;
+                s->packer = ucg_builtin_combine_atomic_sum_length(g->cmb, c->op, c->dtype)
+                            ? PACK_ATOMIC : PACK_REDUCING;
+            }
+        }
+    }
+    return UCS_OK;
 }
 
 static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
@@ -1086,6 +1490,8 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
                                          void *op, ucg_builtin_lcoll_t **coll_p)
 {
     ucg_builtin_lcoll_t *c;
+    plan_ctx_t pc;
+    unsigned ppn = 1;
     ucs_status_t st;
 
     if (rbuf == NULL) {
@@ -1100,10 +1506,12 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
         c->plan        = "none";
         c->init_reduce = 1;
         st = UCS_OK;
-    } else if (allreduce_use_tree(g->size)) {
-        st = plan_tree(c, 1);
-    } else {
-        st = plan_recursive(c);
+    } else if ((st = plan_ctx_init(g, 0, &pc)) == UCS_OK) {
+        st = allreduce_use_tree(g->size) ? plan_tree(c, &pc, 1, &ppn) :
+                                           plan_recursive(c, &pc, &ppn);
+        if (st == UCS_OK) {
+            st = plan_finish(c, ppn);
+        }
     }
     if (st != UCS_OK) {
         free(c);
@@ -1119,6 +1527,8 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
                                       ucg_builtin_lcoll_t **coll_p)
 {
     ucg_builtin_lcoll_t *c;
+    plan_ctx_t pc;
+    unsigned ppn = 1, k;
     ucs_status_t st;
 
     if (g == NULL || root >= g->size || (g->my == root && rbuf == NULL)) {
@@ -1133,9 +1543,25 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
     if (g->size == 1) {
         c->plan        = "none";
         c->init_reduce = 1;
-    } else if ((st = plan_tree(c, 0)) != UCS_OK) {
+    } else if ((st = plan_ctx_init(g, root, &pc)) != UCS_OK ||
+               (st = plan_tree(c, &pc, 0, &ppn)) != UCS_OK ||
+               (st = plan_finish(c, ppn)) != UCS_OK) {
         free(c);
         return st;
+    }
+    /* a member other than the root that combines on the way (a host master,
+     * a waypoint) accumulates in a buffer of the op's own: MPI leaves recvbuf
+     * undefined off the root */
+    for (k = 0; k < c->nsteps && g->my != root; k++) {
+        if (c->steps[k].aggregation != AGG_NOP) {
+            c->scratch = malloc(c->length ? c->length : 1);
+            if (c->scratch == NULL) {
+                free(c);
+                return UCS_ERR_NO_MEMORY;
+            }
+            c->rbuf = c->scratch;
+            break;
+        }
     }
     *coll_p = c;
     return UCS_OK;
@@ -1225,6 +1651,9 @@ void ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *c)
     if (c && c->active) {
         finish(c, UCS_ERR_CANCELED);
     }
+    if (c) {
+        free(c->scratch);
+    }
     free(c);
 }
 
@@ -1250,7 +1679,7 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
         unsigned e;
         PUT("Step #%u (step_idx %u): %s", k, (unsigned)s->step_idx,
             method_name[s->method]);
-        if (s->send_cnt) {
+        if (s->send_cnt && !s->recv_first) {
             PUT(", send %s to", s->send_recv_buffer ? "recv.buffer" : "send.buffer");
             for (e = 0; e < s->send_cnt; e++) {
                 PUT(" %u", s->send_peers[e]);
@@ -1260,6 +1689,12 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             PUT(", receive from");
             for (e = 0; e < s->recv_cnt; e++) {
                 PUT(" %u", s->recv_peers[e]);
+            }
+        }
+        if (s->send_cnt && s->recv_first) {
+            PUT(", then send recv.buffer to");
+            for (e = 0; e < s->send_cnt; e++) {
+                PUT(" %u", s->send_peers[e]);
             }
         }
         if (s->incast) {

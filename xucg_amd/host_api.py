@@ -22,6 +22,12 @@ class ReduceParams(ctypes.Structure):
                 ("is_floating_point_f", DT_FN)]
 
 
+class GroupParams(ctypes.Structure):
+    """ucg_builtin_lgroup_params_t (include/ucg_builtin_ops.h)."""
+    _fields_ = [("distance", ctypes.POINTER(ctypes.c_uint8)), ("tree_radix", ctypes.c_uint),
+                ("sock_thresh", ctypes.c_uint), ("recursive_factor", ctypes.c_uint)]
+
+
 class CombineConfig(ctypes.Structure):
     _fields_ = [("dev_enable", ctypes.c_int), ("dev_min_bytes", _sz),
                 ("stage_bytes", _sz), ("stage_slots", ctypes.c_uint),
@@ -63,6 +69,8 @@ HOST_API = {
     "ucg_builtin_shm_am_incast": (_int, [_vp, _u, _u64, _u, _sz, _vp, _vp, _int]),
     "ucg_builtin_lgroup_create": (_int, [_vp, ctypes.c_uint16, _u, _u, _vp,
                                          ctypes.POINTER(_vp)]),
+    "ucg_builtin_lgroup_create_ex": (_int, [_vp, ctypes.c_uint16, _u, _u, _vp,
+                                            ctypes.POINTER(GroupParams), ctypes.POINTER(_vp)]),
     "ucg_builtin_lgroup_destroy": (None, [_vp]),
     "ucg_builtin_lgroup_progress": (_u, [_vp]),
     "ucg_builtin_lgroup_stats": (None, [_vp, ctypes.POINTER(_u64)]),

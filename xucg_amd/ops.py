@@ -26,13 +26,50 @@ class ShmIface:
             self.handle = None
 
 
+# enum ucg_group_member_distance (api/ucg.h:253-264)
+DISTANCE = {"self": 0, "cache": 1, "socket": 7, "host": 15, "net": 253}
+
+
+def layout_distances(members, my_index, ppn=None, socket=None):
+    """The distance array member `my_index` passes for a "by node" layout:
+    hosts of `ppn` consecutive members (default: one host), each split into
+    sockets of `socket` consecutive members (default: none)."""
+    ppn = ppn or members
+    out = []
+    for m in range(members):
+        if m == my_index:
+            out.append(DISTANCE["self"])
+        elif m // ppn != my_index // ppn:
+            out.append(DISTANCE["net"])
+        elif socket and m // socket != my_index // socket:
+            out.append(DISTANCE["host"])
+        elif socket:
+            out.append(DISTANCE["socket"])
+        else:
+            out.append(DISTANCE["host"])
+    return out
+
+
 class Group:
-    def __init__(self, iface, group_id, members, my_index, combine):
+    """distance: the member's distance array (ucg_group_params_t.distance),
+    None = one host; radix / sock_thresh / factor: the planner's
+    TREE_RADIX, TREE_SOCKET_LEVEL_PPN_THRESH and RECURSIVE_FACTOR (0 = the
+    environment or the default)."""
+
+    def __init__(self, iface, group_id, members, my_index, combine, distance=None,
+                 radix=0, sock_thresh=0, factor=0):
+        from .host_api import GroupParams
         h = ctypes.c_void_p()
-        _lib.check(_lib.host().ucg_builtin_lgroup_create(iface.handle, group_id, members,
-                                                         my_index, combine.handle,
-                                                         ctypes.byref(h)),
-                   "ucg_builtin_lgroup_create")
+        self._dist = None
+        params = None
+        if distance is not None or radix or sock_thresh or factor:
+            if distance is not None:
+                self._dist = (ctypes.c_uint8 * members)(*distance)
+            params = GroupParams(self._dist, radix, sock_thresh, factor)
+        _lib.check(_lib.host().ucg_builtin_lgroup_create_ex(
+            iface.handle, group_id, members, my_index, combine.handle,
+            ctypes.byref(params) if params is not None else None, ctypes.byref(h)),
+            "ucg_builtin_lgroup_create_ex")
         self.handle = h.value
         self.iface = iface
         self.combine = combine
