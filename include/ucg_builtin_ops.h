@@ -18,12 +18,14 @@
  *                  builtin/ops/builtin_comp_step.inl:403-462
  *   completion     pending = ep_cnt x fragments, next step or finish,
  *                  builtin/ops/builtin_comp_step.inl:8-95,342-401
- *   plans          recursive doubling, builtin/plan/builtin_recursive.c:20-228;
- *                  tree fan-in / fan-out (single host: flat, root = parent of
- *                  all), builtin/plan/builtin_tree.c:86-380; the choice,
- *                  builtin/builtin.c:95-121
- *   aggregation    REDUCE for REDUCE_TERMINAL/RECURSIVE, WRITE for the
- *                  fan-out receive, builtin/ops/builtin_control.c:960-972
+ *   plans          recursive K-ing with its intra-host fan-in / fan-out,
+ *                  builtin/plan/builtin_recursive.c:20-228; tree fan-in /
+ *                  fan-out over hosts and sockets (add_intra, add_inter,
+ *                  tree_connect), builtin/plan/builtin_tree.c:86-561; the
+ *                  choice, builtin/builtin.c:95-121
+ *   aggregation    REDUCE for REDUCE_TERMINAL/RECURSIVE/WAYPOINT, WRITE for
+ *                  the fan-out receive, builtin/ops/builtin_control.c:960-972
+ *                  (a REDUCE_WAYPOINT reduces here)
  *   fragments      builtin/ops/builtin_control.c:434,462-465
  *   seeding        ucg_builtin_init_reduce, builtin/ops/builtin_control.c:43-47
  *
