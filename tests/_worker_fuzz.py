@@ -3,13 +3,18 @@ reduce ops (random dtype, op, count, root, in-place) on one group, each
 checked bit for bit against the oracle (integer types and exact-integer
 floats, so the tree's arrival order cannot change a result).
 
-    _worker_fuzz.py <shm-name> <seed> <max_short> <ring_cells>"""
+    _worker_fuzz.py <shm-name> <seed> <max_short> <ring_cells> [ppn:socket:radix:factor:thresh]
+
+With a placement (hosts of ppn, sockets of `socket`, 0 = none) the expected
+results come from the oracle's simulation of every member's plan
+(oracle/plans.py); the inputs keep the association irrelevant."""
 import os
 import sys
 
 import numpy as np
 
 from oracle import oracle as O
+from oracle import plans as P
 from xucg_amd import host, ops
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -26,7 +31,16 @@ def main():
     mpi = MockMPI()
     cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
     iface = ops.ShmIface(name, world, rank, max_short=max_short, ring_cells=cells)
-    group = ops.Group(iface, 5, world, rank, cmb)
+    place = None
+    if len(sys.argv) > 5:
+        ppn, sock, radix, factor, thresh = map(int, sys.argv[5].split(":"))
+        place = dict(ppn=ppn, socket=sock or None, radix=radix, factor=factor,
+                     sock_thresh=thresh)
+        group = ops.Group(iface, 5, world, rank, cmb,
+                          distance=ops.layout_distances(world, rank, ppn, sock or None),
+                          radix=radix, sock_thresh=thresh, factor=factor)
+    else:
+        group = ops.Group(iface, 5, world, rank, cmb)
     pow2 = (world & (world - 1)) == 0
     rc = 0
     for k in range(40):
@@ -43,7 +57,15 @@ def main():
         in_place = bool(rng.random() < 0.3)
         inputs = [O.fill(dt, dist, seed * 1000 + 10 * k + r, count) for r in range(world)]
         sbuf = inputs[rank].copy()
-        if kind == "allreduce":
+        if place and kind == "allreduce":
+            want = P.simulate(kind, op, dt, inputs, **place)[rank]
+            rbuf = sbuf if in_place else np.zeros_like(sbuf)
+            coll = group.allreduce(sbuf, rbuf, count, DTYPES[dt], OPS[op])
+        elif place:
+            want = P.simulate(kind, op, dt, inputs, root=root, **place)[root]
+            rbuf = (sbuf if in_place else np.zeros_like(sbuf)) if rank == root else None
+            coll = group.reduce(sbuf, rbuf, count, DTYPES[dt], OPS[op], root)
+        elif kind == "allreduce":
             want = O.reduce_multi(op, dt, inputs, rank) if pow2 else \
                 O.tree_reduce(op, dt, inputs, 0)
             rbuf = sbuf if in_place else np.zeros_like(sbuf)

@@ -113,6 +113,19 @@ def test_engine_placements_host(spec):
         assert all(x == d[0] for x in d), d
 
 
+@pytest.mark.parametrize("seed,world,max_short,cells,place", [
+    (21, 12, 256, 4, "3:0:2:2:16"), (22, 8, 64, 64, "4:2:8:2:4"),
+    (23, 16, 1024, 8, "4:0:8:4:16"), (24, 6, 128, 3, "1:0:2:2:16")])
+def test_engine_fuzz_placements(seed, world, max_short, cells, place):
+    """The seeded 40-op sequence of test_engine_fuzz on placements: random
+    integer dtype and op (or fp SUM of exact values), count 0-6000, allreduce
+    or reduce to a random root, in place or not, small rings (resends) -
+    every result bit-exact against the oracle's simulation."""
+    codes, outs = launch("_worker_fuzz.py", world,
+                         args=(shm_name(), seed, max_short, cells, place), timeout=300)
+    assert codes == [0] * world, "\n".join(outs)
+
+
 def test_engine_rejects_bad_distance_arrays():
     mpi = MockMPI()
     cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
