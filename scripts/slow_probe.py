@@ -8,7 +8,9 @@ HIP events, median of 3 batches) on
   - the bench's pair (two separate 256 MiB allocations), and
   - src and dst carved out of one allocation at distances of 256 MiB plus
     0, 4 KiB, 64 KiB, 1 MiB and 2 MiB + 4 KiB (where the two streams fall in
-    the channel / bank interleave).
+    the channel / bank interleave),
+  - a one-stream read (src = dst: the second load of each lane is an L2
+    hit, so HBM sees one stream of N bytes).
 
     python scripts/slow_probe.py [out.json]
 """
@@ -54,6 +56,12 @@ def main():
             ctx.fill("float32", "round", 41, d, N)      # the copy overwrote dst
             print(row, flush=True)
             rows.append(row)
+        # one stream: both loads of a lane on the same address (the second
+        # an L2 hit), so HBM sees N bytes of reads in one stream
+        ou = med3(lambda: ctx.profile_stream(0, a.ptr, a.ptr, N * 4, 40))
+        rows.append({"round": rnd, "pair": "one stream (src = dst)",
+                     "read1_gbs": round(N * 4 / (ou * 1e-6) / 1e9, 1)})
+        print(rows[-1], flush=True)
     if len(sys.argv) > 1:
         with open(sys.argv[1], "w") as f:
             json.dump(rows, f, indent=1)
