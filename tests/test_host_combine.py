@@ -281,6 +281,24 @@ def test_stage_fuzz_c_harness_bit_exact(seed):
 
 
 @pytest.mark.gpu
+def test_thread_fuzz_c_harness_bit_exact():
+    """tests/c/thread_fuzz.c: one combine object (and its device context)
+    shared by four host threads, as UCG shares it between the progress
+    thread and the async resend thread: staged steps fragment by fragment on
+    one, whole-buffer combines on pageable, pinned and device-resident
+    buffers on three, every result bit-exact against the oracle."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "c", "_build", "thread_fuzz")
+    p = subprocess.run([exe, "40"], capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout + p.stderr
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["bit_exact"] is True and line["steps_on_device"] == 40
+    assert line["device_calls"] > 240
+
+
+@pytest.mark.gpu
 def test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu():
     """UCX_BUILTIN_DEV_COMBINE=y (default): a host recv buffer is combined by
     reduce_cb_f (staging would cross PCIe); a device-resident one
