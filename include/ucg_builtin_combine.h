@@ -111,6 +111,13 @@ size_t       ucg_builtin_combine_atomic_sum_length(ucg_builtin_combine_t *cmb,
                                                    void *reduce_op,
                                                    void *datatype);
 
+/* The checks ucg_builtin_step_create makes for a step that reduces
+ * (builtin/ops/builtin_control.c:872-888): UCS_ERR_UNSUPPORTED for a
+ * non-commutative op (is_commutative_f) or MPI_MINLOC/MAXLOC
+ * (is_loc_expected_f). */
+ucs_status_t ucg_builtin_combine_check_reduction(ucg_builtin_combine_t *cmb,
+                                                 void *reduce_op);
+
 ucs_status_t ucg_builtin_combine_reduce(ucg_builtin_combine_t *cmb,
                                         void *reduce_op, void *src, void *dst,
                                         int dcount, void *datatype);

@@ -143,6 +143,37 @@ def test_tree_intra_restatement():
     assert up == [1] and down == []
 
 
+def test_reductions_reject_minloc_and_noncommutative_ops():
+    """builtin_control.c:872-888: a reducing plan refuses MPI_MINLOC/MAXLOC
+    (is_loc_expected_f) and non-commutative ops (is_commutative_f) with
+    UCS_ERR_UNSUPPORTED - here on every member, reducing or not."""
+    from mock_mpi import OP_MINLOC
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    assert cmb.check_reduction(OP_MINLOC) == -22
+    assert cmb.check_reduction(OPS["sum"]) == 0
+    cmb.close()
+    noncomm = MockMPI()
+    noncomm.is_commutative_f = staticmethod(lambda op: op != OPS["prod"])
+    cmb = host.BuiltinCombine(noncomm.callbacks(), host.make_config(dev_enable=0))
+    assert cmb.check_reduction(OPS["prod"]) == -22
+    cmb.close()
+    # through the engine: a 2-member group, member 0's view (no message sent)
+    iface = ops.ShmIface(shm_name(), 1, 0, max_short=256)
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    g = ops.Group(iface, 3, 1, 0, cmb)
+    x = np.arange(16, dtype=np.int32)
+    y = np.zeros_like(x)
+    # a one-member group has no reducing step: nothing to refuse
+    c = g.allreduce(x, y, 16, DTYPES["int32"], OP_MINLOC)
+    assert c.status == 0
+    c.close()
+    g.close()
+    iface.close()
+    cmb.close()
+
+
 def test_allreduce_rejects_bad_reduce_root():
     mpi = MockMPI()
     cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))

@@ -236,6 +236,24 @@ size_t ucg_builtin_combine_atomic_sum_length(ucg_builtin_combine_t *cmb,
     return (len == 1 || len == 2 || len == 4 || len == 8) ? len : 0;
 }
 
+/* builtin_control.c:872-888: a plan step that reduces needs the reduce_op
+ * callbacks, a commutative op (the plans reduce in arrival order) and not
+ * MPI_MINLOC/MAXLOC */
+ucs_status_t ucg_builtin_combine_check_reduction(ucg_builtin_combine_t *cmb,
+                                                 void *reduce_op)
+{
+    if (cmb == NULL || cmb->params.reduce_cb_f == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (cmb->params.is_commutative_f && !cmb->params.is_commutative_f(reduce_op)) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    if (cmb->params.is_loc_expected_f && cmb->params.is_loc_expected_f(reduce_op)) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    return UCS_OK;
+}
+
 int ucg_builtin_combine_classify(ucg_builtin_combine_t *cmb, void *reduce_op,
                                  void *datatype, ucg_dev_op_t *op_out,
                                  ucg_dev_dtype_t *dt_out)

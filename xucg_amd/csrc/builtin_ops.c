@@ -1506,7 +1506,11 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
         c->plan        = "none";
         c->init_reduce = 1;
         st = UCS_OK;
-    } else if ((st = plan_ctx_init(g, 0, &pc)) == UCS_OK) {
+    } else if ((st = ucg_builtin_combine_check_reduction(g->cmb, op)) == UCS_OK &&
+               (st = plan_ctx_init(g, 0, &pc)) == UCS_OK) {
+        /* the reduction checks of builtin_control.c:872-888 are made by every
+         * member, not only by those with a reducing step: a leaf that went
+         * ahead would wait for a fan-out nobody sends */
         st = allreduce_use_tree(g->size) ? plan_tree(c, &pc, 1, &ppn) :
                                            plan_recursive(c, &pc, &ppn);
         if (st == UCS_OK) {
@@ -1543,7 +1547,8 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
     if (g->size == 1) {
         c->plan        = "none";
         c->init_reduce = 1;
-    } else if ((st = plan_ctx_init(g, root, &pc)) != UCS_OK ||
+    } else if ((st = ucg_builtin_combine_check_reduction(g->cmb, op)) != UCS_OK ||
+               (st = plan_ctx_init(g, root, &pc)) != UCS_OK ||
                (st = plan_tree(c, &pc, 0, &ppn)) != UCS_OK ||
                (st = plan_finish(c, ppn)) != UCS_OK) {
         free(c);

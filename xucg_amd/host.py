@@ -123,6 +123,11 @@ class BuiltinCombine:
                                                       ctypes.byref(o), ctypes.byref(d))
         return (o.value, d.value) if ok else None
 
+    def check_reduction(self, op):
+        """0, or UCS_ERR_UNSUPPORTED for MINLOC/MAXLOC and non-commutative
+        ops (builtin_control.c:872-888)."""
+        return _lib.host().ucg_builtin_combine_check_reduction(self.handle, op)
+
     def reduce(self, op, src, dst, count, dtype):
         return _lib.host().ucg_builtin_combine_reduce(self.handle, op, _vp(src),
                                                       _vp(dst), count, dtype)

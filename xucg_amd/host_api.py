@@ -58,6 +58,7 @@ HOST_API = {
     "ucg_builtin_recursive_peer": (_u64, [_u64, _u, _u, _u]),
     "ucg_builtin_combine_dtype_length": (_sz, [_vp, _vp]),
     "ucg_builtin_combine_atomic_sum_length": (_sz, [_vp, _vp, _vp]),
+    "ucg_builtin_combine_check_reduction": (_int, [_vp, _vp]),
     # include/ucg_builtin_ops.h
     "ucg_builtin_shm_iface_open": (_int, [ctypes.c_char_p, _u, _u, _sz, _u,
                                           ctypes.POINTER(_vp)]),
