@@ -119,7 +119,7 @@ int main(int argc, char **argv)
         fprintf(stderr, "rank %u: allreduce create failed\n", rank);
         return 1;
     }
-    for (i = 0; i < 100; i++) {        /* warm-up */
+    for (i = 0; i < (count > 65536 ? 2 : 100); i++) {        /* warm-up */
         if (ucg_builtin_lcoll_start(c) == UCS_INPROGRESS) {
             ucg_builtin_lcoll_wait(c);
         }
