@@ -134,6 +134,10 @@ ucs_status_t ucg_builtin_combine_fragment(ucg_builtin_combine_t *cmb,
                                           size_t offset, const void *src,
                                           size_t length);
 ucs_status_t ucg_builtin_combine_step_end(ucg_builtin_combine_t *cmb);
+/* 1 when the open step is mirrored on the device (its fragments land in the
+ * accumulator only at step_end), 0 when each fragment is combined into the
+ * recv buffer by the time ucg_builtin_combine_fragment returns. */
+int          ucg_builtin_combine_step_on_device(ucg_builtin_combine_t *cmb);
 
 /* [0] host calls, [1] host bytes, [2] device calls, [3] device bytes,
  * [4] steps staged on the device, [5] callback errors seen */

@@ -44,15 +44,18 @@ def test_c1_harness_bit_exact(max_short, world):
     assert line["bit_exact"] and line["ranks"] == world and line["bytes"] == 4096
 
 
-@pytest.mark.parametrize("world,max_short,plan,incast,place", [
-    (4, 256, "", "", ""), (3, 256, "", "", ""), (8, 100, "", "", ""),
-    (4, 256, "tree", "1", ""), (5, 64, "tree", "", ""),
-    (8, 256, "", "", "4"), (12, 100, "", "", "3"), (8, 256, "tree", "1", "8:4")])
-def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast, place):
+@pytest.mark.parametrize("world,max_short,plan,incast,place,pipe", [
+    (4, 256, "", "", "", ""), (3, 256, "", "", "", ""), (8, 100, "", "", "", ""),
+    (4, 256, "tree", "1", "", ""), (5, 64, "tree", "", "", ""),
+    (8, 256, "", "", "4", ""), (12, 100, "", "", "3", ""), (8, 256, "tree", "1", "8:4", ""),
+    (12, 100, "", "", "3", "y")])
+def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast, place,
+                                    pipe):
     """The host engine (libucg_builtin.so sources) and the C1 harness rebuilt
     with ASan + UBSan (tests/c/Makefile, target asan): recursive and tree
-    plans, fragmenting and resend-heavy sizes, the incast fan-in. Any
-    sanitizer report (invalid access, UB, leak at exit) fails the rank."""
+    plans, fragmenting and resend-heavy sizes, the incast fan-in, waypoints
+    forwarding fragment by fragment. Any sanitizer report (invalid access, UB,
+    leak at exit) fails the rank."""
     import json
     import subprocess
     cdir = os.path.join(os.path.dirname(__file__), "c")
@@ -64,6 +67,8 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
         monkeypatch.setenv("UCX_BUILTIN_ALLREDUCE_PLAN", plan)
     if incast:
         monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", incast)
+    if pipe:
+        monkeypatch.setenv("UCX_BUILTIN_PIPELINE", pipe)
     if place:
         # placements (test_topology.py): hosts of C1_PPN, sockets of
         # C1_SOCKET; radix 2 so 4 hosts of 3 have an inter-host waypoint, and

@@ -113,17 +113,40 @@ def test_engine_placements_host(spec):
         assert all(x == d[0] for x in d), d
 
 
-@pytest.mark.parametrize("seed,world,max_short,cells,place", [
-    (21, 12, 256, 4, "3:0:2:2:16"), (22, 8, 64, 64, "4:2:8:2:4"),
-    (23, 16, 1024, 8, "4:0:8:4:16"), (24, 6, 128, 3, "1:0:2:2:16")])
-def test_engine_fuzz_placements(seed, world, max_short, cells, place):
+@pytest.mark.parametrize("seed,world,max_short,cells,place,pipeline", [
+    (21, 12, 256, 4, "3:0:2:2:16", "n"), (22, 8, 64, 64, "4:2:8:2:4", "n"),
+    (23, 16, 1024, 8, "4:0:8:4:16", "n"), (24, 6, 128, 3, "1:0:2:2:16", "n"),
+    (25, 12, 64, 3, "3:0:2:2:16", "y"), (26, 12, 128, 4, "2:0:2:2:16", "y")])
+def test_engine_fuzz_placements(seed, world, max_short, cells, place, pipeline,
+                                monkeypatch):
     """The seeded 40-op sequence of test_engine_fuzz on placements: random
     integer dtype and op (or fp SUM of exact values), count 0-6000, allreduce
     or reduce to a random root, in place or not, small rings (resends) -
-    every result bit-exact against the oracle's simulation."""
+    every result bit-exact against the oracle's simulation; the last two with
+    the waypoints forwarding fragment by fragment (UCX_BUILTIN_PIPELINE=y)
+    through rings of 3-4 cells, so the pipelined sends get NO_RESOURCE and
+    resume."""
+    monkeypatch.setenv("UCX_BUILTIN_PIPELINE", pipeline)
     codes, outs = launch("_worker_fuzz.py", world,
                          args=(shm_name(), seed, max_short, cells, place), timeout=300)
     assert codes == [0] * world, "\n".join(outs)
+
+
+@pytest.mark.parametrize("pipeline", ["y", "n"])
+@pytest.mark.parametrize("spec,max_short", [("12:3:0:2:2:16", 64), ("6:6:3:8:2:4", 100)])
+def test_waypoint_pipelining_on_and_off(spec, max_short, pipeline, monkeypatch):
+    """Fragmented waypoints forward each fragment once all its contributions
+    are in (PIPELINED / BY_FRAGMENT_OFFSET, builtin_control.c:831-834,
+    builtin_data.c:425-520) with UCX_BUILTIN_PIPELINE=y, or - the default
+    of this engine - the whole message after the last one: the same plans and the same bits either way,
+    with small messages (many fragments per step)."""
+    monkeypatch.setenv("UCX_BUILTIN_PIPELINE", pipeline)
+    n = int(spec.split(":")[0])
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "host", max_short, spec),
+                         timeout=300)
+    assert codes == [0] * n, "\n".join(outs)
+    text = "\n".join(outs)
+    assert ("(pipelined by fragment)" in text) == (pipeline == "y")
 
 
 def test_engine_rejects_bad_distance_arrays():

@@ -463,6 +463,18 @@ ucs_status_t ucg_builtin_combine_step_end(ucg_builtin_combine_t *cmb)
     return st;
 }
 
+int ucg_builtin_combine_step_on_device(ucg_builtin_combine_t *cmb)
+{
+    int on;
+    if (cmb == NULL) {
+        return 0;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    on = cmb->step.active && cmb->step.on_dev;
+    pthread_mutex_unlock(&cmb->lock);
+    return on;
+}
+
 void ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb, uint64_t out[6])
 {
     int i;

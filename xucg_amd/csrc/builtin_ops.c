@@ -444,6 +444,10 @@ typedef struct {
                                      before its sends (RECV_BEFORE_SEND1 /
                                      RECV1_BEFORE_SEND, builtin_control.c:
                                      379-389) */
+    int         pipelined;        /* a fragmented waypoint: each fragment goes
+                                     on once all its contributions are in
+                                     (PIPELINED / BY_FRAGMENT_OFFSET,
+                                     builtin_control.c:831-834, 978-980) */
     int         incast;           /* sends / receives go through the incast */
     uint8_t     packer;           /* op_packer_t of an incast send */
     unsigned    incast_expected;  /* children packing each incast message */
@@ -456,6 +460,7 @@ typedef struct {
     ucg_builtin_lcoll_t *req;     /* the op running in this slot */
     uint16_t             expecting;
     stash_t             *msgs;    /* slot->messages */
+    stash_t            **msgs_tail; /* &last->next (or &msgs): O(1) append */
 } op_slot_t;
 
 struct ucg_builtin_lgroup {
@@ -504,6 +509,17 @@ struct ucg_builtin_lcoll {
     int          step_open;       /* a combine step is open */
     int          send_pending;
     int          recv_done;       /* a recv_first step has all its data */
+    /* the pipelined waypoint step in progress (builtin_data.c:425-520,
+     * builtin_comp_step.inl:155-174) */
+    int          pipelining;      /* this step forwards fragment by fragment */
+    unsigned    *frag_left;       /* contributions still due per fragment
+                                   * (not a byte: a waypoint may have more
+                                   * than 255 children) */
+    uint64_t    *frag_fifo;       /* complete fragments not yet sent out */
+    uint64_t     fifo_head, fifo_tail;
+    unsigned     fifo_ep;         /* next endpoint of the head fragment */
+    uint64_t     frags_sent;
+    uint64_t     pipe_cap;        /* entries of frag_left and frag_fifo */
     unsigned     iter_ep;
     size_t       iter_offset;
 };
@@ -532,6 +548,13 @@ static void stash_append(stash_t **list, stash_t *m)
     *list = m;
 }
 
+/* a slot's stash is appended to on every early message: keep it O(1) */
+static void slot_stash(op_slot_t *slot, stash_t *m)
+{
+    *slot->msgs_tail = m;
+    slot->msgs_tail  = &m->next;
+}
+
 /* finish the op: ucg_builtin_comp_last_step_cb, builtin_comp_step.inl:8-38 */
 static void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
 {
@@ -556,9 +579,12 @@ static void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
 static void check_pending(ucg_builtin_lcoll_t *c, uint16_t local_id)
 {
     op_slot_t *slot = &c->g->slots[c->coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    stash_t **pp = &slot->msgs, *m;
     slot->expecting = local_id;
     for (;;) {
-        stash_t **pp = &slot->msgs, *m;
+        /* the messages before pp did not match and still do not: a step
+         * that is not done yet only sends from recv_cb, so the list is not
+         * touched behind the cursor */
         while (*pp) {
             ops_header_t h;
             h.header = (*pp)->header;
@@ -571,6 +597,9 @@ static void check_pending(ucg_builtin_lcoll_t *c, uint16_t local_id)
             return;
         }
         *pp = m->next;   /* remove first: the next call may recurse here */
+        if (m->next == NULL) {
+            slot->msgs_tail = pp;
+        }
         ops_header_t h;
         h.header = m->header;
         int step_done = recv_cb(c, h.remote_offset, m->data, m->length);
@@ -732,6 +761,48 @@ static int step_send(ucg_builtin_lcoll_t *c)
     return 1;
 }
 
+/* the sends of a pipelined waypoint: every fragment whose contributions are
+ * all in, to every endpoint of the step, oldest first, resumable after
+ * UCS_ERR_NO_RESOURCE at (fifo_head, fifo_ep) - the reference marks such a
+ * fragment FRAG_PENDING and resends it (builtin_data.c:496-520, 650-657).
+ * Returns 1 when nothing is left to send for now, 0 when it has to be
+ * resumed or the op failed. */
+static int pipe_send(ucg_builtin_lcoll_t *c)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    op_step_t *s = &c->steps[c->cur];
+    ops_header_t h;
+    ucs_status_t st;
+
+    h.header   = 0;
+    h.group_id = g->group_id;
+    h.coll_id  = c->coll_id;
+    h.step_idx = s->step_idx;
+    while (c->fifo_head != c->fifo_tail) {
+        const uint64_t idx = c->frag_fifo[c->fifo_head % c->pipe_cap];
+        const size_t off   = (size_t)idx * s->frag_len;
+        const size_t n     = c->length - off < s->frag_len ? c->length - off : s->frag_len;
+        h.remote_offset    = (uint32_t)off;
+        for (; c->fifo_ep < s->send_cnt; c->fifo_ep++) {
+            st = send_one(c, s, s->send_peers[c->fifo_ep], h.header, c->rbuf + off, n);
+            if (st == UCS_ERR_NO_RESOURCE) {
+                c->send_pending = 1;
+                return 0;
+            }
+            if (st != UCS_OK) {
+                finish(c, st);
+                return 0;
+            }
+            g->stats[0]++;
+        }
+        c->fifo_ep = 0;
+        c->fifo_head++;
+        c->frags_sent++;
+    }
+    c->send_pending = 0;
+    return 1;
+}
+
 /* ucg_builtin_step_execute, builtin_data.c:411-668. A step sends first and
  * then either completes (no receive: comp_criteria SEND, builtin_control.c:
  * 1000-1002) or drains what is already stashed for it (builtin_comp_step.inl:
@@ -764,11 +835,38 @@ static void step_execute(ucg_builtin_lcoll_t *c)
         c->pending      = s->fragments_total;
         c->iter_ep      = 0;
         c->iter_offset  = 0;
+        /* fragment by fragment only while each fragment is combined into
+         * recv.buffer as it arrives: a step mirrored on the device holds its
+         * data until step_end */
+        c->pipelining   = s->pipelined &&
+                          !(c->step_open && ucg_builtin_combine_step_on_device(g->cmb));
+        if (c->pipelining) {
+            uint64_t f;
+            for (f = 0; f < s->frags; f++) {
+                c->frag_left[f] = s->recv_cnt;
+            }
+            c->fifo_head  = c->fifo_tail = 0;
+            c->fifo_ep    = 0;
+            c->frags_sent = 0;
+        }
     }
     h.header   = 0;
     h.group_id = g->group_id;
     h.coll_id  = c->coll_id;
     h.step_idx = s->step_idx;
+    if (c->pipelining) {
+        if (!pipe_send(c)) {
+            return;
+        }
+        if (c->recv_done && c->frags_sent == s->frags) {
+            step_complete(c);
+            return;
+        }
+        if (!c->recv_done) {
+            check_pending(c, h.local_id);
+        }
+        return;
+    }
     if (s->recv_first && !c->recv_done) {
         check_pending(c, h.local_id);
         return;
@@ -807,6 +905,26 @@ static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
     if (st != UCS_OK) {
         finish(c, st);      /* recv_handle_error, :332-333 */
         return 1;
+    }
+    if (c->pipelining) {
+        /* ucg_builtin_comp_send_check_frag_by_offset, :155-174: the
+         * fragment at this offset is complete once every contributor's part
+         * of it was combined; it goes on at once */
+        const uint64_t idx = offset / s->frag_len;
+        if (--c->frag_left[idx] == 0) {
+            c->frag_fifo[c->fifo_tail++ % c->pipe_cap] = idx;
+        }
+        if (--c->pending == 0) {
+            c->recv_done = 1;
+        }
+        if (!pipe_send(c)) {
+            return c->recv_done || c->done;   /* resumed by the resend path */
+        }
+        if (c->recv_done && c->frags_sent == s->frags) {
+            step_complete(c);
+            return 1;
+        }
+        return c->recv_done;
     }
     if (--c->pending != 0) {
         return 0;
@@ -859,7 +977,7 @@ static ucs_status_t am_handler(void *arg, void *data, size_t length)
     if (m == NULL) {
         return UCS_ERR_NO_MEMORY;
     }
-    stash_append(&slot->msgs, m);
+    slot_stash(slot, m);
     return UCS_OK;
 }
 
@@ -910,6 +1028,9 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
         const char *e = getenv("UCX_BUILTIN_SM_INCAST");
         g->incast = e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1');
     }
+    for (m = 0; m < UCG_BUILTIN_OPS_MAX_CONCURRENT; m++) {
+        g->slots[m].msgs_tail = &g->slots[m].msgs;
+    }
     for (m = 0; m < member_count; m++) {
         g->distance[m] = (params && params->distance) ? params->distance[m] :
                          (m == my_index) ? UCG_BUILTIN_DISTANCE_SELF : UCG_BUILTIN_DISTANCE_HOST;
@@ -932,7 +1053,7 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
             stash_t *msg = *pp;
             *pp = msg->next;
             msg->next = NULL;
-            stash_append(&g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT].msgs, msg);
+            slot_stash(&g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT], msg);
         } else {
             pp = &(*pp)->next;
         }
@@ -1403,12 +1524,23 @@ static ucs_status_t plan_recursive(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc,
  * accumulator is seeded (ucg_builtin_init_reduce) when the member reduces,
  * and the SM-root children of a one-level host fan-in may pack into one
  * incast cell at their master (builtin_control.c:535-537) */
+/* The reference forwards every fragmented waypoint fragment by fragment
+ * (builtin_control.c:831-834). On the shared-memory transport of this engine
+ * that is slower (early fragments land in the parent's stash
+ * while it still fans in), so it is off unless UCX_BUILTIN_PIPELINE=y. */
+static int pipeline_enabled(void)
+{
+    const char *e = getenv("UCX_BUILTIN_PIPELINE");
+    return e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1');
+}
+
 static ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn)
 {
     ucg_builtin_lgroup_t *g = c->g;
     int received = 0;
     unsigned k;
     c->init_reduce = 0;
+    c->pipe_cap    = 0;
     for (k = 0; k < c->nsteps; k++) {
         op_step_t *s = &c->steps[k];
         s->send_recv_buffer = received || s->recv_first;
@@ -1420,6 +1552,10 @@ static ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn)
         }
         if (step_fragments(c, s) != UCS_OK) {
             return UCS_ERR_UNSUPPORTED;
+        }
+        s->pipelined = s->recv_first && s->frag_len && pipeline_enabled();
+        if (s->pipelined && s->frags > c->pipe_cap) {
+            c->pipe_cap = s->frags;
         }
         if (g->incast && s->step_idx == 1 && ppn > 2 && ppn < g->sock_thresh) {
             if (s->method == M_REDUCE_TERMINAL) {
@@ -1433,7 +1569,27 @@ static ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn)
             }
         }
     }
+    if (c->pipe_cap) {
+        /* one count per fragment (the reference allocates sizeof(ep_cnt)
+         * bytes for frags_per_ep counts, builtin_control.c:738-739 against
+         * builtin_data.c:433) */
+        c->frag_left = malloc(c->pipe_cap * sizeof(*c->frag_left));
+        c->frag_fifo = malloc(c->pipe_cap * sizeof(*c->frag_fifo));
+        if (c->frag_left == NULL || c->frag_fifo == NULL) {
+            return UCS_ERR_NO_MEMORY;
+        }
+    }
     return UCS_OK;
+}
+
+static void lcoll_free(ucg_builtin_lcoll_t *c)
+{
+    if (c) {
+        free(c->scratch);
+        free(c->frag_left);
+        free(c->frag_fifo);
+    }
+    free(c);
 }
 
 static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
@@ -1518,7 +1674,7 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
         }
     }
     if (st != UCS_OK) {
-        free(c);
+        lcoll_free(c);
         return st;
     }
     *coll_p = c;
@@ -1551,7 +1707,7 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
                (st = plan_ctx_init(g, root, &pc)) != UCS_OK ||
                (st = plan_tree(c, &pc, 0, &ppn)) != UCS_OK ||
                (st = plan_finish(c, ppn)) != UCS_OK) {
-        free(c);
+        lcoll_free(c);
         return st;
     }
     /* a member other than the root that combines on the way (a host master,
@@ -1561,7 +1717,7 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
         if (c->steps[k].aggregation != AGG_NOP) {
             c->scratch = malloc(c->length ? c->length : 1);
             if (c->scratch == NULL) {
-                free(c);
+                lcoll_free(c);
                 return UCS_ERR_NO_MEMORY;
             }
             c->rbuf = c->scratch;
@@ -1656,10 +1812,7 @@ void ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *c)
     if (c && c->active) {
         finish(c, UCS_ERR_CANCELED);
     }
-    if (c) {
-        free(c->scratch);
-    }
-    free(c);
+    lcoll_free(c);
 }
 
 size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
@@ -1700,6 +1853,9 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             PUT(", then send recv.buffer to");
             for (e = 0; e < s->send_cnt; e++) {
                 PUT(" %u", s->send_peers[e]);
+            }
+            if (s->pipelined) {
+                PUT(" (pipelined by fragment)");
             }
         }
         if (s->incast) {

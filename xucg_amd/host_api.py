@@ -50,6 +50,7 @@ HOST_API = {
     "ucg_builtin_combine_step_begin": (_int, [_vp, _vp, _vp, _vp, _sz]),
     "ucg_builtin_combine_fragment": (_int, [_vp, _sz, _vp, _sz]),
     "ucg_builtin_combine_step_end": (_int, [_vp]),
+    "ucg_builtin_combine_step_on_device": (_int, [_vp]),
     "ucg_builtin_combine_stats": (None, [_vp, ctypes.POINTER(_u64)]),
     "ucg_builtin_step_fragment_length": (_sz, [_sz, _sz]),
     "ucg_builtin_step_fragments_total": (_u64, [_sz, _sz, _u]),
