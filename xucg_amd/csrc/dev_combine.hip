@@ -1316,9 +1316,14 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
      * exported through hipIpcGetMemHandle (ucg_builtin_dev_ipc_export) */
     const size_t gran = (size_t)2 << 20;
     bytes = bytes ? (bytes + gran - 1) / gran * gran : gran;
-    hipError_t e = hipMalloc(&p, bytes);
+    /* A/B knob: UCX_BUILTIN_DEV_MALLOC=contiguous asks the runtime for
+     * physically contiguous memory ("Slow phases") */
+    const char *kind = getenv("UCX_BUILTIN_DEV_MALLOC");
+    const bool contiguous = kind && kind[0] == 'c';
+    hipError_t e = contiguous ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous)
+                              : hipMalloc(&p, bytes);
     if (e != hipSuccess) {
-        hip_status(e, "hipMalloc");
+        hip_status(e, contiguous ? "hipExtMallocWithFlags(contiguous)" : "hipMalloc");
         return nullptr;
     }
     return p;
