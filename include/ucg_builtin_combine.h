@@ -139,6 +139,34 @@ ucs_status_t ucg_builtin_combine_step_end(ucg_builtin_combine_t *cmb);
  * recv buffer by the time ucg_builtin_combine_fragment returns. */
 int          ucg_builtin_combine_step_on_device(ucg_builtin_combine_t *cmb);
 
+/* ---- device-resident buffers: the engine's remote-key steps ------------- */
+/* The zero-copy form of a step (the reference's rkey exchange and
+ * SEND_GET_ZCOPY, builtin_control.c:1014-1076, builtin_data.c:326-340) for
+ * buffers in GPU memory: each member exposes a device buffer of its own
+ * through a HIP IPC handle (the packed remote key, once per op), and a
+ * receiver reads its peers' buffers over xGMI in one kernel. Every call takes
+ * the combine's lock and returns once the device work is complete. */
+void        *ucg_builtin_combine_dev_alloc(ucg_builtin_combine_t *cmb, size_t bytes);
+void         ucg_builtin_combine_dev_free(ucg_builtin_combine_t *cmb, void *ptr);
+ucs_status_t ucg_builtin_combine_dev_export(ucg_builtin_combine_t *cmb,
+                                            const void *dev_ptr, void *handle);
+ucs_status_t ucg_builtin_combine_dev_import(ucg_builtin_combine_t *cmb,
+                                            const void *handle, void **dev_ptr);
+void         ucg_builtin_combine_dev_release(ucg_builtin_combine_t *cmb, void *dev_ptr);
+/* dst = srcs[nsrc-1] (op) (... (srcs[1] (op) srcs[0])): the accumulator
+ * srcs[0] with every peer's data reduced into it in the given (arrival)
+ * order, as reduce_cb_f would one message at a time (builtin_comp_step.inl:
+ * 213-221). Any nsrc >= 1 (launched 16 operands at a time); dst may alias
+ * srcs[0]; srcs may be peer-mapped. UCS_ERR_UNSUPPORTED for an (op, dtype)
+ * the device cannot classify. */
+ucs_status_t ucg_builtin_combine_dev_fold(ucg_builtin_combine_t *cmb, void *reduce_op,
+                                          void *datatype, void *dst,
+                                          const void *const *srcs, unsigned nsrc,
+                                          size_t count);
+/* dst[0:bytes] = src[0:bytes], either side device or peer-mapped memory */
+ucs_status_t ucg_builtin_combine_dev_copy(ucg_builtin_combine_t *cmb, void *dst,
+                                          const void *src, size_t bytes);
+
 /* [0] host calls, [1] host bytes, [2] device calls, [3] device bytes,
  * [4] steps staged on the device, [5] callback errors seen */
 void         ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb,

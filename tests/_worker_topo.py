@@ -4,9 +4,13 @@ against the oracle's restatement (oracle/plans.py), then allreduce and
 reduce to several roots run and are checked against the oracle's simulation
 of every member's plan.
 
-    _worker_topo.py <shm-name> <mode: host|dev> <max_short> <n:ppn:socket:radix:factor:thresh>
+    _worker_topo.py <shm-name> <mode: host|dev|rma> <max_short> <n:ppn:socket:radix:factor:thresh>
 
-socket = 0 means no socket level. The transport is the shared-memory one
+socket = 0 means no socket level. Mode dev stages every REDUCE step of host
+buffers on the GPU; mode rma gives the engine device buffers (GPU memory on
+device rank % device count), which it runs as remote-key steps: keys once per
+op, READY / DONE over the transport, every receive one kernel reading the
+senders' buffers. The transport is the shared-memory one
 for every member: a NET distance changes the plan, not the wire.
 
 Checks:
@@ -62,13 +66,34 @@ def main():
     world = int(os.environ["WORLD_SIZE"])
     assert world == n
     mpi = MockMPI()
-    cfg = (host.make_config(dev_enable=2, dev_min_bytes=0, stage_bytes=1 << 16)
-           if mode == "dev" else host.make_config(dev_enable=0))
+    dctx = None
+    if mode == "rma":
+        import xucg_amd
+        from xucg_amd import _lib
+        ndev = max(1, _lib.dev().ucg_builtin_dev_device_count())
+        dctx = xucg_amd.DevContext(device=rank % ndev)
+        cfg = host.make_config(device=rank % ndev)
+    elif mode == "dev":
+        cfg = host.make_config(dev_enable=2, dev_min_bytes=0, stage_bytes=1 << 16)
+    else:
+        cfg = host.make_config(dev_enable=0)
     cmb = host.BuiltinCombine(mpi.callbacks(), cfg, op_classifier=op_classifier,
                               dt_classifier=dt_classifier)
-    if mode == "dev" and not cmb.has_device:
+    if mode in ("dev", "rma") and not cmb.has_device:
         print("no device", flush=True)
         sys.exit(2)
+
+    def buf(a):
+        """the op's buffer: the array itself, or a device copy of it"""
+        if dctx is None:
+            return a
+        b = dctx.alloc(max(a.nbytes, 1))
+        b.upload(a)
+        return b
+
+    def back(b, like):
+        return b if dctx is None else b.download(like.dtype, like.size)
+
     iface = ops.ShmIface(name, n, rank, max_short=max_short, ring_cells=16)
     dist = ops.layout_distances(n, rank, ppn, socket or None)
     assert dist == P.layout(n, rank, ppn, socket or None)
@@ -93,8 +118,9 @@ def main():
                 oplan = P.plan(kind, n, rank, root=root, **cfgkw)
             except P.Unsupported:
                 want = oplan = None
-            sbuf = inputs[rank].copy()
-            rbuf = np.zeros_like(sbuf) if (kind == "allreduce" or rank == root) else None
+            sbuf = buf(inputs[rank].copy())
+            rbuf = buf(np.zeros_like(inputs[rank])) if (kind == "allreduce" or
+                                                         rank == root) else None
             coll = (group.allreduce(sbuf, rbuf, count, DTYPES[dt], OPS[op]) if kind == "allreduce"
                     else group.reduce(sbuf, rbuf, count, DTYPES[dt], OPS[op], root))
             if oplan is None:
@@ -114,27 +140,36 @@ def main():
                     fail(f"{kind} root={root} plan\n engine {got}\n oracle {exp}\n{text}")
                 if kind == "allreduce" or root == n - 1:
                     print(f"describe {kind} root={root}:\n{text}", flush=True)
-            st = coll.run()
-            if st != 0:
-                fail(f"{kind} {dt} {op} root={root} status={st}")
-            elif rbuf is not None and not (O.bits(rbuf) == O.bits(want[rank])).all():
-                fail(f"{kind} {dt} {op} n={count} root={root}")
-            if not (O.bits(sbuf) == O.bits(inputs[rank])).all():
+                if (mode == "rma") != ("Buffers: device memory" in text):
+                    fail(f"{kind} root={root}: device buffers not described\n{text}")
+            # persistent: a second start reuses the keys of the first
+            for rep in range(2 if mode == "rma" and ci < 2 else 1):
+                st = coll.run()
+                got = back(rbuf, inputs[rank]) if rbuf is not None else None
+                if st != 0:
+                    fail(f"{kind} {dt} {op} root={root} start {rep} status={st}")
+                elif got is not None and not (O.bits(got) == O.bits(want[rank])).all():
+                    fail(f"{kind} {dt} {op} n={count} root={root} start {rep}")
+            if not (O.bits(back(sbuf, inputs[rank])) == O.bits(inputs[rank])).all():
                 fail(f"{kind} {dt} {op}: send buffer modified")
             coll.close()
+            for b in (sbuf, rbuf):
+                if dctx is not None and b is not None:
+                    b.free()
 
     # rounded fp32: tolerance against the fp64 sum, digests for identity
     for ci, count in enumerate((4096, 1000)):
         xs = [O.fill("float32", "round", 7000 + 11 * ci + m, count) for m in range(n)]
         f64 = np.sum([x.astype(np.float64) for x in xs], axis=0)
         scale = np.sum([np.abs(x.astype(np.float64)) for x in xs], axis=0)
-        rbuf = np.zeros(count, np.float32)
-        sbuf = xs[rank].copy()           # the op keeps the address: keep it alive
-        coll = group.allreduce(sbuf, rbuf, count, DTYPES["float32"], OPS["sum"])
+        rbuf_d = buf(np.zeros(count, np.float32))
+        sbuf = buf(xs[rank].copy())      # the op keeps the address: keep it alive
+        coll = group.allreduce(sbuf, rbuf_d, count, DTYPES["float32"], OPS["sum"])
         if coll.status == UCS_ERR_UNSUPPORTED:
             coll.close()
             continue
         st = coll.run()
+        rbuf = back(rbuf_d, np.zeros(count, np.float32))
         tol = 2 * (n - 1) * 2.0 ** -24 * scale + 1e-30
         err = np.abs(rbuf.astype(np.float64) - f64)
         if st != 0 or not (err <= tol).all():
@@ -148,6 +183,8 @@ def main():
     group.close()
     iface.close()
     cmb.close()
+    if dctx is not None:
+        dctx.close()
     if rc == 0:
         print(f"rank {rank}: ok", flush=True)
     sys.exit(rc)

@@ -175,6 +175,27 @@ def test_layout_distances_match_oracle():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("spec", ["4:4:0:8:2:16", "8:8:0:8:2:16", "6:6:0:8:2:16",
+                                  "12:3:0:2:2:16", "8:8:4:8:2:4", "8:2:0:8:4:16",
+                                  "5:1:0:2:2:16"])
+def test_engine_placements_device_buffers(spec, monkeypatch):
+    """Device buffers: the same plans as remote-key steps (the reference's
+    rkey exchange + zero-copy reads, builtin_control.c:1014-1076,
+    builtin_data.c:326-340) - recursive doubling, the one-host tree, waypoints
+    of the inter-host tree and of the socket level, K-ing with K = 4, a
+    three-level tree - each member's plan equal to the oracle's and every
+    result bit-exact against its simulation, twice per persistent op."""
+    n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")   # a lost message fails fast
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
+                         timeout=150)
+    assert codes == [0] * n, "\n".join(outs)
+    if factor == 2:
+        d = _digests(outs)
+        assert all(x == d[0] for x in d), d
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("spec", ["12:3:0:2:2:16", "8:8:4:8:2:4", "8:4:0:8:2:16"])
 def test_engine_placements_device_staging(spec):
     """The same plans with every REDUCE step (waypoints included) staged on

@@ -475,6 +475,131 @@ int ucg_builtin_combine_step_on_device(ucg_builtin_combine_t *cmb)
     return on;
 }
 
+/* ------------------------------------------------------------------------ */
+/* device-resident buffers (the engine's remote-key steps)                  */
+/* ------------------------------------------------------------------------ */
+void *ucg_builtin_combine_dev_alloc(ucg_builtin_combine_t *cmb, size_t bytes)
+{
+    void *p;
+    if (cmb == NULL || cmb->dev == NULL) {
+        return NULL;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    p = ucg_builtin_dev_malloc(cmb->dev, bytes);
+    pthread_mutex_unlock(&cmb->lock);
+    return p;
+}
+
+void ucg_builtin_combine_dev_free(ucg_builtin_combine_t *cmb, void *ptr)
+{
+    if (cmb == NULL || cmb->dev == NULL || ptr == NULL) {
+        return;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    ucg_builtin_dev_free(cmb->dev, ptr);
+    pthread_mutex_unlock(&cmb->lock);
+}
+
+ucs_status_t ucg_builtin_combine_dev_export(ucg_builtin_combine_t *cmb,
+                                            const void *dev_ptr, void *handle)
+{
+    ucs_status_t st;
+    if (cmb == NULL || cmb->dev == NULL) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    st = ucg_builtin_dev_ipc_export(cmb->dev, dev_ptr, handle);
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
+ucs_status_t ucg_builtin_combine_dev_import(ucg_builtin_combine_t *cmb,
+                                            const void *handle, void **dev_ptr)
+{
+    ucs_status_t st;
+    if (cmb == NULL || cmb->dev == NULL) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    st = ucg_builtin_dev_ipc_import(cmb->dev, handle, dev_ptr);
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
+void ucg_builtin_combine_dev_release(ucg_builtin_combine_t *cmb, void *dev_ptr)
+{
+    if (cmb == NULL || cmb->dev == NULL || dev_ptr == NULL) {
+        return;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    (void)ucg_builtin_dev_ipc_release(cmb->dev, dev_ptr);
+    pthread_mutex_unlock(&cmb->lock);
+}
+
+ucs_status_t ucg_builtin_combine_dev_fold(ucg_builtin_combine_t *cmb, void *reduce_op,
+                                          void *datatype, void *dst,
+                                          const void *const *srcs, unsigned nsrc,
+                                          size_t count)
+{
+    ucg_dev_op_t op;
+    ucg_dev_dtype_t dt;
+    ucs_status_t st = UCS_OK;
+    const void *chunk[16];
+    unsigned done = 0;
+
+    if (cmb == NULL || cmb->dev == NULL || srcs == NULL || nsrc == 0) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (!ucg_builtin_combine_classify(cmb, reduce_op, datatype, &op, &dt)) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    if (count == 0) {
+        return UCS_OK;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    /* acc = srcs[0]; acc = srcs[m] (op) acc: k_reduce_tree takes 16
+     * operands, the accumulator first, so longer folds continue from dst */
+    while (st == UCS_OK && done < nsrc) {
+        unsigned n = 0;
+        chunk[n++] = done ? dst : srcs[0];
+        if (done == 0) {
+            done = 1;
+        }
+        while (n < 16 && done < nsrc) {
+            chunk[n++] = srcs[done++];
+        }
+        st = ucg_builtin_dev_reduce_tree(cmb->dev, op, dt, dst, chunk, n, count);
+        cmb->stats[2]++;
+        cmb->stats[3] += count * ucg_builtin_dev_dtype_size(dt) * (n - 1);
+    }
+    if (st == UCS_OK) {
+        st = ucg_builtin_dev_sync(cmb->dev);
+    }
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
+ucs_status_t ucg_builtin_combine_dev_copy(ucg_builtin_combine_t *cmb, void *dst,
+                                          const void *src, size_t bytes)
+{
+    ucs_status_t st;
+    void *const d[1]       = {dst};
+    const void *const s[1] = {src};
+    if (cmb == NULL || cmb->dev == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (bytes == 0 || dst == src) {
+        return UCS_OK;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    st = ucg_builtin_dev_copy_multi(cmb->dev, d, s, 1, bytes);
+    if (st == UCS_OK) {
+        st = ucg_builtin_dev_sync(cmb->dev);
+    }
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
 void ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb, uint64_t out[6])
 {
     int i;

@@ -478,6 +478,15 @@ struct ucg_builtin_lgroup {
     unsigned                 radix;
     unsigned                 sock_thresh;
     unsigned                 factor;
+    /* device buffers of the remote-key steps, registered once per group
+     * (the memory registration cache behind ucg_builtin_step_zcopy_prep,
+     * builtin_control.c:276-286): an op's buffers return here when it is
+     * destroyed and peers' mappings stay open until the group goes, so a key
+     * always names the memory it named when it was sent */
+    struct rma_pool         *pool;
+    unsigned                 npool;
+    struct rma_imp          *imp;
+    unsigned                 nimp;
 };
 
 struct ucg_builtin_lcoll {
@@ -522,11 +531,35 @@ struct ucg_builtin_lcoll {
     uint64_t     pipe_cap;        /* entries of frag_left and frag_fifo */
     unsigned     iter_ep;
     size_t       iter_offset;
+    /* device-resident buffers: remote-key steps (the rkey exchange of
+     * ucg_builtin_step_create_rkey_bcast and the zero-copy reads of
+     * SEND_GET_ZCOPY, builtin_control.c:1014-1076, builtin_data.c:326-340) */
+    int          rma;
+    char        *rbuf_user;       /* where the result goes; NULL off a
+                                     reduce's root */
+    void        *dbuf[2];         /* this member's exposed device buffers */
+    int          pool_idx[2];     /* their entries in the group's pool */
+    uint8_t      key[2][UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+    int          keys_sent;       /* the keys go out on the first start only */
+    unsigned     cur_buf;         /* the dbuf holding this member's data */
+    unsigned     readers[2];      /* peers still reading each dbuf */
+    void        *peer_buf[UCG_BUILTIN_OPS_MAX_MEMBERS][2];
+    unsigned     rdy_cnt[OPS_MAX_STEPS];   /* READY messages per step ... */
+    uint8_t      rdy_peer[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
+    uint8_t      rdy_buf[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
+                                  /* ... in arrival order: the fold order */
+    int          rma_sent, rma_recvd, rma_final, rma_busy, rma_again;
+    struct rma_msg *outbox;       /* control messages not sent yet */
+    unsigned     out_head, out_tail, out_cap;
 };
 
 static int  recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
                     size_t length);
 static void step_execute(ucg_builtin_lcoll_t *c);
+static void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *data,
+                    size_t length);
+static void rma_advance(ucg_builtin_lcoll_t *c);
+static void rma_group_free(ucg_builtin_lgroup_t *g);
 
 static stash_t *stash_new(uint64_t header, const void *payload, size_t length)
 {
@@ -967,6 +1000,11 @@ static ucs_status_t am_handler(void *arg, void *data, size_t length)
         return UCS_OK;
     }
     slot = &g->slots[h.coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    if (slot->req && slot->req->rma && h.coll_id == slot->req->coll_id) {
+        g->stats[1]++;
+        rma_msg(slot->req, h, (char*)data + 8, length - 8);
+        return UCS_OK;
+    }
     if (slot->req && h.local_id == slot->expecting) {
         g->stats[1]++;
         (void)recv_cb(slot->req, h.remote_offset, (char*)data + 8, length - 8);
@@ -1086,6 +1124,7 @@ void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
         }
     }
     g->iface->groups[g->group_id % UNEXP_GROUPS] = NULL;
+    rma_group_free(g);
     free(g);
 }
 
@@ -1097,7 +1136,11 @@ unsigned ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *g)
         ucg_builtin_lcoll_t *c = g->slots[i].req;
         if (c && c->send_pending) {
             g->stats[3]++;
-            step_execute(c);
+            if (c->rma) {
+                rma_advance(c);
+            } else {
+                step_execute(c);
+            }
             n++;
         }
     }
@@ -1582,9 +1625,457 @@ static ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn)
     return UCS_OK;
 }
 
+/* ------------------------------------------------------------------------ */
+/* device-resident buffers: remote-key steps                                */
+/* ------------------------------------------------------------------------ */
+/* An op whose buffers are GPU memory runs the same plan, but no data crosses
+ * the AM transport: every member keeps its data in a device buffer of its
+ * own, exposed to the peers that read it through a HIP IPC handle - the
+ * packed remote key of the reference's rkey-exchange step
+ * (ucg_builtin_step_create_rkey_bcast, builtin_control.c:1014-1076), sent
+ * once per op since the buffers outlive every start. A step's send becomes
+ * READY (my buffer b holds what you would receive) and its receive becomes one
+ * kernel reading the senders' buffers over xGMI (SEND_GET_ZCOPY,
+ * builtin_data.c:326-340), after which the reader answers DONE so the sender
+ * may write that buffer again. Two buffers per member alternate, so a member
+ * never waits for readers of the data it is combining into: step k reads
+ * dbuf[cur] and writes dbuf[!cur] unless nobody reads dbuf[cur]. The
+ * association is the host path's: the accumulator first, then the peers in
+ * the order their READYs arrived (builtin_comp_step.inl:213-221). */
+#define RMA_DONE 0x40   /* payload {from, buf}: done reading your dbuf[buf] */
+#define RMA_RKEY 0x80   /* payload {from, buf, handle}: the key of my dbuf[buf] */
+#define RMA_MIN_SHORT (8 + 8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES)
+
+struct rma_msg {
+    unsigned peer;
+    uint64_t header;
+    uint32_t length;
+    uint8_t  payload[8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+};
+
+struct rma_pool {
+    void    *ptr;
+    size_t   bytes;
+    int      busy;
+    uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+};
+
+struct rma_imp {
+    unsigned peer;
+    uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+    void    *ptr;
+};
+
+/* a free registered buffer of exactly `bytes`, or a new one */
+static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes)
+{
+    struct rma_pool *p;
+    unsigned i;
+    for (i = 0; i < g->npool; i++) {
+        if (!g->pool[i].busy && g->pool[i].bytes == bytes) {
+            g->pool[i].busy = 1;
+            return (int)i;
+        }
+    }
+    p = realloc(g->pool, (g->npool + 1) * sizeof(*p));
+    if (p == NULL) {
+        return -1;
+    }
+    g->pool = p;
+    p = &g->pool[g->npool];
+    p->ptr   = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
+    p->bytes = bytes;
+    p->busy  = 1;
+    if (p->ptr == NULL) {
+        return -1;
+    }
+    if (ucg_builtin_combine_dev_export(g->cmb, p->ptr, p->key) != UCS_OK) {
+        ucg_builtin_combine_dev_free(g->cmb, p->ptr);
+        return -1;
+    }
+    return (int)g->npool++;
+}
+
+/* a peer's buffer by its key: mapped once per group */
+static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, const void *key,
+                               void **ptr)
+{
+    struct rma_imp *m;
+    unsigned i;
+    ucs_status_t st;
+    for (i = 0; i < g->nimp; i++) {
+        if (g->imp[i].peer == peer &&
+            memcmp(g->imp[i].key, key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES) == 0) {
+            *ptr = g->imp[i].ptr;
+            return UCS_OK;
+        }
+    }
+    m = realloc(g->imp, (g->nimp + 1) * sizeof(*m));
+    if (m == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    g->imp = m;
+    st = ucg_builtin_combine_dev_import(g->cmb, key, ptr);
+    if (st != UCS_OK) {
+        return st;
+    }
+    m = &g->imp[g->nimp++];
+    m->peer = peer;
+    memcpy(m->key, key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    m->ptr = *ptr;
+    return UCS_OK;
+}
+
+static void rma_group_free(ucg_builtin_lgroup_t *g)
+{
+    unsigned i;
+    for (i = 0; i < g->nimp; i++) {
+        ucg_builtin_combine_dev_release(g->cmb, g->imp[i].ptr);
+    }
+    for (i = 0; i < g->npool; i++) {
+        ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
+    }
+    free(g->imp);
+    free(g->pool);
+}
+
+/* the op's buffers decide: device memory (both, or the one given) -> 1,
+ * host memory -> 0, one of each -> -1 */
+static int rma_kind(ucg_builtin_lgroup_t *g, const void *sbuf, const void *rbuf)
+{
+    int sk, rk;
+    if (!ucg_builtin_combine_has_device(g->cmb)) {
+        return 0;
+    }
+    sk = sbuf ? ucg_builtin_dev_mem_kind(sbuf) : -1;
+    rk = rbuf ? ucg_builtin_dev_mem_kind(rbuf) : -1;
+    if (sk != UCG_DEV_MEM_DEVICE && rk != UCG_DEV_MEM_DEVICE) {
+        return 0;
+    }
+    return (sbuf && sk != UCG_DEV_MEM_DEVICE) || (rbuf && rk != UCG_DEV_MEM_DEVICE) ? -1 : 1;
+}
+
+static void rma_post(ucg_builtin_lcoll_t *c, unsigned peer, uint8_t kind,
+                     unsigned buf, const void *extra, size_t extra_len)
+{
+    struct rma_msg *m;
+    ops_header_t h;
+    uint32_t w[2] = {c->g->my, buf};
+    if (c->out_tail == c->out_cap) {
+        unsigned cap = c->out_cap ? 2 * c->out_cap : 64;
+        struct rma_msg *o = realloc(c->outbox, cap * sizeof(*o));
+        if (o == NULL) {
+            finish(c, UCS_ERR_NO_MEMORY);
+            return;
+        }
+        c->outbox  = o;
+        c->out_cap = cap;
+    }
+    m = &c->outbox[c->out_tail++];
+    h.header   = 0;
+    h.group_id = c->g->group_id;
+    h.coll_id  = c->coll_id;
+    h.step_idx = kind;
+    m->peer    = peer;
+    m->header  = h.header;
+    m->length  = (uint32_t)(8 + extra_len);
+    memcpy(m->payload, w, 8);
+    if (extra_len) {
+        memcpy(m->payload + 8, extra, extra_len);
+    }
+}
+
+/* in order; resumed from lgroup_progress after UCS_ERR_NO_RESOURCE */
+static void rma_flush(ucg_builtin_lcoll_t *c)
+{
+    while (!c->done && c->out_head < c->out_tail) {
+        struct rma_msg *m = &c->outbox[c->out_head];
+        ucs_status_t st = ucg_builtin_shm_am_short(c->g->iface, m->peer, m->header,
+                                                   m->payload, m->length);
+        if (st == UCS_ERR_NO_RESOURCE) {
+            c->send_pending = 1;
+            return;
+        }
+        if (st != UCS_OK) {
+            finish(c, st);
+            return;
+        }
+        c->g->stats[0]++;
+        c->out_head++;
+    }
+    c->out_head = c->out_tail = 0;
+    c->send_pending = 0;
+}
+
+/* the send half of a step: READY to every reader, who now holds one more
+ * reference to the buffer */
+static void rma_expose(ucg_builtin_lcoll_t *c, const op_step_t *s)
+{
+    unsigned e;
+    for (e = 0; e < s->send_cnt; e++) {
+        rma_post(c, s->send_peers[e], s->step_idx, c->cur_buf, NULL, 0);
+    }
+    c->readers[c->cur_buf] += s->send_cnt;
+}
+
+/* the receive half: once every sender's READY is in and the target buffer
+ * has no readers left, one kernel; then DONE to every sender. 0 = wait. */
+static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
+{
+    const unsigned k = c->cur;
+    const void *srcs[UCG_BUILTIN_OPS_MAX_MEMBERS + 1];
+    unsigned out, i;
+    ucs_status_t st;
+
+    if (c->rdy_cnt[k] < s->recv_cnt) {
+        return 0;
+    }
+    out = c->readers[c->cur_buf] ? !c->cur_buf : c->cur_buf;
+    if (c->readers[out]) {
+        return 0;
+    }
+    for (i = 0; i < s->recv_cnt; i++) {
+        srcs[1 + i] = c->peer_buf[c->rdy_peer[k][i]][c->rdy_buf[k][i]];
+        if (srcs[1 + i] == NULL) {
+            finish(c, UCS_ERR_IO_ERROR);      /* a READY without a key */
+            return 0;
+        }
+    }
+    if (s->aggregation == AGG_REDUCE) {
+        srcs[0] = c->dbuf[c->cur_buf];
+        st = ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, c->dbuf[out], srcs,
+                                          1 + s->recv_cnt, (size_t)c->count);
+    } else {
+        st = (s->recv_cnt == 1) ?
+             ucg_builtin_combine_dev_copy(c->g->cmb, c->dbuf[out], srcs[1], c->length) :
+             UCS_ERR_IO_ERROR;
+    }
+    if (st != UCS_OK) {
+        finish(c, st);
+        return 0;
+    }
+    for (i = 0; i < s->recv_cnt; i++) {
+        rma_post(c, c->rdy_peer[k][i], RMA_DONE, c->rdy_buf[k][i], NULL, 0);
+    }
+    c->cur_buf = out;
+    return 1;
+}
+
+/* as far as the messages in allow; the op completes once the result is in
+ * recv.buffer and nobody reads this member's buffers any more */
+static void rma_advance(ucg_builtin_lcoll_t *c)
+{
+    if (c->rma_busy) {
+        c->rma_again = 1;
+        return;
+    }
+    c->rma_busy = 1;
+    do {
+        c->rma_again = 0;
+        rma_flush(c);
+        while (!c->done && c->cur < c->nsteps) {
+            const op_step_t *s = &c->steps[c->cur];
+            if (!s->recv_first && !c->rma_sent) {
+                rma_expose(c, s);
+                c->rma_sent = 1;
+            }
+            if (s->recv_cnt && !c->rma_recvd) {
+                if (!rma_receive(c, s)) {
+                    break;
+                }
+                c->rma_recvd = 1;
+            }
+            if (s->recv_first && !c->rma_sent) {
+                rma_expose(c, s);
+                c->rma_sent = 1;
+            }
+            c->cur++;
+            c->rma_sent = c->rma_recvd = 0;
+        }
+        if (!c->done && c->cur == c->nsteps && !c->rma_final) {
+            ucs_status_t st = c->rbuf_user ?
+                ucg_builtin_combine_dev_copy(c->g->cmb, c->rbuf_user,
+                                             c->dbuf[c->cur_buf], c->length) : UCS_OK;
+            if (st != UCS_OK) {
+                finish(c, st);
+            }
+            c->rma_final = 1;
+        }
+        rma_flush(c);
+        if (!c->done && c->rma_final && c->out_tail == 0 &&
+            c->readers[0] == 0 && c->readers[1] == 0) {
+            finish(c, UCS_OK);
+        }
+    } while (c->rma_again && !c->done);
+    c->rma_busy = 0;
+}
+
+/* a control message of this op (am_handler, or the stash at start) */
+static void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *data,
+                    size_t length)
+{
+    uint32_t w[2];
+    unsigned k;
+    if (c->done) {
+        return;
+    }
+    if (length < 8) {
+        finish(c, UCS_ERR_IO_ERROR);
+        return;
+    }
+    memcpy(w, data, 8);
+    if (w[0] >= c->g->size || w[0] == c->g->my || w[1] > 1) {
+        finish(c, UCS_ERR_IO_ERROR);   /* e.g. a member that took the host path */
+        return;
+    }
+    if (h.step_idx == RMA_RKEY) {
+        void *p = NULL;
+        ucs_status_t st;
+        if (length != 8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES || c->peer_buf[w[0]][w[1]]) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        st = rma_import(c->g, w[0], (const char*)data + 8, &p);
+        if (st != UCS_OK) {
+            finish(c, st);
+            return;
+        }
+        c->peer_buf[w[0]][w[1]] = p;
+        return;                        /* nothing waits on a key alone */
+    }
+    if (h.step_idx == RMA_DONE) {
+        if (c->readers[w[1]] == 0) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        c->readers[w[1]]--;
+    } else {
+        for (k = 0; k < c->nsteps && c->steps[k].step_idx != h.step_idx; k++) {
+        }
+        if (k == c->nsteps || c->rdy_cnt[k] == c->steps[k].recv_cnt) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        c->rdy_peer[k][c->rdy_cnt[k]] = (uint8_t)w[0];
+        c->rdy_buf[k][c->rdy_cnt[k]]  = (uint8_t)w[1];
+        c->rdy_cnt[k]++;
+    }
+    rma_advance(c);
+}
+
+/* at create: the op's own buffers and their keys */
+static ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
+{
+    ucg_dev_op_t o;
+    ucg_dev_dtype_t d;
+    unsigned i;
+    if (ucg_builtin_shm_iface_max_short(c->g->iface) < RMA_MIN_SHORT ||
+        !ucg_builtin_combine_classify(c->g->cmb, c->op, c->dtype, &o, &d)) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    c->rma       = 1;
+    c->rbuf_user = rbuf_user;
+    c->pool_idx[0] = c->pool_idx[1] = -1;
+    for (i = 0; i < 2; i++) {
+        int k = rma_pool_get(c->g, c->length ? c->length : 1);
+        if (k < 0) {
+            return UCS_ERR_NO_MEMORY;
+        }
+        c->pool_idx[i] = k;
+        c->dbuf[i]     = c->g->pool[k].ptr;
+        memcpy(c->key[i], c->g->pool[k].key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    }
+    return UCS_OK;
+}
+
+static ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    ucs_status_t st;
+    unsigned k, e;
+    stash_t **pp;
+
+    c->cur       = 0;
+    c->cur_buf   = 0;
+    c->rma_sent  = c->rma_recvd = c->rma_final = 0;
+    c->readers[0] = c->readers[1] = 0;
+    c->out_head  = c->out_tail = 0;
+    c->send_pending = 0;
+    memset(c->rdy_cnt, 0, sizeof(c->rdy_cnt));
+    if (c->length == 0) {
+        c->done   = 1;
+        c->status = UCS_OK;
+        return UCS_OK;
+    }
+    /* ucg_builtin_init_reduce (builtin_control.c:43-47): this member's data
+     * into its first buffer - every member, since every member exposes it */
+    st = ucg_builtin_combine_dev_copy(g->cmb, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf,
+                                      c->length);
+    if (st != UCS_OK) {
+        c->done   = 1;
+        c->status = st;
+        return st;
+    }
+    c->done   = 0;
+    c->status = UCS_INPROGRESS;
+    c->active = 1;
+    slot->req = c;
+    c->rma_busy = 1;                  /* post and drain before advancing */
+    if (!c->keys_sent) {
+        /* the keys go to every member that reads from this one */
+        uint8_t sent[UCG_BUILTIN_OPS_MAX_MEMBERS] = {0};
+        for (k = 0; k < c->nsteps; k++) {
+            for (e = 0; e < c->steps[k].send_cnt; e++) {
+                unsigned p = c->steps[k].send_peers[e];
+                if (!sent[p]) {
+                    sent[p] = 1;
+                    rma_post(c, p, RMA_RKEY, 0, c->key[0], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+                    rma_post(c, p, RMA_RKEY, 1, c->key[1], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+                }
+            }
+        }
+        c->keys_sent = 1;
+    }
+    /* what arrived before this start (ucg_builtin_step_check_pending) */
+    pp = &slot->msgs;
+    while (*pp && !c->done) {
+        stash_t *m = *pp;
+        ops_header_t h;
+        h.header = m->header;
+        if (h.coll_id != c->coll_id) {
+            pp = &m->next;
+            continue;
+        }
+        *pp = m->next;
+        if (m->next == NULL) {
+            slot->msgs_tail = pp;
+        }
+        rma_msg(c, h, m->data, m->length);
+        free(m);
+    }
+    c->rma_busy = 0;
+    rma_advance(c);
+    return c->done ? c->status : UCS_INPROGRESS;
+}
+
+/* the op's buffers go back to the group's pool; peers' mappings stay */
+static void rma_free(ucg_builtin_lcoll_t *c)
+{
+    unsigned i;
+    for (i = 0; i < 2; i++) {
+        if (c->pool_idx[i] >= 0) {
+            c->g->pool[c->pool_idx[i]].busy = 0;
+        }
+    }
+    free(c->outbox);
+}
+
 static void lcoll_free(ucg_builtin_lcoll_t *c)
 {
     if (c) {
+        if (c->rma) {
+            rma_free(c);
+        }
         free(c->scratch);
         free(c->frag_left);
         free(c->frag_fifo);
@@ -1598,6 +2089,7 @@ static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
 {
     ucg_builtin_lcoll_t *c;
     size_t dt_len;
+    int rma;
 
     if (g == NULL || coll_p == NULL || count < 0 || (count && sbuf == NULL)) {
         return UCS_ERR_INVALID_PARAM;
@@ -1606,7 +2098,11 @@ static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
     if (dt_len == 0) {
         return UCS_ERR_INVALID_PARAM;
     }
-    if ((size_t)count * dt_len * g->size > 0xffffffffull) {
+    rma = count ? rma_kind(g, sbuf, rbuf) : 0;
+    if (rma < 0) {
+        return UCS_ERR_UNSUPPORTED;   /* one buffer on the host, one on the GPU */
+    }
+    if (!rma && (size_t)count * dt_len * g->size > 0xffffffffull) {
         return UCS_ERR_UNSUPPORTED;   /* 32-bit remote_offset, SURVEY 7 (ix) */
     }
     c = calloc(1, sizeof(*c));
@@ -1621,6 +2117,7 @@ static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
     c->op     = op;
     c->dt_len = dt_len;
     c->length = (size_t)count * dt_len;
+    c->rma    = rma;              /* buffers set up once the plan is known */
     c->done   = 1;
     c->status = UCS_OK;
     *coll_p   = c;
@@ -1673,6 +2170,9 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
             st = plan_finish(c, ppn);
         }
     }
+    if (st == UCS_OK && c->rma) {
+        st = rma_setup(c, rbuf);
+    }
     if (st != UCS_OK) {
         lcoll_free(c);
         return st;
@@ -1710,6 +2210,14 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
         lcoll_free(c);
         return st;
     }
+    if (c->rma) {
+        if ((st = rma_setup(c, g->my == root ? rbuf : NULL)) != UCS_OK) {
+            lcoll_free(c);
+            return st;
+        }
+        *coll_p = c;
+        return UCS_OK;
+    }
     /* a member other than the root that combines on the way (a host master,
      * a waypoint) accumulates in a buffer of the op's own: MPI leaves recvbuf
      * undefined off the root */
@@ -1746,6 +2254,9 @@ ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *c)
         return UCS_ERR_BUSY;    /* more than 16 ops outstanding */
     }
     g->next_coll_id++;          /* ucg_collective_trigger, base/ucg_group.c:485 */
+    if (c->rma) {
+        return rma_start(c, slot);
+    }
     /* ucg_builtin_init_reduce: recv <- send (in place: nothing to copy);
      * tree leaves have no init (builtin_control.c:755-767) */
     if (c->init_reduce && c->rbuf != c->sbuf && c->length) {
@@ -1832,6 +2343,10 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
         PUT(", root %u", c->root);
     }
     PUT("\nPhases: %u\n", c->nsteps);
+    if (c->rma) {
+        PUT("Buffers: device memory; remote keys once per op, every step reads its "
+            "senders' buffers in one kernel\n");
+    }
     for (k = 0; k < c->nsteps; k++) {
         const op_step_t *s = &c->steps[k];
         unsigned e;

@@ -60,6 +60,14 @@ HOST_API = {
     "ucg_builtin_combine_dtype_length": (_sz, [_vp, _vp]),
     "ucg_builtin_combine_atomic_sum_length": (_sz, [_vp, _vp, _vp]),
     "ucg_builtin_combine_check_reduction": (_int, [_vp, _vp]),
+    "ucg_builtin_combine_dev_alloc": (_vp, [_vp, _sz]),
+    "ucg_builtin_combine_dev_free": (None, [_vp, _vp]),
+    "ucg_builtin_combine_dev_export": (_int, [_vp, _vp, _vp]),
+    "ucg_builtin_combine_dev_import": (_int, [_vp, _vp, ctypes.POINTER(_vp)]),
+    "ucg_builtin_combine_dev_release": (None, [_vp, _vp]),
+    "ucg_builtin_combine_dev_fold": (_int, [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp), _u,
+                                            _sz]),
+    "ucg_builtin_combine_dev_copy": (_int, [_vp, _vp, _vp, _sz]),
     # include/ucg_builtin_ops.h
     "ucg_builtin_shm_iface_open": (_int, [ctypes.c_char_p, _u, _u, _sz, _u,
                                           ctypes.POINTER(_vp)]),
