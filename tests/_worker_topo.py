@@ -109,7 +109,8 @@ def main():
         rc = 1
 
     kinds = [("allreduce", 0)] + [("reduce", r) for r in sorted({0, n - 1, n // 2})]
-    for ci, (dt, op, count) in enumerate(CASES):
+    # TOPO_REPEAT=k runs the case list k times (a stress knob for races)
+    for ci, (dt, op, count) in enumerate(CASES * int(os.environ.get("TOPO_REPEAT", "1"))):
         dist_kind = "exact" if dt.startswith("float") else "round"
         inputs = [O.fill(dt, dist_kind, 5000 + 31 * ci + m, count) for m in range(n)]
         for kind, root in kinds:
@@ -149,7 +150,10 @@ def main():
                 if st != 0:
                     fail(f"{kind} {dt} {op} root={root} start {rep} status={st}")
                 elif got is not None and not (O.bits(got) == O.bits(want[rank])).all():
-                    fail(f"{kind} {dt} {op} n={count} root={root} start {rep}")
+                    bad = np.nonzero(O.bits(got) != O.bits(want[rank]))[0]
+                    fail(f"{kind} {dt} {op} n={count} root={root} start {rep}: "
+                         f"{bad.size} elements differ, first {bad[:6].tolist()}: got "
+                         f"{got[bad[:3]].tolist()} want {want[rank][bad[:3]].tolist()}")
             if not (O.bits(back(sbuf, inputs[rank])) == O.bits(inputs[rank])).all():
                 fail(f"{kind} {dt} {op}: send buffer modified")
             coll.close()

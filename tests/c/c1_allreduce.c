@@ -6,6 +6,9 @@
  *   RANK=r WORLD_SIZE=n c1_allreduce <shm-name> [iters] [max_short] [count]
  *
  * C1_DEVICE_STAGING=1 forces every combine onto the GPU (staged steps).
+ * C1_DEVICE_BUFFERS=1 gives the engine device buffers (GPU rank % count): the
+ * plan runs as remote-key steps, every receive one kernel reading the
+ * senders' buffers over IPC.
  * C1_PPN=p [C1_SOCKET=s] places the members on hosts of p consecutive
  * members (sockets of s) through ucg_builtin_lgroup_create_ex; the planner
  * knobs come from the environment (UCX_BUILTIN_TREE_RADIX, ...).
@@ -73,6 +76,9 @@ int main(int argc, char **argv)
     uint8_t dist[UCG_BUILTIN_OPS_MAX_MEMBERS];
     ucg_builtin_lgroup_params_t gp = {NULL, 0, 0, 0};
     double t0, us;
+    const int devbufs = getenv("C1_DEVICE_BUFFERS") != NULL;
+    ucg_builtin_dev_ctx_t *dev = NULL;
+    void *dsend = NULL, *drecv = NULL;
 
     if (getenv("C1_DEVICE_STAGING")) {
         /* every step staged on the GPU: the configuration read the way UCX
@@ -80,6 +86,11 @@ int main(int argc, char **argv)
         ucg_builtin_combine_config_read(&cfg);
         cfg.dev_enable    = 2;
         cfg.dev_min_bytes = 0;
+    }
+    if (devbufs) {
+        int n = ucg_builtin_dev_device_count();
+        cfg.dev_enable = 1;
+        cfg.device     = n > 0 ? (int)(rank % (unsigned)n) : 0;
     }
     {
         const char *pp = getenv("C1_PPN"), *ps = getenv("C1_SOCKET");
@@ -114,7 +125,18 @@ int main(int argc, char **argv)
         ucg_oracle_tree_reduce(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
                                world, 0, NULL, count);
     }
-    if (ucg_builtin_lcoll_allreduce(g, inputs[rank], out, count, (void*)1,
+    if (devbufs) {
+        dev = ucg_builtin_combine_dev_ctx(cmb);
+        dsend = dev ? ucg_builtin_dev_malloc(dev, count * sizeof(float)) : NULL;
+        drecv = dev ? ucg_builtin_dev_malloc(dev, count * sizeof(float)) : NULL;
+        if (dsend == NULL || drecv == NULL ||
+            ucg_builtin_dev_memcpy(dev, dsend, inputs[rank], count * sizeof(float)) != UCS_OK) {
+            fprintf(stderr, "rank %u: no device buffers\n", rank);
+            return 1;
+        }
+    }
+    if (ucg_builtin_lcoll_allreduce(g, devbufs ? dsend : (void*)inputs[rank],
+                                    devbufs ? drecv : (void*)out, count, (void*)1,
                                     (void*)1, &c) != UCS_OK) {
         fprintf(stderr, "rank %u: allreduce create failed\n", rank);
         return 1;
@@ -137,25 +159,34 @@ int main(int argc, char **argv)
         }
     }
     us = (now_s() - t0) / iters * 1e6;
+    if (devbufs && ucg_builtin_dev_memcpy(dev, out, drecv, count * sizeof(float)) != UCS_OK) {
+        fprintf(stderr, "rank %u: download failed\n", rank);
+        return 1;
+    }
     ok = memcmp(out, want, count * sizeof(float)) == 0;
     ucg_builtin_shm_barrier(iface);
     if (rank == 0) {
         uint64_t st[4], cs[6];
         ucg_builtin_lgroup_stats(g, st);
         ucg_builtin_combine_stats(cmb, cs);
-        printf("{\"config\": \"C1: %u-rank loopback allreduce, %d fp32 SUM\", "
+        printf("{\"config\": \"C1: %u-rank loopback allreduce, %d fp32 SUM%s\", "
                "\"ranks\": %u, \"bytes\": %zu, \"max_short\": %zu, "
                "\"latency_us\": %.3f, \"iters\": %d, \"bit_exact\": %s, "
                "\"messages_sent\": %llu, \"stashed\": %llu, "
                "\"host_combines\": %llu, \"device_combines\": %llu, "
                "\"device_staged_steps\": %llu}\n",
-               world, count, world, count * sizeof(float), max_short, us, iters,
+               world, count, devbufs ? ", device buffers" : "", world,
+               count * sizeof(float), max_short, us, iters,
                ok ? "true" : "false", (unsigned long long)st[0],
                (unsigned long long)st[2], (unsigned long long)cs[0],
                (unsigned long long)cs[2], (unsigned long long)cs[4]);
     }
     ucg_builtin_lcoll_destroy(c);
     ucg_builtin_lgroup_destroy(g);
+    if (devbufs) {
+        ucg_builtin_dev_free(dev, dsend);
+        ucg_builtin_dev_free(dev, drecv);
+    }
     ucg_builtin_shm_iface_close(iface);
     ucg_builtin_combine_destroy(cmb);
     for (r = 0; r < world; r++) {

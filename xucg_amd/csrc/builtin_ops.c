@@ -1824,16 +1824,22 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
 {
     const unsigned k = c->cur;
     const void *srcs[UCG_BUILTIN_OPS_MAX_MEMBERS + 1];
+    /* the last receive with nothing exposed after it writes the result
+     * straight into recv.buffer (no final copy) */
+    const int direct = c->rbuf_user && k + 1 == c->nsteps &&
+                       !(s->recv_first && s->send_cnt);
     unsigned out, i;
+    void *dst;
     ucs_status_t st;
 
     if (c->rdy_cnt[k] < s->recv_cnt) {
         return 0;
     }
     out = c->readers[c->cur_buf] ? !c->cur_buf : c->cur_buf;
-    if (c->readers[out]) {
+    if (!direct && c->readers[out]) {
         return 0;
     }
+    dst = direct ? (void*)c->rbuf_user : c->dbuf[out];
     for (i = 0; i < s->recv_cnt; i++) {
         srcs[1 + i] = c->peer_buf[c->rdy_peer[k][i]][c->rdy_buf[k][i]];
         if (srcs[1 + i] == NULL) {
@@ -1843,11 +1849,11 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
     }
     if (s->aggregation == AGG_REDUCE) {
         srcs[0] = c->dbuf[c->cur_buf];
-        st = ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, c->dbuf[out], srcs,
+        st = ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst, srcs,
                                           1 + s->recv_cnt, (size_t)c->count);
     } else {
         st = (s->recv_cnt == 1) ?
-             ucg_builtin_combine_dev_copy(c->g->cmb, c->dbuf[out], srcs[1], c->length) :
+             ucg_builtin_combine_dev_copy(c->g->cmb, dst, srcs[1], c->length) :
              UCS_ERR_IO_ERROR;
     }
     if (st != UCS_OK) {
@@ -1857,7 +1863,11 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
     for (i = 0; i < s->recv_cnt; i++) {
         rma_post(c, c->rdy_peer[k][i], RMA_DONE, c->rdy_buf[k][i], NULL, 0);
     }
-    c->cur_buf = out;
+    if (direct) {
+        c->rma_final = 1;
+    } else {
+        c->cur_buf = out;
+    }
     return 1;
 }
 
