@@ -157,7 +157,17 @@ unsigned     ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *group);
  *    host's master (two levels from sock_thresh members per host), the
  *    inter-host tree of `tree_radix` over the masters, and the fan-out back.
  * UCX_BUILTIN_ALLREDUCE_PLAN=tree|recursive overrides the choice (a knob of
- * this build). sbuf == rbuf means in place. The op is reusable (persistent). */
+ * this build). sbuf == rbuf means in place. The op is reusable (persistent).
+ *
+ * Device buffers (GPU memory, with a device attached to the combine): the same
+ * plan runs as remote-key steps - the reference's rkey exchange and zero-copy
+ * reads (builtin_control.c:1014-1076, builtin_data.c:326-340). Each member
+ * keeps its data in two registered device buffers of the group's pool, sends
+ * their IPC keys once per op to the members that read from it, and a step
+ * becomes READY (to the readers) and one kernel over the senders' buffers
+ * followed by DONE (to the senders). Every member must pass device buffers
+ * (one host and one device buffer is UCS_ERR_UNSUPPORTED), and the transport
+ * must carry 112-byte messages. The (op, dtype) must classify for the device. */
 ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *group,
                                          const void *sbuf, void *rbuf,
                                          int count, void *dtype, void *op,

@@ -1985,7 +1985,6 @@ static ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
     }
     c->rma       = 1;
     c->rbuf_user = rbuf_user;
-    c->pool_idx[0] = c->pool_idx[1] = -1;
     for (i = 0; i < 2; i++) {
         int k = rma_pool_get(c->g, c->length ? c->length : 1);
         if (k < 0) {
@@ -2128,6 +2127,7 @@ static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
     c->dt_len = dt_len;
     c->length = (size_t)count * dt_len;
     c->rma    = rma;              /* buffers set up once the plan is known */
+    c->pool_idx[0] = c->pool_idx[1] = -1;
     c->done   = 1;
     c->status = UCS_OK;
     *coll_p   = c;
