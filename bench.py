@@ -477,6 +477,14 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             G.push_allreduce(ctx, init.data_ptr(), tpeers, apeers, n5, "float64", "sum",
                              rank, world, sbar)
 
+        # (d) the builtin plan itself: the operation engine (libucg_builtin.so)
+        # on device buffers - remote-key steps over IPC, every member's plan
+        # from builtin_recursive.c, the combine as ucg_builtin_dev_fold
+        eng = builtin_engine(rank, world, local_rank, init.data_ptr(), acc.data_ptr(), n5)
+
+        def once_engine():
+            eng.run()
+
         # parity: every member's input regenerated locally, one-shot tree
         allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
         for r in range(world):
@@ -490,7 +498,9 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 ("doubling", once, n5 * 8 * G.recursive_steps(world)),
                 ("halving", once_halving, 2 * (world - 1) * n5 * 8 // world),
                 ("oneshot_xgmi", once_oneshot, 2 * (world - 1) * n5 * 8 // world),
-                ("oneshot_xgmi_push", once_push, 2 * (world - 1) * n5 * 8 // world)):
+                ("oneshot_xgmi_push", once_push, 2 * (world - 1) * n5 * 8 // world),
+                ("builtin_engine_device_buffers", once_engine,
+                 n5 * 8 * G.recursive_steps(world))):
             acc.zero_()
             fn()
             torch.cuda.synchronize()
@@ -506,6 +516,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                          "bit_exact_vs_oneshot_tree": same}
         torch.cuda.synchronize()
         dist.barrier()
+        res["builtin_engine_device_buffers"]["plan"] = eng.describe().splitlines()[0]
+        eng.close()
         ipeers.close()
         apeers.close()
         tpeers.close()
@@ -531,6 +543,53 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     agreed(recursive_doubling, "c5_recursive_allreduce_512mib_fp64")
     out["wall_s"] = round(time.perf_counter() - t_start, 1)
     return out
+
+
+class builtin_engine:
+    """An fp64 SUM allreduce through the builtin operation engine on device
+    buffers (include/ucg_builtin_ops.h): the shared-memory AM transport
+    between the node's ranks for keys, READY and DONE, the data read over
+    xGMI by the combine kernels. The "MPI library" behind reduce_cb_f knows
+    one op (SUM) and one type (double): handles are the device enums + 1."""
+
+    def __init__(self, rank, world, local_rank, sbuf, rbuf, count):
+        import ctypes
+        import numpy as np
+        from xucg_amd import host, ops, OPS, DTYPES
+        sum_h, f64_h = OPS.index("sum") + 1, DTYPES.index("float64") + 1
+
+        def reduce_cb(op, src, dst, n, dtype):     # host buffers only
+            s = np.ctypeslib.as_array((ctypes.c_double * n).from_address(src))
+            d = np.ctypeslib.as_array((ctypes.c_double * n).from_address(dst))
+            d[:] = s + d
+            return 0
+        cbs = {"reduce_cb_f": reduce_cb, "is_sum_f": lambda op: op == sum_h,
+               "is_loc_expected_f": lambda op: False, "is_commutative_f": lambda op: True,
+               "convert": lambda dt: 8 << 3, "is_integer_f": lambda dt: (False, False),
+               "is_floating_point_f": lambda dt: True}
+        self.cmb = host.BuiltinCombine(cbs, host.make_config(device=local_rank),
+                                       op_classifier=lambda op: op - 1,
+                                       dt_classifier=lambda dt: dt - 1)
+        self.iface = ops.ShmIface(f"/xucg_bench_{os.environ.get('MASTER_PORT', '0')}",
+                                  world, rank, max_short=256)
+        self.group = ops.Group(self.iface, 7, world, rank, self.cmb)
+        self.coll = self.group.allreduce(sbuf, rbuf, count, f64_h, sum_h)
+        if self.coll.status != 0:
+            raise RuntimeError(f"builtin allreduce create failed: {self.coll.status}")
+
+    def run(self):
+        st = self.coll.run()
+        if st != 0:
+            raise RuntimeError(f"builtin allreduce failed: {st}")
+
+    def describe(self):
+        return self.coll.describe()
+
+    def close(self):
+        self.coll.close()
+        self.group.close()
+        self.iface.close()
+        self.cmb.close()
 
 
 def same_box_reference(n, iters=50):
@@ -621,6 +680,8 @@ def collective_child():
     rank = int(os.environ["RANK"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
+    # the engine's waits give up after this long instead of outliving the child
+    os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "60")
     dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
                             device_id=torch.device(f"cuda:{local_rank}"))
     ctx = xucg_amd.DevContext.on_torch_stream(local_rank)
