@@ -196,6 +196,11 @@ void         ucg_builtin_dev_ctx_destroy(ucg_builtin_dev_ctx_t *ctx);
 void        *ucg_builtin_dev_ctx_stream(ucg_builtin_dev_ctx_t *ctx);
 /* Wait for all work queued on the context's stream(s). */
 ucs_status_t ucg_builtin_dev_sync(ucg_builtin_dev_ctx_t *ctx);
+/* Wait for the work queued on the context's launch stream the way the
+ * context ends a staged step (params.completion): with the completion word a
+ * one-workgroup kernel behind the work writes, spun on for 200 us before the
+ * runtime's blocking wait; with COMPLETION_SYNC, hipStreamSynchronize. */
+ucs_status_t ucg_builtin_dev_complete(ucg_builtin_dev_ctx_t *ctx);
 
 /* ---- device-resident combine ---------------------------------------------*/
 /* dst[i] = src[i] (op) dst[i] for i < count; dst/src are device pointers.

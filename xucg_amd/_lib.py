@@ -69,6 +69,7 @@ DEV_API = {
     "ucg_builtin_dev_ctx_destroy": (None, [_vp]),
     "ucg_builtin_dev_ctx_stream": (_vp, [_vp]),
     "ucg_builtin_dev_sync": (_st, [_vp]),
+    "ucg_builtin_dev_complete": (_st, [_vp]),
     "ucg_builtin_dev_reduce": (_st, [_vp, _int, _int, _vp, _vp, _sz]),
     "ucg_builtin_dev_reduce_multi": (_st, [_vp, _int, _int, _vp,
                                            ctypes.POINTER(_vp), _u, _u, _sz]),

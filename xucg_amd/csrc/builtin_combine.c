@@ -573,7 +573,7 @@ ucs_status_t ucg_builtin_combine_dev_fold(ucg_builtin_combine_t *cmb, void *redu
         cmb->stats[3] += count * ucg_builtin_dev_dtype_size(dt) * (n - 1);
     }
     if (st == UCS_OK) {
-        st = ucg_builtin_dev_sync(cmb->dev);
+        st = ucg_builtin_dev_complete(cmb->dev);   /* before READY / DONE go out */
     }
     pthread_mutex_unlock(&cmb->lock);
     return st;
@@ -594,7 +594,7 @@ ucs_status_t ucg_builtin_combine_dev_copy(ucg_builtin_combine_t *cmb, void *dst,
     pthread_mutex_lock(&cmb->lock);
     st = ucg_builtin_dev_copy_multi(cmb->dev, d, s, 1, bytes);
     if (st == UCS_OK) {
-        st = ucg_builtin_dev_sync(cmb->dev);
+        st = ucg_builtin_dev_complete(cmb->dev);   /* before READY / DONE go out */
     }
     pthread_mutex_unlock(&cmb->lock);
     return st;

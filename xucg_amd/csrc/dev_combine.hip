@@ -538,6 +538,15 @@ ucs_status_t ucg_builtin_dev_sync(ucg_builtin_dev_ctx_t *ctx)
     return UCS_OK;
 }
 
+ucs_status_t ucg_builtin_dev_complete(ucg_builtin_dev_ctx_t *ctx)
+{
+    if (ctx == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "complete", "ctx is NULL");
+    }
+    ctx->queued = true;          /* whatever was launched since the last wait */
+    return stream_complete(ctx, true);
+}
+
 static ucs_status_t check_args(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
                                ucg_dev_dtype_t dt, const char *what)
 {
