@@ -95,10 +95,14 @@ class Group:
 
 
 def _addr(x):
+    """an address, a numpy array, a torch tensor (device buffers run as
+    remote-key steps) or a DevBuffer / HostBuffer"""
     if isinstance(x, int):
         return x
     if hasattr(x, "ctypes"):
         return x.ctypes.data
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
     return x.ptr
 
 
