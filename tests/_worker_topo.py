@@ -4,13 +4,15 @@ against the oracle's restatement (oracle/plans.py), then allreduce and
 reduce to several roots run and are checked against the oracle's simulation
 of every member's plan.
 
-    _worker_topo.py <shm-name> <mode: host|dev|rma> <max_short> <n:ppn:socket:radix:factor:thresh>
+    _worker_topo.py <shm-name> <mode: host|dev|rma|shm> <max_short> <n:ppn:socket:radix:factor:thresh>
 
 socket = 0 means no socket level. Mode dev stages every REDUCE step of host
 buffers on the GPU; mode rma gives the engine device buffers (GPU memory on
 device rank % device count), which it runs as remote-key steps: keys once per
 op, READY / DONE over the transport, every receive one kernel reading the
-senders' buffers. The transport is the shared-memory one
+senders' buffers. Mode shm runs host buffers through the same steps with
+POSIX shared memory segments as the exposed buffers
+(UCX_BUILTIN_SHM_ZCOPY_THRESH=1). The transport is the shared-memory one
 for every member: a NET distance changes the plan, not the wire.
 
 Checks:
@@ -73,6 +75,9 @@ def main():
         ndev = max(1, _lib.dev().ucg_builtin_dev_device_count())
         dctx = xucg_amd.DevContext(device=rank % ndev)
         cfg = host.make_config(device=rank % ndev)
+    elif mode == "shm":
+        os.environ["UCX_BUILTIN_SHM_ZCOPY_THRESH"] = "1"
+        cfg = host.make_config(dev_enable=0)
     elif mode == "dev":
         cfg = host.make_config(dev_enable=2, dev_min_bytes=0, stage_bytes=1 << 16)
     else:
@@ -141,10 +146,11 @@ def main():
                     fail(f"{kind} root={root} plan\n engine {got}\n oracle {exp}\n{text}")
                 if kind == "allreduce" or root == n - 1:
                     print(f"describe {kind} root={root}:\n{text}", flush=True)
-                if (mode == "rma") != ("Buffers: device memory" in text):
-                    fail(f"{kind} root={root}: device buffers not described\n{text}")
+                if (mode == "rma") != ("Buffers: device memory" in text) or \
+                        (mode == "shm") != ("Buffers: shared memory" in text):
+                    fail(f"{kind} root={root}: buffers not described\n{text}")
             # persistent: a second start reuses the keys of the first
-            for rep in range(2 if mode == "rma" and ci < 2 else 1):
+            for rep in range(2 if mode in ("rma", "shm") and ci < 2 else 1):
                 st = coll.run()
                 got = back(rbuf, inputs[rank]) if rbuf is not None else None
                 if st != 0:

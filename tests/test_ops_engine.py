@@ -48,14 +48,16 @@ def test_c1_harness_bit_exact(max_short, world):
     (4, 256, "", "", "", ""), (3, 256, "", "", "", ""), (8, 100, "", "", "", ""),
     (4, 256, "tree", "1", "", ""), (5, 64, "tree", "", "", ""),
     (8, 256, "", "", "4", ""), (12, 100, "", "", "3", ""), (8, 256, "tree", "1", "8:4", ""),
-    (12, 100, "", "", "3", "y")])
+    (12, 100, "", "", "3", "y"), (8, 256, "", "", "", "zcopy"),
+    (12, 256, "", "", "3", "zcopy"), (6, 256, "tree", "", "", "zcopy")])
 def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast, place,
                                     pipe):
     """The host engine (libucg_builtin.so sources) and the C1 harness rebuilt
     with ASan + UBSan (tests/c/Makefile, target asan): recursive and tree
     plans, fragmenting and resend-heavy sizes, the incast fan-in, waypoints
-    forwarding fragment by fragment. Any sanitizer report (invalid access, UB,
-    leak at exit) fails the rank."""
+    forwarding fragment by fragment, the shared-memory remote-key steps
+    (pipe = "zcopy"). Any sanitizer report (invalid access, UB, leak at exit)
+    fails the rank."""
     import json
     import subprocess
     cdir = os.path.join(os.path.dirname(__file__), "c")
@@ -67,7 +69,9 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
         monkeypatch.setenv("UCX_BUILTIN_ALLREDUCE_PLAN", plan)
     if incast:
         monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", incast)
-    if pipe:
+    if pipe == "zcopy":
+        monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", "1")
+    elif pipe:
         monkeypatch.setenv("UCX_BUILTIN_PIPELINE", pipe)
     if place:
         # placements (test_topology.py): hosts of C1_PPN, sockets of

@@ -174,6 +174,23 @@ def test_layout_distances_match_oracle():
             assert ops.layout_distances(n, m, ppn, socket) == P.layout(n, m, ppn, socket)
 
 
+@pytest.mark.parametrize("spec", LAYOUTS)
+def test_engine_placements_shm_zcopy(spec, monkeypatch):
+    """The remote-key steps of the device path with host buffers in POSIX
+    shared memory (UCX_BUILTIN_SHM_ZCOPY_THRESH): the same protocol - keys
+    once per op, READY / DONE, reads of the senders' buffers in place, two
+    buffers per member, the last receive into recv.buffer - on every
+    placement, bit-exact against the oracle's simulation, twice per op."""
+    n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "shm", 256, spec),
+                         timeout=240)
+    assert codes == [0] * n, "\n".join(outs)
+    if factor == 2:
+        d = _digests(outs)
+        assert all(x == d[0] for x in d), d
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec", ["4:4:0:8:2:16", "8:8:0:8:2:16", "6:6:0:8:2:16",
                                   "12:3:0:2:2:16", "8:8:4:8:2:4", "8:2:0:8:4:16",

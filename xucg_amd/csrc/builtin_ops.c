@@ -1653,26 +1653,106 @@ struct rma_msg {
     uint8_t  payload[8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
 };
 
+#define RMA_DEV 1       /* device buffers: HIP IPC keys, kernels */
+#define RMA_SHM 2       /* host buffers: POSIX shared memory keys, reduce_cb_f */
+
 struct rma_pool {
     void    *ptr;
     size_t   bytes;
+    int      kind;
     int      busy;
     uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
 };
 
 struct rma_imp {
     unsigned peer;
+    int      kind;
     uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
     void    *ptr;
 };
 
+/* Host buffers behind the same steps: the op's buffers are POSIX shared
+ * memory segments and a key names one (the reference's remote-key step
+ * serves "both shared memory and network", builtin_control.c:712-719). A
+ * zero-copy step for large host messages, as the reference switches to
+ * zcopy above its 100000-byte threshold (builtin_control.c:474). */
+typedef struct {
+    uint32_t magic;
+    uint32_t pad;
+    uint64_t bytes;
+    char     name[64];
+} shm_key_t;
+
+_Static_assert(sizeof(shm_key_t) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES, "shm key size");
+#define SHM_KEY_MAGIC 0x4d485358u
+
+static void *shm_seg_alloc(size_t bytes, void *key)
+{
+    static _Atomic unsigned seq;
+    shm_key_t k;
+    void *p;
+    int fd;
+    memset(&k, 0, sizeof(k));
+    k.magic = SHM_KEY_MAGIC;
+    k.bytes = bytes;
+    snprintf(k.name, sizeof(k.name), "/xucg_rma_%d_%u", (int)getpid(),
+             atomic_fetch_add(&seq, 1));
+    fd = shm_open(k.name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) {
+        return NULL;
+    }
+    if (ftruncate(fd, (off_t)bytes) != 0) {
+        close(fd);
+        shm_unlink(k.name);
+        return NULL;
+    }
+    p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        shm_unlink(k.name);
+        return NULL;
+    }
+    memset(key, 0, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    memcpy(key, &k, sizeof(k));
+    return p;
+}
+
+static ucs_status_t shm_seg_import(const void *key, void **ptr)
+{
+    shm_key_t k;
+    void *p;
+    int fd;
+    memcpy(&k, key, sizeof(k));
+    if (k.magic != SHM_KEY_MAGIC || memchr(k.name, 0, sizeof(k.name)) == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    fd = shm_open(k.name, O_RDWR, 0);
+    if (fd < 0) {
+        return UCS_ERR_IO_ERROR;
+    }
+    p = mmap(NULL, k.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    *ptr = p;
+    return UCS_OK;
+}
+
+static size_t shm_key_bytes(const void *key)
+{
+    shm_key_t k;
+    memcpy(&k, key, sizeof(k));
+    return (size_t)k.bytes;
+}
+
 /* a free registered buffer of exactly `bytes`, or a new one */
-static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes)
+static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
 {
     struct rma_pool *p;
     unsigned i;
     for (i = 0; i < g->npool; i++) {
-        if (!g->pool[i].busy && g->pool[i].bytes == bytes) {
+        if (!g->pool[i].busy && g->pool[i].bytes == bytes && g->pool[i].kind == kind) {
             g->pool[i].busy = 1;
             return (int)i;
         }
@@ -1683,9 +1763,14 @@ static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes)
     }
     g->pool = p;
     p = &g->pool[g->npool];
-    p->ptr   = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
     p->bytes = bytes;
+    p->kind  = kind;
     p->busy  = 1;
+    if (kind == RMA_SHM) {
+        p->ptr = shm_seg_alloc(bytes, p->key);
+        return p->ptr ? (int)g->npool++ : -1;
+    }
+    p->ptr = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
     if (p->ptr == NULL) {
         return -1;
     }
@@ -1697,14 +1782,14 @@ static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes)
 }
 
 /* a peer's buffer by its key: mapped once per group */
-static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, const void *key,
-                               void **ptr)
+static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
+                               const void *key, void **ptr)
 {
     struct rma_imp *m;
     unsigned i;
     ucs_status_t st;
     for (i = 0; i < g->nimp; i++) {
-        if (g->imp[i].peer == peer &&
+        if (g->imp[i].peer == peer && g->imp[i].kind == kind &&
             memcmp(g->imp[i].key, key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES) == 0) {
             *ptr = g->imp[i].ptr;
             return UCS_OK;
@@ -1715,12 +1800,14 @@ static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, const voi
         return UCS_ERR_NO_MEMORY;
     }
     g->imp = m;
-    st = ucg_builtin_combine_dev_import(g->cmb, key, ptr);
+    st = (kind == RMA_SHM) ? shm_seg_import(key, ptr) :
+                             ucg_builtin_combine_dev_import(g->cmb, key, ptr);
     if (st != UCS_OK) {
         return st;
     }
     m = &g->imp[g->nimp++];
     m->peer = peer;
+    m->kind = kind;
     memcpy(m->key, key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
     m->ptr = *ptr;
     return UCS_OK;
@@ -1730,29 +1817,83 @@ static void rma_group_free(ucg_builtin_lgroup_t *g)
 {
     unsigned i;
     for (i = 0; i < g->nimp; i++) {
-        ucg_builtin_combine_dev_release(g->cmb, g->imp[i].ptr);
+        if (g->imp[i].kind == RMA_SHM) {
+            munmap(g->imp[i].ptr, shm_key_bytes(g->imp[i].key));
+        } else {
+            ucg_builtin_combine_dev_release(g->cmb, g->imp[i].ptr);
+        }
     }
     for (i = 0; i < g->npool; i++) {
-        ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
+        if (g->pool[i].kind == RMA_SHM) {
+            shm_key_t k;
+            memcpy(&k, g->pool[i].key, sizeof(k));
+            munmap(g->pool[i].ptr, g->pool[i].bytes);
+            shm_unlink(k.name);
+        } else {
+            ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
+        }
     }
     free(g->imp);
     free(g->pool);
 }
 
-/* the op's buffers decide: device memory (both, or the one given) -> 1,
- * host memory -> 0, one of each -> -1 */
-static int rma_kind(ucg_builtin_lgroup_t *g, const void *sbuf, const void *rbuf)
+/* UCX_BUILTIN_SHM_ZCOPY_THRESH: host messages of at least this many bytes
+ * take the shared-memory remote-key steps (0 or unset = never; this build's
+ * knob - the reference hard-codes 100000, builtin_control.c:474) */
+static size_t shm_zcopy_thresh(void)
+{
+    const char *e = getenv("UCX_BUILTIN_SHM_ZCOPY_THRESH");
+    return (e && *e) ? (size_t)strtoull(e, NULL, 0) : 0;
+}
+
+/* the op's buffers decide: device memory (both, or the one given) ->
+ * RMA_DEV, large host messages with the knob -> RMA_SHM, other host
+ * memory -> 0, one of each -> -1 */
+static int rma_kind(ucg_builtin_lgroup_t *g, const void *sbuf, const void *rbuf,
+                    size_t length)
 {
     int sk, rk;
-    if (!ucg_builtin_combine_has_device(g->cmb)) {
-        return 0;
+    const size_t thresh = shm_zcopy_thresh();
+    if (ucg_builtin_combine_has_device(g->cmb)) {
+        sk = sbuf ? ucg_builtin_dev_mem_kind(sbuf) : -1;
+        rk = rbuf ? ucg_builtin_dev_mem_kind(rbuf) : -1;
+        if (sk == UCG_DEV_MEM_DEVICE || rk == UCG_DEV_MEM_DEVICE) {
+            return (sbuf && sk != UCG_DEV_MEM_DEVICE) ||
+                   (rbuf && rk != UCG_DEV_MEM_DEVICE) ? -1 : RMA_DEV;
+        }
     }
-    sk = sbuf ? ucg_builtin_dev_mem_kind(sbuf) : -1;
-    rk = rbuf ? ucg_builtin_dev_mem_kind(rbuf) : -1;
-    if (sk != UCG_DEV_MEM_DEVICE && rk != UCG_DEV_MEM_DEVICE) {
-        return 0;
+    return (thresh && length >= thresh) ? RMA_SHM : 0;
+}
+
+/* the receive's combine: dst = srcs[n-1] (op) (... (srcs[1] (op) srcs[0])) */
+static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *const *srcs,
+                             unsigned n)
+{
+    unsigned m;
+    ucs_status_t st = UCS_OK;
+    if (c->rma == RMA_DEV) {
+        return ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst, srcs, n,
+                                            (size_t)c->count);
     }
-    return (sbuf && sk != UCG_DEV_MEM_DEVICE) || (rbuf && rk != UCG_DEV_MEM_DEVICE) ? -1 : 1;
+    if (dst != srcs[0]) {
+        memcpy(dst, srcs[0], c->length);
+    }
+    for (m = 1; m < n && st == UCS_OK; m++) {
+        st = ucg_builtin_combine_reduce(c->g->cmb, c->op, (void*)srcs[m], dst, c->count,
+                                        c->dtype);
+    }
+    return st;
+}
+
+static ucs_status_t rma_copy(ucg_builtin_lcoll_t *c, void *dst, const void *src)
+{
+    if (c->rma == RMA_DEV) {
+        return ucg_builtin_combine_dev_copy(c->g->cmb, dst, src, c->length);
+    }
+    if (dst != src) {
+        memcpy(dst, src, c->length);
+    }
+    return UCS_OK;
 }
 
 static void rma_post(ucg_builtin_lcoll_t *c, unsigned peer, uint8_t kind,
@@ -1849,12 +1990,9 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
     }
     if (s->aggregation == AGG_REDUCE) {
         srcs[0] = c->dbuf[c->cur_buf];
-        st = ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst, srcs,
-                                          1 + s->recv_cnt, (size_t)c->count);
+        st = rma_fold(c, dst, srcs, 1 + s->recv_cnt);
     } else {
-        st = (s->recv_cnt == 1) ?
-             ucg_builtin_combine_dev_copy(c->g->cmb, dst, srcs[1], c->length) :
-             UCS_ERR_IO_ERROR;
+        st = (s->recv_cnt == 1) ? rma_copy(c, dst, srcs[1]) : UCS_ERR_IO_ERROR;
     }
     if (st != UCS_OK) {
         finish(c, st);
@@ -1904,8 +2042,7 @@ static void rma_advance(ucg_builtin_lcoll_t *c)
         }
         if (!c->done && c->cur == c->nsteps && !c->rma_final) {
             ucs_status_t st = c->rbuf_user ?
-                ucg_builtin_combine_dev_copy(c->g->cmb, c->rbuf_user,
-                                             c->dbuf[c->cur_buf], c->length) : UCS_OK;
+                rma_copy(c, c->rbuf_user, c->dbuf[c->cur_buf]) : UCS_OK;
             if (st != UCS_OK) {
                 finish(c, st);
             }
@@ -1945,7 +2082,7 @@ static void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *data,
             finish(c, UCS_ERR_IO_ERROR);
             return;
         }
-        st = rma_import(c->g, w[0], (const char*)data + 8, &p);
+        st = rma_import(c->g, w[0], c->rma, (const char*)data + 8, &p);
         if (st != UCS_OK) {
             finish(c, st);
             return;
@@ -1980,13 +2117,13 @@ static ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
     ucg_dev_dtype_t d;
     unsigned i;
     if (ucg_builtin_shm_iface_max_short(c->g->iface) < RMA_MIN_SHORT ||
-        !ucg_builtin_combine_classify(c->g->cmb, c->op, c->dtype, &o, &d)) {
+        (c->rma == RMA_DEV &&
+         !ucg_builtin_combine_classify(c->g->cmb, c->op, c->dtype, &o, &d))) {
         return UCS_ERR_UNSUPPORTED;
     }
-    c->rma       = 1;
     c->rbuf_user = rbuf_user;
     for (i = 0; i < 2; i++) {
-        int k = rma_pool_get(c->g, c->length ? c->length : 1);
+        int k = rma_pool_get(c->g, c->length ? c->length : 1, c->rma);
         if (k < 0) {
             return UCS_ERR_NO_MEMORY;
         }
@@ -1999,7 +2136,6 @@ static ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
 
 static ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
 {
-    ucg_builtin_lgroup_t *g = c->g;
     ucs_status_t st;
     unsigned k, e;
     stash_t **pp;
@@ -2018,8 +2154,7 @@ static ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     }
     /* ucg_builtin_init_reduce (builtin_control.c:43-47): this member's data
      * into its first buffer - every member, since every member exposes it */
-    st = ucg_builtin_combine_dev_copy(g->cmb, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf,
-                                      c->length);
+    st = rma_copy(c, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf);
     if (st != UCS_OK) {
         c->done   = 1;
         c->status = st;
@@ -2107,7 +2242,7 @@ static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
     if (dt_len == 0) {
         return UCS_ERR_INVALID_PARAM;
     }
-    rma = count ? rma_kind(g, sbuf, rbuf) : 0;
+    rma = count ? rma_kind(g, sbuf, rbuf, (size_t)count * dt_len) : 0;
     if (rma < 0) {
         return UCS_ERR_UNSUPPORTED;   /* one buffer on the host, one on the GPU */
     }
@@ -2354,8 +2489,11 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
     }
     PUT("\nPhases: %u\n", c->nsteps);
     if (c->rma) {
-        PUT("Buffers: device memory; remote keys once per op, every step reads its "
-            "senders' buffers in one kernel\n");
+        PUT(c->rma == RMA_DEV ?
+            "Buffers: device memory; remote keys once per op, every step reads its "
+            "senders' buffers in one kernel\n" :
+            "Buffers: shared memory; remote keys once per op, every step reads its "
+            "senders' buffers in place\n");
     }
     for (k = 0; k < c->nsteps; k++) {
         const op_step_t *s = &c->steps[k];
