@@ -477,13 +477,6 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             G.push_allreduce(ctx, init.data_ptr(), tpeers, apeers, n5, "float64", "sum",
                              rank, world, sbar)
 
-        # (d) the builtin plan itself: the operation engine (libucg_builtin.so)
-        # on device buffers - remote-key steps over IPC, every member's plan
-        # from builtin_recursive.c, the combine as ucg_builtin_dev_fold
-        eng = builtin_engine(rank, world, local_rank, init.data_ptr(), acc.data_ptr(), n5)
-
-        def once_engine():
-            eng.run()
 
         # parity: every member's input regenerated locally, one-shot tree
         allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
@@ -498,9 +491,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 ("doubling", once, n5 * 8 * G.recursive_steps(world)),
                 ("halving", once_halving, 2 * (world - 1) * n5 * 8 // world),
                 ("oneshot_xgmi", once_oneshot, 2 * (world - 1) * n5 * 8 // world),
-                ("oneshot_xgmi_push", once_push, 2 * (world - 1) * n5 * 8 // world),
-                ("builtin_engine_device_buffers", once_engine,
-                 n5 * 8 * G.recursive_steps(world))):
+                ("oneshot_xgmi_push", once_push, 2 * (world - 1) * n5 * 8 // world)):
             acc.zero_()
             fn()
             torch.cuda.synchronize()
@@ -516,8 +507,6 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                          "bit_exact_vs_oneshot_tree": same}
         torch.cuda.synchronize()
         dist.barrier()
-        res["builtin_engine_device_buffers"]["plan"] = eng.describe().splitlines()[0]
-        eng.close()
         ipeers.close()
         apeers.close()
         tpeers.close()
@@ -541,6 +530,41 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         del ref
         return res
     agreed(recursive_doubling, "c5_recursive_allreduce_512mib_fp64")
+
+    def engine_c5():
+        """(e) C5 through the builtin plan itself: the operation engine
+        (libucg_builtin.so) on device buffers - remote-key steps, the partner's
+        buffer read over xGMI by the fold kernel. Its own phase, so a failure
+        here costs this entry only."""
+        if world & (world - 1):
+            return {"skipped": "the recursive plan needs a power-of-two group"}
+        n5 = 1 << 26
+        init = torch.empty(n5, dtype=torch.float64, device=dev)
+        ctx.fill("float64", "round", 0x5EED5000 + rank, init, n5)
+        acc = torch.zeros_like(init)
+        allx = [torch.empty(n5, dtype=torch.float64, device=dev) for _ in range(world)]
+        for r in range(world):
+            ctx.fill("float64", "round", 0x5EED5000 + r, allx[r], n5)
+        ref = torch.empty_like(init)
+        chk = ctx.reduce_multi("sum", "float64", ref, allx, rank, n5)
+        ctx.sync()
+        del allx
+        eng = builtin_engine(rank, world, local_rank, init.data_ptr(), acc.data_ptr(), n5)
+        try:
+            eng.run()
+            same = chk == 0 and bool(torch.equal(acc.view(torch.int64), ref.view(torch.int64)))
+            for _ in range(warmup):
+                eng.run()
+            t = timed(eng.run, steps)
+            link = n5 * 8 * G.recursive_steps(world)
+            return {"plan": eng.describe().splitlines()[0], "ms": round(t * 1e3, 3),
+                    "algbw_gbs": round(n5 * 8 / t / 1e9, 1), "sent_bytes_per_rank": link,
+                    "link_gbs": round(link / t / 1e9, 1), "bit_exact_vs_oneshot_tree": same}
+        finally:
+            torch.cuda.synchronize()
+            dist.barrier()
+            eng.close()
+    agreed(engine_c5, "c5_builtin_engine_device_buffers_512mib_fp64")
     out["wall_s"] = round(time.perf_counter() - t_start, 1)
     return out
 
@@ -681,7 +705,7 @@ def collective_child():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local_rank)
     # the engine's waits give up after this long instead of outliving the child
-    os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "30")
     dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
                             device_id=torch.device(f"cuda:{local_rank}"))
     ctx = xucg_amd.DevContext.on_torch_stream(local_rank)
