@@ -2,7 +2,7 @@
 simulation that runs every member's plan to produce the expected results.
 
 TEST INFRASTRUCTURE ONLY (like the rest of oracle/): imported by tests/ as
-the checker of the operation engine's plans (xucg_amd/csrc/builtin_ops.c),
+the checker of the operation engine's plans (xucg_amd/csrc/builtin_plan.c),
 never by the product package.
 
 Restated from (paths relative to the reference tree):

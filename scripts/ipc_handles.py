@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Are HIP IPC handles of live allocations distinct, and what do they hold?
 The engine's per-group mapping cache keys peers' buffers by handle bytes
-(builtin_ops.c rma_import). Allocates 40 registered-size buffers (freeing
+(builtin_rma.c rma_import). Allocates 40 registered-size buffers (freeing
 every third one as it goes, as ops come and go), exports each live one,
 and reports duplicate handles among live allocations and the handle bytes
 that vary.   python scripts/ipc_handles.py [out.json]"""

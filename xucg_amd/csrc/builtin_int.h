@@ -1,0 +1,311 @@
+/*
+ * builtin_int.h - state shared by the translation units of libucg_builtin.so's
+ * operation engine (not an installed header):
+ *   builtin_shm.c   f2, the shared-memory AM transport
+ *   builtin_ops.c   f1, the operation engine (slots, stash, steps) and its API
+ *   builtin_plan.c  the planner (tree, recursive K-ing, placements)
+ *   builtin_rma.c   remote-key steps (device and shared-memory buffers)
+ * Internal functions are hidden: the library exports only include/'s API.
+ */
+#ifndef XUCG_BUILTIN_INT_H
+#define XUCG_BUILTIN_INT_H
+
+#include "ucg_builtin_ops.h"
+
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <time.h>
+
+#define UCG_INTERNAL __attribute__((visibility("hidden")))
+
+/* ======================================================================== */
+/* f2: shared-memory AM transport state                                     */
+/* ======================================================================== */
+typedef struct {
+    _Alignas(64) _Atomic uint64_t head;   /* producer index */
+    _Alignas(64) _Atomic uint64_t tail;   /* consumer index */
+} ring_ctl_t;
+
+typedef struct {
+    uint32_t length;    /* payload bytes (without the header) */
+    uint32_t reserved;
+    uint64_t header;    /* followed by the payload: data = &header */
+} cell_t;
+
+#define SEG_CTL_BYTES 128
+#define UNEXP_GROUPS  64
+
+/* Incast cell (the SM-root "bcopy into a shared buffer" of the UCX
+ * collectives extension the reference's reducing packers are written for,
+ * builtin_pack.c:50-72, 100-148): every child of a root packs the same
+ * (header) message into one cell of the root's incast area - the first copies
+ * (or, for a concurrent packer, zeroes), the others reduce into it - and the
+ * root receives the cell as one message once all `expected` children packed. */
+typedef struct {
+    _Atomic uint32_t lock;
+    _Atomic uint32_t state;     /* INCAST_FREE / _FILLING / _READY */
+    _Atomic uint32_t count;     /* children packed so far */
+    uint32_t         expected;
+    uint32_t         length;    /* payload bytes */
+    uint32_t         reserved;
+    uint64_t         header;    /* followed by the payload: data = &header */
+} incast_cell_t;
+
+enum { INCAST_FREE, INCAST_FILLING, INCAST_READY };
+
+typedef struct {
+    _Alignas(64) _Atomic uint64_t ready;   /* cells in INCAST_READY */
+} incast_ctl_t;
+
+typedef struct stash {
+    struct stash *next;
+    uint64_t      header;
+    size_t        length;  /* payload bytes */
+    uint8_t       data[];
+} stash_t;
+
+struct ucg_builtin_shm_iface {
+    char      name[256];
+    unsigned  members;
+    unsigned  my;
+    size_t    max_short;
+    size_t    cell_size;
+    unsigned  cells;
+    size_t    ring_bytes;
+    size_t    incast_cell_size;
+    size_t    incast_bytes;    /* one member's incast area */
+    size_t    incast_base;     /* offset of member 0's incast area */
+    size_t    seg_bytes;
+    char     *seg;
+    uint64_t  barrier_gen;
+    /* ops layer: groups by id and messages for groups not created yet
+     * (the reference's bctx->group_by_id / bctx->unexpected, builtin.c:
+     * 150-205) */
+    ucg_builtin_lgroup_t *groups[UNEXP_GROUPS];
+    stash_t  *unexpected;
+};
+
+static inline double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static inline double wait_timeout_s(void)
+{
+    const char *t = getenv("UCX_BUILTIN_WAIT_TIMEOUT");
+    return t ? atof(t) : 300.0;
+}
+
+/* ======================================================================== */
+/* f1: engine state                                                         */
+/* ======================================================================== */
+/* builtin/ops/builtin_ops.h:45-60 */
+typedef union {
+    struct {
+        uint16_t group_id;
+        union {
+            struct {
+                uint8_t coll_id;
+                uint8_t step_idx;
+            };
+            uint16_t local_id;
+        };
+        uint32_t remote_offset;
+    };
+    uint64_t header;
+} ops_header_t;
+
+_Static_assert(sizeof(ops_header_t) == 8, "wire header is 8 bytes");
+
+#define OPS_MAX_STEPS 12
+
+/* the plan methods this engine runs (builtin/plan/builtin_plan.h:28-44), and
+ * the aggregation each receive applies (builtin_control.c:960-972) */
+typedef enum {
+    M_REDUCE_RECURSIVE,   /* send to the step's peers, receive and reduce */
+    M_REDUCE_TERMINAL,    /* tree root: receive from every child and reduce */
+    M_SEND_TO_SM_ROOT,    /* tree leaf, fan-in (ppn > 2) */
+    M_SEND_TERMINAL,      /* tree leaf fan-in at ppn == 2, root fan-out */
+    M_RECV_TERMINAL,      /* tree leaf, fan-out: receive the result */
+    M_REDUCE_WAYPOINT,    /* receive from the children and reduce, then send
+                             the accumulator to the parent */
+    M_BCAST_WAYPOINT      /* receive from the parent, then send to the
+                             children */
+} op_method_t;
+
+typedef enum { AGG_NOP, AGG_REDUCE, AGG_WRITE } op_aggregation_t;
+
+/* bcopy packers of an SM-root child (builtin_pack.c): plain copy, reducing
+ * (:50-72) or unsigned-SUM atomic (:100-148) */
+typedef enum { PACK_COPY, PACK_REDUCING, PACK_ATOMIC } op_packer_t;
+
+
+typedef struct {
+    uint8_t     method;           /* op_method_t */
+    uint8_t     aggregation;      /* op_aggregation_t */
+    uint8_t     step_idx;         /* phase->step_index, 1-based */
+    unsigned    send_cnt;         /* endpoints sent to, in this order */
+    unsigned    send_peers[UCG_BUILTIN_OPS_MAX_MEMBERS];
+    unsigned    recv_cnt;         /* endpoints received from */
+    unsigned    recv_peers[UCG_BUILTIN_OPS_MAX_MEMBERS];  /* describe only */
+    int         send_recv_buffer; /* 0: send.buffer, 1: recv.buffer */
+    int         recv_first;       /* *_WAYPOINT: every receive of the step
+                                     before its sends (RECV_BEFORE_SEND1 /
+                                     RECV1_BEFORE_SEND, builtin_control.c:
+                                     379-389) */
+    int         pipelined;        /* a fragmented waypoint: each fragment goes
+                                     on once all its contributions are in
+                                     (PIPELINED / BY_FRAGMENT_OFFSET,
+                                     builtin_control.c:831-834, 978-980) */
+    int         incast;           /* sends / receives go through the incast */
+    uint8_t     packer;           /* op_packer_t of an incast send */
+    unsigned    incast_expected;  /* children packing each incast message */
+    size_t      frag_len;         /* 0: single message */
+    uint64_t    frags;            /* messages per endpoint */
+    uint64_t    fragments_total;  /* recv_cnt x frags */
+} op_step_t;
+
+typedef struct {
+    ucg_builtin_lcoll_t *req;     /* the op running in this slot */
+    uint16_t             expecting;
+    stash_t             *msgs;    /* slot->messages */
+    stash_t            **msgs_tail; /* &last->next (or &msgs): O(1) append */
+} op_slot_t;
+
+struct ucg_builtin_lgroup {
+    ucg_builtin_shm_iface_t *iface;
+    uint16_t                 group_id;
+    unsigned                 size;
+    unsigned                 my;
+    ucg_builtin_combine_t   *cmb;
+    op_slot_t                slots[UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    uint8_t                  next_coll_id;
+    int                      incast;   /* UCX_BUILTIN_SM_INCAST */
+    uint64_t                 stats[4];
+    /* placement and planner knobs (ucg_builtin_lgroup_params_t) */
+    uint8_t                  distance[UCG_BUILTIN_OPS_MAX_MEMBERS];
+    unsigned                 radix;
+    unsigned                 sock_thresh;
+    unsigned                 factor;
+    /* device buffers of the remote-key steps, registered once per group
+     * (the memory registration cache behind ucg_builtin_step_zcopy_prep,
+     * builtin_control.c:276-286): an op's buffers return here when it is
+     * destroyed and peers' mappings stay open until the group goes, so a key
+     * always names the memory it named when it was sent */
+    struct rma_pool         *pool;
+    unsigned                 npool;
+    struct rma_imp          *imp;
+    unsigned                 nimp;
+};
+
+struct ucg_builtin_lcoll {
+    ucg_builtin_lgroup_t *g;
+    const char  *sbuf;
+    char        *rbuf;
+    int          count;
+    void        *dtype;
+    void        *op;
+    size_t       dt_len;
+    size_t       length;
+    const char  *plan;            /* "recursive doubling" / "tree" / ... */
+    int          kind;            /* 0 allreduce, 1 reduce */
+    char        *scratch;         /* accumulator of a non-root member that
+                                     combines in a reduce (rbuf then points
+                                     here) */
+    unsigned     root;
+    int          init_reduce;     /* ucg_builtin_init_reduce on start */
+    op_step_t    steps[OPS_MAX_STEPS];
+    unsigned     nsteps;
+    /* request state (builtin_ops.h:233-241) */
+    int          active;
+    int          done;
+    ucs_status_t status;
+    uint8_t      coll_id;
+    unsigned     cur;
+    uint64_t     pending;
+    int          step_started;
+    int          step_open;       /* a combine step is open */
+    int          send_pending;
+    int          recv_done;       /* a recv_first step has all its data */
+    /* the pipelined waypoint step in progress (builtin_data.c:425-520,
+     * builtin_comp_step.inl:155-174) */
+    int          pipelining;      /* this step forwards fragment by fragment */
+    unsigned    *frag_left;       /* contributions still due per fragment
+                                   * (not a byte: a waypoint may have more
+                                   * than 255 children) */
+    uint64_t    *frag_fifo;       /* complete fragments not yet sent out */
+    uint64_t     fifo_head, fifo_tail;
+    unsigned     fifo_ep;         /* next endpoint of the head fragment */
+    uint64_t     frags_sent;
+    uint64_t     pipe_cap;        /* entries of frag_left and frag_fifo */
+    unsigned     iter_ep;
+    size_t       iter_offset;
+    /* device-resident buffers: remote-key steps (the rkey exchange of
+     * ucg_builtin_step_create_rkey_bcast and the zero-copy reads of
+     * SEND_GET_ZCOPY, builtin_control.c:1014-1076, builtin_data.c:326-340) */
+    int          rma;
+    char        *rbuf_user;       /* where the result goes; NULL off a
+                                     reduce's root */
+    void        *dbuf[2];         /* this member's exposed device buffers */
+    int          pool_idx[2];     /* their entries in the group's pool */
+    uint8_t      key[2][UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+    int          keys_sent;       /* the keys go out on the first start only */
+    unsigned     cur_buf;         /* the dbuf holding this member's data */
+    unsigned     readers[2];      /* peers still reading each dbuf */
+    void        *peer_buf[UCG_BUILTIN_OPS_MAX_MEMBERS][2];
+    unsigned     rdy_cnt[OPS_MAX_STEPS];   /* READY messages per step ... */
+    uint8_t      rdy_peer[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
+    uint8_t      rdy_buf[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
+                                  /* ... in arrival order: the fold order */
+    int          rma_sent, rma_recvd, rma_final, rma_busy, rma_again;
+    struct rma_msg *outbox;       /* control messages not sent yet */
+    unsigned     out_head, out_tail, out_cap;
+};
+
+/* planner state (builtin_plan.c) */
+#define TREE_MAX_RADIX 128   /* UCG_BUILTIN_TREE_MAX_RADIX, builtin_plan.h:98 */
+#define PM               UCG_BUILTIN_OPS_MAX_MEMBERS
+
+typedef struct {
+    unsigned n, my;              /* group size, my virtual index */
+    uint8_t  d[PM];               /* my distances, virtual order */
+    unsigned v2r[PM];
+    unsigned radix, sock_thresh, factor;
+} plan_ctx_t;
+
+enum {
+    D_SELF = UCG_BUILTIN_DISTANCE_SELF, D_SOCKET = UCG_BUILTIN_DISTANCE_SOCKET,
+    D_HOST = UCG_BUILTIN_DISTANCE_HOST, D_NET = UCG_BUILTIN_DISTANCE_NET,
+    D_LAST = 255                 /* UCG_GROUP_MEMBER_DISTANCE_LAST */
+};
+
+#define RMA_DEV 1       /* device buffers: HIP IPC keys, kernels */
+#define RMA_SHM 2       /* host buffers: POSIX shared memory keys, reduce_cb_f */
+
+/* builtin_ops.c */
+UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status);
+
+/* builtin_plan.c */
+UCG_INTERNAL ucs_status_t plan_ctx_init(ucg_builtin_lgroup_t *g, unsigned root,
+                                        plan_ctx_t *pc);
+UCG_INTERNAL ucs_status_t plan_tree(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc,
+                                    int fanout, unsigned *ppn);
+UCG_INTERNAL ucs_status_t plan_recursive(ucg_builtin_lcoll_t *c, const plan_ctx_t *pc,
+                                         unsigned *ppn_out);
+UCG_INTERNAL ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn);
+
+/* builtin_rma.c */
+UCG_INTERNAL int          rma_kind(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                   const void *rbuf, size_t length);
+UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user);
+UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot);
+UCG_INTERNAL void         rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h,
+                                  const void *data, size_t length);
+UCG_INTERNAL void         rma_advance(ucg_builtin_lcoll_t *c);
+UCG_INTERNAL void         rma_free(ucg_builtin_lcoll_t *c);
+UCG_INTERNAL void         rma_group_free(ucg_builtin_lgroup_t *g);
+
+#endif

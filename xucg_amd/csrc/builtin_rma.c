@@ -1,0 +1,603 @@
+/*
+ * builtin_rma.c - remote-key steps of the builtin engine: an op on device
+ * buffers (HIP IPC keys, the combine kernels reading peers over xGMI) or on
+ * large host messages (POSIX shared-memory keys, reduce_cb_f) runs its plan as
+ * READY / DONE control messages around reads of the senders' buffers.
+ */
+#define _GNU_SOURCE
+#include "builtin_int.h"
+
+#include <fcntl.h>
+#include <sched.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------------ */
+/* device-resident buffers: remote-key steps                                */
+/* ------------------------------------------------------------------------ */
+/* An op whose buffers are GPU memory runs the same plan, but no data crosses
+ * the AM transport: every member keeps its data in a device buffer of its
+ * own, exposed to the peers that read it through a HIP IPC handle - the
+ * packed remote key of the reference's rkey-exchange step
+ * (ucg_builtin_step_create_rkey_bcast, builtin_control.c:1014-1076), sent
+ * once per op since the buffers outlive every start. A step's send becomes
+ * READY (my buffer b holds what you would receive) and its receive becomes one
+ * kernel reading the senders' buffers over xGMI (SEND_GET_ZCOPY,
+ * builtin_data.c:326-340), after which the reader answers DONE so the sender
+ * may write that buffer again. Two buffers per member alternate, so a member
+ * never waits for readers of the data it is combining into: step k reads
+ * dbuf[cur] and writes dbuf[!cur] unless nobody reads dbuf[cur]. The
+ * association is the host path's: the accumulator first, then the peers in
+ * the order their READYs arrived (builtin_comp_step.inl:213-221). */
+#define RMA_DONE 0x40   /* payload {from, buf}: done reading your dbuf[buf] */
+#define RMA_RKEY 0x80   /* payload {from, buf, handle}: the key of my dbuf[buf] */
+#define RMA_MIN_SHORT (8 + 8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES)
+
+struct rma_msg {
+    unsigned peer;
+    uint64_t header;
+    uint32_t length;
+    uint8_t  payload[8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+};
+
+
+struct rma_pool {
+    void    *ptr;
+    size_t   bytes;
+    int      kind;
+    int      busy;
+    uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+};
+
+struct rma_imp {
+    unsigned peer;
+    int      kind;
+    uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+    void    *ptr;
+};
+
+/* Host buffers behind the same steps: the op's buffers are POSIX shared
+ * memory segments and a key names one (the reference's remote-key step
+ * serves "both shared memory and network", builtin_control.c:712-719). A
+ * zero-copy step for large host messages, as the reference switches to
+ * zcopy above its 100000-byte threshold (builtin_control.c:474). */
+typedef struct {
+    uint32_t magic;
+    uint32_t pad;
+    uint64_t bytes;
+    char     name[64];
+} shm_key_t;
+
+_Static_assert(sizeof(shm_key_t) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES, "shm key size");
+#define SHM_KEY_MAGIC 0x4d485358u
+
+static void *shm_seg_alloc(size_t bytes, void *key)
+{
+    static _Atomic unsigned seq;
+    shm_key_t k;
+    void *p;
+    int fd;
+    memset(&k, 0, sizeof(k));
+    k.magic = SHM_KEY_MAGIC;
+    k.bytes = bytes;
+    snprintf(k.name, sizeof(k.name), "/xucg_rma_%d_%u", (int)getpid(),
+             atomic_fetch_add(&seq, 1));
+    fd = shm_open(k.name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    if (fd < 0) {
+        return NULL;
+    }
+    if (ftruncate(fd, (off_t)bytes) != 0) {
+        close(fd);
+        shm_unlink(k.name);
+        return NULL;
+    }
+    p = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        shm_unlink(k.name);
+        return NULL;
+    }
+    memset(key, 0, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    memcpy(key, &k, sizeof(k));
+    return p;
+}
+
+static ucs_status_t shm_seg_import(const void *key, void **ptr)
+{
+    shm_key_t k;
+    void *p;
+    int fd;
+    memcpy(&k, key, sizeof(k));
+    if (k.magic != SHM_KEY_MAGIC || memchr(k.name, 0, sizeof(k.name)) == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    fd = shm_open(k.name, O_RDWR, 0);
+    if (fd < 0) {
+        return UCS_ERR_IO_ERROR;
+    }
+    p = mmap(NULL, k.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    *ptr = p;
+    return UCS_OK;
+}
+
+static size_t shm_key_bytes(const void *key)
+{
+    shm_key_t k;
+    memcpy(&k, key, sizeof(k));
+    return (size_t)k.bytes;
+}
+
+/* a free registered buffer of exactly `bytes`, or a new one */
+static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
+{
+    struct rma_pool *p;
+    unsigned i;
+    for (i = 0; i < g->npool; i++) {
+        if (!g->pool[i].busy && g->pool[i].bytes == bytes && g->pool[i].kind == kind) {
+            g->pool[i].busy = 1;
+            return (int)i;
+        }
+    }
+    p = realloc(g->pool, (g->npool + 1) * sizeof(*p));
+    if (p == NULL) {
+        return -1;
+    }
+    g->pool = p;
+    p = &g->pool[g->npool];
+    p->bytes = bytes;
+    p->kind  = kind;
+    p->busy  = 1;
+    if (kind == RMA_SHM) {
+        p->ptr = shm_seg_alloc(bytes, p->key);
+        return p->ptr ? (int)g->npool++ : -1;
+    }
+    p->ptr = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
+    if (p->ptr == NULL) {
+        return -1;
+    }
+    if (ucg_builtin_combine_dev_export(g->cmb, p->ptr, p->key) != UCS_OK) {
+        ucg_builtin_combine_dev_free(g->cmb, p->ptr);
+        return -1;
+    }
+    return (int)g->npool++;
+}
+
+/* a peer's buffer by its key: mapped once per group */
+static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
+                               const void *key, void **ptr)
+{
+    struct rma_imp *m;
+    unsigned i;
+    ucs_status_t st;
+    for (i = 0; i < g->nimp; i++) {
+        if (g->imp[i].peer == peer && g->imp[i].kind == kind &&
+            memcmp(g->imp[i].key, key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES) == 0) {
+            *ptr = g->imp[i].ptr;
+            return UCS_OK;
+        }
+    }
+    m = realloc(g->imp, (g->nimp + 1) * sizeof(*m));
+    if (m == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    g->imp = m;
+    st = (kind == RMA_SHM) ? shm_seg_import(key, ptr) :
+                             ucg_builtin_combine_dev_import(g->cmb, key, ptr);
+    if (st != UCS_OK) {
+        return st;
+    }
+    m = &g->imp[g->nimp++];
+    m->peer = peer;
+    m->kind = kind;
+    memcpy(m->key, key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    m->ptr = *ptr;
+    return UCS_OK;
+}
+
+UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
+{
+    unsigned i;
+    for (i = 0; i < g->nimp; i++) {
+        if (g->imp[i].kind == RMA_SHM) {
+            munmap(g->imp[i].ptr, shm_key_bytes(g->imp[i].key));
+        } else {
+            ucg_builtin_combine_dev_release(g->cmb, g->imp[i].ptr);
+        }
+    }
+    for (i = 0; i < g->npool; i++) {
+        if (g->pool[i].kind == RMA_SHM) {
+            shm_key_t k;
+            memcpy(&k, g->pool[i].key, sizeof(k));
+            munmap(g->pool[i].ptr, g->pool[i].bytes);
+            shm_unlink(k.name);
+        } else {
+            ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
+        }
+    }
+    free(g->imp);
+    free(g->pool);
+}
+
+/* UCX_BUILTIN_SHM_ZCOPY_THRESH: host messages of at least this many bytes
+ * take the shared-memory remote-key steps (0 or unset = never; this build's
+ * knob - the reference hard-codes 100000, builtin_control.c:474) */
+static size_t shm_zcopy_thresh(void)
+{
+    const char *e = getenv("UCX_BUILTIN_SHM_ZCOPY_THRESH");
+    return (e && *e) ? (size_t)strtoull(e, NULL, 0) : 0;
+}
+
+/* the op's buffers decide: device memory (both, or the one given) ->
+ * RMA_DEV, large host messages with the knob -> RMA_SHM, other host
+ * memory -> 0, one of each -> -1 */
+UCG_INTERNAL int rma_kind(ucg_builtin_lgroup_t *g, const void *sbuf, const void *rbuf,
+                    size_t length)
+{
+    int sk, rk;
+    const size_t thresh = shm_zcopy_thresh();
+    if (ucg_builtin_combine_has_device(g->cmb)) {
+        sk = sbuf ? ucg_builtin_dev_mem_kind(sbuf) : -1;
+        rk = rbuf ? ucg_builtin_dev_mem_kind(rbuf) : -1;
+        if (sk == UCG_DEV_MEM_DEVICE || rk == UCG_DEV_MEM_DEVICE) {
+            return (sbuf && sk != UCG_DEV_MEM_DEVICE) ||
+                   (rbuf && rk != UCG_DEV_MEM_DEVICE) ? -1 : RMA_DEV;
+        }
+    }
+    return (thresh && length >= thresh) ? RMA_SHM : 0;
+}
+
+/* the receive's combine: dst = srcs[n-1] (op) (... (srcs[1] (op) srcs[0])) */
+static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *const *srcs,
+                             unsigned n)
+{
+    unsigned m;
+    ucs_status_t st = UCS_OK;
+    if (c->rma == RMA_DEV) {
+        return ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst, srcs, n,
+                                            (size_t)c->count);
+    }
+    if (dst != srcs[0]) {
+        memcpy(dst, srcs[0], c->length);
+    }
+    for (m = 1; m < n && st == UCS_OK; m++) {
+        st = ucg_builtin_combine_reduce(c->g->cmb, c->op, (void*)srcs[m], dst, c->count,
+                                        c->dtype);
+    }
+    return st;
+}
+
+static ucs_status_t rma_copy(ucg_builtin_lcoll_t *c, void *dst, const void *src)
+{
+    if (c->rma == RMA_DEV) {
+        return ucg_builtin_combine_dev_copy(c->g->cmb, dst, src, c->length);
+    }
+    if (dst != src) {
+        memcpy(dst, src, c->length);
+    }
+    return UCS_OK;
+}
+
+static void rma_post(ucg_builtin_lcoll_t *c, unsigned peer, uint8_t kind,
+                     unsigned buf, const void *extra, size_t extra_len)
+{
+    struct rma_msg *m;
+    ops_header_t h;
+    uint32_t w[2] = {c->g->my, buf};
+    if (c->out_tail == c->out_cap) {
+        unsigned cap = c->out_cap ? 2 * c->out_cap : 64;
+        struct rma_msg *o = realloc(c->outbox, cap * sizeof(*o));
+        if (o == NULL) {
+            finish(c, UCS_ERR_NO_MEMORY);
+            return;
+        }
+        c->outbox  = o;
+        c->out_cap = cap;
+    }
+    m = &c->outbox[c->out_tail++];
+    h.header   = 0;
+    h.group_id = c->g->group_id;
+    h.coll_id  = c->coll_id;
+    h.step_idx = kind;
+    m->peer    = peer;
+    m->header  = h.header;
+    m->length  = (uint32_t)(8 + extra_len);
+    memcpy(m->payload, w, 8);
+    if (extra_len) {
+        memcpy(m->payload + 8, extra, extra_len);
+    }
+}
+
+/* in order; resumed from lgroup_progress after UCS_ERR_NO_RESOURCE */
+static void rma_flush(ucg_builtin_lcoll_t *c)
+{
+    while (!c->done && c->out_head < c->out_tail) {
+        struct rma_msg *m = &c->outbox[c->out_head];
+        ucs_status_t st = ucg_builtin_shm_am_short(c->g->iface, m->peer, m->header,
+                                                   m->payload, m->length);
+        if (st == UCS_ERR_NO_RESOURCE) {
+            c->send_pending = 1;
+            return;
+        }
+        if (st != UCS_OK) {
+            finish(c, st);
+            return;
+        }
+        c->g->stats[0]++;
+        c->out_head++;
+    }
+    c->out_head = c->out_tail = 0;
+    c->send_pending = 0;
+}
+
+/* the send half of a step: READY to every reader, who now holds one more
+ * reference to the buffer */
+static void rma_expose(ucg_builtin_lcoll_t *c, const op_step_t *s)
+{
+    unsigned e;
+    for (e = 0; e < s->send_cnt; e++) {
+        rma_post(c, s->send_peers[e], s->step_idx, c->cur_buf, NULL, 0);
+    }
+    c->readers[c->cur_buf] += s->send_cnt;
+}
+
+/* the receive half: once every sender's READY is in and the target buffer
+ * has no readers left, one kernel; then DONE to every sender. 0 = wait. */
+static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
+{
+    const unsigned k = c->cur;
+    const void *srcs[UCG_BUILTIN_OPS_MAX_MEMBERS + 1];
+    /* the last receive with nothing exposed after it writes the result
+     * straight into recv.buffer (no final copy) */
+    const int direct = c->rbuf_user && k + 1 == c->nsteps &&
+                       !(s->recv_first && s->send_cnt);
+    unsigned out, i;
+    void *dst;
+    ucs_status_t st;
+
+    if (c->rdy_cnt[k] < s->recv_cnt) {
+        return 0;
+    }
+    out = c->readers[c->cur_buf] ? !c->cur_buf : c->cur_buf;
+    if (!direct && c->readers[out]) {
+        return 0;
+    }
+    dst = direct ? (void*)c->rbuf_user : c->dbuf[out];
+    for (i = 0; i < s->recv_cnt; i++) {
+        srcs[1 + i] = c->peer_buf[c->rdy_peer[k][i]][c->rdy_buf[k][i]];
+        if (srcs[1 + i] == NULL) {
+            finish(c, UCS_ERR_IO_ERROR);      /* a READY without a key */
+            return 0;
+        }
+    }
+    if (s->aggregation == AGG_REDUCE) {
+        srcs[0] = c->dbuf[c->cur_buf];
+        st = rma_fold(c, dst, srcs, 1 + s->recv_cnt);
+    } else {
+        st = (s->recv_cnt == 1) ? rma_copy(c, dst, srcs[1]) : UCS_ERR_IO_ERROR;
+    }
+    if (st != UCS_OK) {
+        finish(c, st);
+        return 0;
+    }
+    for (i = 0; i < s->recv_cnt; i++) {
+        rma_post(c, c->rdy_peer[k][i], RMA_DONE, c->rdy_buf[k][i], NULL, 0);
+    }
+    if (direct) {
+        c->rma_final = 1;
+    } else {
+        c->cur_buf = out;
+    }
+    return 1;
+}
+
+/* as far as the messages in allow; the op completes once the result is in
+ * recv.buffer and nobody reads this member's buffers any more */
+UCG_INTERNAL void rma_advance(ucg_builtin_lcoll_t *c)
+{
+    if (c->rma_busy) {
+        c->rma_again = 1;
+        return;
+    }
+    c->rma_busy = 1;
+    do {
+        c->rma_again = 0;
+        rma_flush(c);
+        while (!c->done && c->cur < c->nsteps) {
+            const op_step_t *s = &c->steps[c->cur];
+            if (!s->recv_first && !c->rma_sent) {
+                rma_expose(c, s);
+                c->rma_sent = 1;
+            }
+            if (s->recv_cnt && !c->rma_recvd) {
+                if (!rma_receive(c, s)) {
+                    break;
+                }
+                c->rma_recvd = 1;
+            }
+            if (s->recv_first && !c->rma_sent) {
+                rma_expose(c, s);
+                c->rma_sent = 1;
+            }
+            c->cur++;
+            c->rma_sent = c->rma_recvd = 0;
+        }
+        if (!c->done && c->cur == c->nsteps && !c->rma_final) {
+            ucs_status_t st = c->rbuf_user ?
+                rma_copy(c, c->rbuf_user, c->dbuf[c->cur_buf]) : UCS_OK;
+            if (st != UCS_OK) {
+                finish(c, st);
+            }
+            c->rma_final = 1;
+        }
+        rma_flush(c);
+        if (!c->done && c->rma_final && c->out_tail == 0 &&
+            c->readers[0] == 0 && c->readers[1] == 0) {
+            finish(c, UCS_OK);
+        }
+    } while (c->rma_again && !c->done);
+    c->rma_busy = 0;
+}
+
+/* a control message of this op (am_handler, or the stash at start) */
+UCG_INTERNAL void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *data,
+                    size_t length)
+{
+    uint32_t w[2];
+    unsigned k;
+    if (c->done) {
+        return;
+    }
+    if (length < 8) {
+        finish(c, UCS_ERR_IO_ERROR);
+        return;
+    }
+    memcpy(w, data, 8);
+    if (w[0] >= c->g->size || w[0] == c->g->my || w[1] > 1) {
+        finish(c, UCS_ERR_IO_ERROR);   /* e.g. a member that took the host path */
+        return;
+    }
+    if (h.step_idx == RMA_RKEY) {
+        void *p = NULL;
+        ucs_status_t st;
+        if (length != 8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES || c->peer_buf[w[0]][w[1]]) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        st = rma_import(c->g, w[0], c->rma, (const char*)data + 8, &p);
+        if (st != UCS_OK) {
+            finish(c, st);
+            return;
+        }
+        c->peer_buf[w[0]][w[1]] = p;
+        return;                        /* nothing waits on a key alone */
+    }
+    if (h.step_idx == RMA_DONE) {
+        if (c->readers[w[1]] == 0) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        c->readers[w[1]]--;
+    } else {
+        for (k = 0; k < c->nsteps && c->steps[k].step_idx != h.step_idx; k++) {
+        }
+        if (k == c->nsteps || c->rdy_cnt[k] == c->steps[k].recv_cnt) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        c->rdy_peer[k][c->rdy_cnt[k]] = (uint8_t)w[0];
+        c->rdy_buf[k][c->rdy_cnt[k]]  = (uint8_t)w[1];
+        c->rdy_cnt[k]++;
+    }
+    rma_advance(c);
+}
+
+/* at create: the op's own buffers and their keys */
+UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
+{
+    ucg_dev_op_t o;
+    ucg_dev_dtype_t d;
+    unsigned i;
+    if (ucg_builtin_shm_iface_max_short(c->g->iface) < RMA_MIN_SHORT ||
+        (c->rma == RMA_DEV &&
+         !ucg_builtin_combine_classify(c->g->cmb, c->op, c->dtype, &o, &d))) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    c->rbuf_user = rbuf_user;
+    for (i = 0; i < 2; i++) {
+        int k = rma_pool_get(c->g, c->length ? c->length : 1, c->rma);
+        if (k < 0) {
+            return UCS_ERR_NO_MEMORY;
+        }
+        c->pool_idx[i] = k;
+        c->dbuf[i]     = c->g->pool[k].ptr;
+        memcpy(c->key[i], c->g->pool[k].key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    }
+    return UCS_OK;
+}
+
+UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
+{
+    ucs_status_t st;
+    unsigned k, e;
+    stash_t **pp;
+
+    c->cur       = 0;
+    c->cur_buf   = 0;
+    c->rma_sent  = c->rma_recvd = c->rma_final = 0;
+    c->readers[0] = c->readers[1] = 0;
+    c->out_head  = c->out_tail = 0;
+    c->send_pending = 0;
+    memset(c->rdy_cnt, 0, sizeof(c->rdy_cnt));
+    if (c->length == 0) {
+        c->done   = 1;
+        c->status = UCS_OK;
+        return UCS_OK;
+    }
+    /* ucg_builtin_init_reduce (builtin_control.c:43-47): this member's data
+     * into its first buffer - every member, since every member exposes it */
+    st = rma_copy(c, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf);
+    if (st != UCS_OK) {
+        c->done   = 1;
+        c->status = st;
+        return st;
+    }
+    c->done   = 0;
+    c->status = UCS_INPROGRESS;
+    c->active = 1;
+    slot->req = c;
+    c->rma_busy = 1;                  /* post and drain before advancing */
+    if (!c->keys_sent) {
+        /* the keys go to every member that reads from this one */
+        uint8_t sent[UCG_BUILTIN_OPS_MAX_MEMBERS] = {0};
+        for (k = 0; k < c->nsteps; k++) {
+            for (e = 0; e < c->steps[k].send_cnt; e++) {
+                unsigned p = c->steps[k].send_peers[e];
+                if (!sent[p]) {
+                    sent[p] = 1;
+                    rma_post(c, p, RMA_RKEY, 0, c->key[0], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+                    rma_post(c, p, RMA_RKEY, 1, c->key[1], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+                }
+            }
+        }
+        c->keys_sent = 1;
+    }
+    /* what arrived before this start (ucg_builtin_step_check_pending) */
+    pp = &slot->msgs;
+    while (*pp && !c->done) {
+        stash_t *m = *pp;
+        ops_header_t h;
+        h.header = m->header;
+        if (h.coll_id != c->coll_id) {
+            pp = &m->next;
+            continue;
+        }
+        *pp = m->next;
+        if (m->next == NULL) {
+            slot->msgs_tail = pp;
+        }
+        rma_msg(c, h, m->data, m->length);
+        free(m);
+    }
+    c->rma_busy = 0;
+    rma_advance(c);
+    return c->done ? c->status : UCS_INPROGRESS;
+}
+
+/* the op's buffers go back to the group's pool; peers' mappings stay */
+UCG_INTERNAL void rma_free(ucg_builtin_lcoll_t *c)
+{
+    unsigned i;
+    for (i = 0; i < 2; i++) {
+        if (c->pool_idx[i] >= 0) {
+            c->g->pool[c->pool_idx[i]].busy = 0;
+        }
+    }
+    free(c->outbox);
+}

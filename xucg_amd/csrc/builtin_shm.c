@@ -1,0 +1,296 @@
+/*
+ * builtin_shm.c - f2: a minimal shared-memory active-message transport for the
+ * builtin engine (include/ucg_builtin_ops.h): per-pair SPSC rings of AM-short
+ * cells (UCS_ERR_NO_RESOURCE when full, as uct_ep_am_short), delivery with
+ * the data borrowed for the callback only, the incast cell of the UCX
+ * collectives extension, and a barrier for set-up and tear-down.
+ */
+#define _GNU_SOURCE
+#include "builtin_int.h"
+
+#include <fcntl.h>
+#include <sched.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+static ring_ctl_t *ring_ctl(ucg_builtin_shm_iface_t *it, unsigned src, unsigned dst)
+{
+    return (ring_ctl_t*)(it->seg + SEG_CTL_BYTES +
+                         ((size_t)src * it->members + dst) * it->ring_bytes);
+}
+
+static cell_t *ring_cell(ucg_builtin_shm_iface_t *it, ring_ctl_t *r, uint64_t idx)
+{
+    return (cell_t*)((char*)r + sizeof(ring_ctl_t) + (idx % it->cells) * it->cell_size);
+}
+
+static incast_ctl_t *incast_ctl(ucg_builtin_shm_iface_t *it, unsigned member)
+{
+    return (incast_ctl_t*)(it->seg + it->incast_base + member * it->incast_bytes);
+}
+
+static incast_cell_t *incast_cell(ucg_builtin_shm_iface_t *it, unsigned member,
+                                  unsigned idx)
+{
+    return (incast_cell_t*)((char*)incast_ctl(it, member) + sizeof(incast_ctl_t) +
+                            (size_t)idx * it->incast_cell_size);
+}
+
+ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
+                                        unsigned my_index, size_t max_short,
+                                        unsigned ring_cells,
+                                        ucg_builtin_shm_iface_t **iface_p)
+{
+    ucg_builtin_shm_iface_t *it;
+    int fd;
+    struct stat stt;
+
+    if (name == NULL || iface_p == NULL || members == 0 ||
+        members > UCG_BUILTIN_OPS_MAX_MEMBERS || my_index >= members ||
+        max_short <= 8 || max_short > (1u << 20) || ring_cells < 2) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    it = calloc(1, sizeof(*it));
+    if (it == NULL) {
+        return UCS_ERR_NO_MEMORY;
+    }
+    snprintf(it->name, sizeof(it->name), "/%s", name[0] == '/' ? name + 1 : name);
+    it->members    = members;
+    it->my         = my_index;
+    it->max_short  = max_short;
+    it->cells      = ring_cells;
+    it->cell_size  = (sizeof(cell_t) + (max_short - 8) + 63) & ~(size_t)63;
+    it->ring_bytes = sizeof(ring_ctl_t) + (size_t)ring_cells * it->cell_size;
+    it->incast_cell_size = (sizeof(incast_cell_t) + (max_short - 8) + 63) & ~(size_t)63;
+    it->incast_bytes     = sizeof(incast_ctl_t) + (size_t)ring_cells * it->incast_cell_size;
+    it->incast_base      = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
+    it->seg_bytes        = it->incast_base + (size_t)members * it->incast_bytes;
+
+    fd = shm_open(it->name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) {
+        free(it);
+        return UCS_ERR_IO_ERROR;
+    }
+    /* a fresh object is zero-filled: every ring starts empty (head = tail) */
+    if (fstat(fd, &stt) != 0 ||
+        ((size_t)stt.st_size < it->seg_bytes && ftruncate(fd, it->seg_bytes) != 0)) {
+        close(fd);
+        free(it);
+        return UCS_ERR_IO_ERROR;
+    }
+    it->seg = mmap(NULL, it->seg_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (it->seg == MAP_FAILED) {
+        free(it);
+        return UCS_ERR_NO_MEMORY;
+    }
+    ucg_builtin_shm_barrier(it);   /* everybody mapped before any send */
+    *iface_p = it;
+    return UCS_OK;
+}
+
+void ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *it)
+{
+    stash_t *m;
+    if (it == NULL) {
+        return;
+    }
+    ucg_builtin_shm_barrier(it);
+    munmap(it->seg, it->seg_bytes);
+    if (it->my == 0) {
+        shm_unlink(it->name);
+    }
+    while ((m = it->unexpected) != NULL) {
+        it->unexpected = m->next;
+        free(m);
+    }
+    free(it);
+}
+
+size_t ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *it)
+{
+    return it ? it->max_short : 0;
+}
+
+void ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
+{
+    _Atomic uint64_t *arrive = (_Atomic uint64_t*)it->seg;
+    uint64_t gen = ++it->barrier_gen;
+    double t0 = now_s(), lim = wait_timeout_s();
+    atomic_fetch_add_explicit(arrive, 1, memory_order_acq_rel);
+    while (atomic_load_explicit(arrive, memory_order_acquire) < gen * it->members) {
+        if (now_s() - t0 > lim) {
+            fprintf(stderr, "ucg_builtin_shm_barrier(%s): timed out after %.0f s\n",
+                    it->name, lim);
+            abort();
+        }
+        sched_yield();
+    }
+}
+
+ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *it, unsigned peer,
+                                      uint64_t header, const void *payload,
+                                      size_t length)
+{
+    ring_ctl_t *r;
+    uint64_t head, tail;
+    cell_t *c;
+
+    if (peer >= it->members || peer == it->my) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (length + 8 > it->max_short) {
+        return UCS_ERR_INVALID_PARAM;   /* UCS_ERR_MESSAGE_TRUNCATED in UCT */
+    }
+    r    = ring_ctl(it, it->my, peer);
+    head = atomic_load_explicit(&r->head, memory_order_relaxed);
+    tail = atomic_load_explicit(&r->tail, memory_order_acquire);
+    if (head - tail >= it->cells) {
+        return UCS_ERR_NO_RESOURCE;
+    }
+    c = ring_cell(it, r, head);
+    c->length = (uint32_t)length;
+    c->header = header;
+    if (length) {
+        memcpy(c + 1, payload, length);
+    }
+    atomic_store_explicit(&r->head, head + 1, memory_order_release);
+    return UCS_OK;
+}
+
+static void spin_lock(_Atomic uint32_t *l)
+{
+    unsigned spins = 0;
+    uint32_t z = 0;
+    double t0 = 0.0;
+    while (!atomic_compare_exchange_weak_explicit(l, &z, 1, memory_order_acquire,
+                                                  memory_order_relaxed)) {
+        z = 0;
+        /* the holder packs at most one fragment: spin briefly, then yield;
+         * a holder that never lets go (a dead peer) is fatal, not a hang */
+        if (++spins < 256) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        if (t0 == 0.0) {
+            t0 = now_s();
+        } else if ((spins & 1023) == 0 && now_s() - t0 > wait_timeout_s()) {
+            fprintf(stderr, "ucg_builtin_shm: incast cell lock held for over %.0f s\n",
+                    wait_timeout_s());
+            abort();
+        }
+        sched_yield();
+    }
+}
+
+static void spin_unlock(_Atomic uint32_t *l)
+{
+    atomic_store_explicit(l, 0, memory_order_release);
+}
+
+ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *it, unsigned root,
+                                       uint64_t header, unsigned expected,
+                                       size_t length, ucg_builtin_pack_cb_f pack,
+                                       void *arg, int concurrent)
+{
+    unsigned idx;
+    incast_cell_t *c;
+    int first;
+
+    if (root >= it->members || root == it->my || expected == 0 || pack == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (length + 8 > it->max_short) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    /* the cell of this message: consecutive fragments of one message
+     * (remote_offset in steps of at most max_short - 8) take consecutive
+     * cells from a start that a multiplicative hash of the rest of the
+     * header (group, coll_id, step) spreads out */
+    idx = (unsigned)((((header & 0xffffffffull) * 0x9E3779B97F4A7C15ull) >> 40) +
+                     (header >> 32) / (it->max_short - 8)) % it->cells;
+    c   = incast_cell(it, root, idx);
+    spin_lock(&c->lock);
+    /* acquire: the root's reads of a delivered cell precede our writes */
+    if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FREE) {
+        atomic_store_explicit(&c->state, INCAST_FILLING, memory_order_relaxed);
+        atomic_store_explicit(&c->count, 0, memory_order_relaxed);
+        c->header   = header;
+        c->expected = expected;
+        c->length   = (uint32_t)length;
+        first       = 1;
+    } else if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FILLING &&
+               c->header == header) {
+        first = 0;
+    } else {
+        spin_unlock(&c->lock);
+        return UCS_ERR_NO_RESOURCE;   /* cell busy with another message */
+    }
+    if (concurrent) {
+        /* atomic packers add into a zeroed cell outside the lock */
+        if (first) {
+            memset(c + 1, 0, length);
+        }
+        spin_unlock(&c->lock);
+        pack(arg, c + 1, 1);
+    } else {
+        pack(arg, c + 1, !first);     /* first copies, the others reduce */
+    }
+    if (atomic_fetch_add_explicit(&c->count, 1, memory_order_acq_rel) + 1 == expected) {
+        atomic_store_explicit(&c->state, INCAST_READY, memory_order_release);
+        atomic_fetch_add_explicit(&incast_ctl(it, root)->ready, 1, memory_order_release);
+    }
+    if (!concurrent) {
+        spin_unlock(&c->lock);
+    }
+    return UCS_OK;
+}
+
+static unsigned incast_progress(ucg_builtin_shm_iface_t *it, ucg_builtin_am_cb_f cb,
+                                void *arg)
+{
+    incast_ctl_t *ctl = incast_ctl(it, it->my);
+    unsigned i, n = 0;
+    if (atomic_load_explicit(&ctl->ready, memory_order_acquire) == 0) {
+        return 0;
+    }
+    for (i = 0; i < it->cells; i++) {
+        incast_cell_t *c = incast_cell(it, it->my, i);
+        if (atomic_load_explicit(&c->state, memory_order_acquire) != INCAST_READY) {
+            continue;
+        }
+        (void)cb(arg, &c->header, 8 + (size_t)c->length);
+        atomic_fetch_sub_explicit(&ctl->ready, 1, memory_order_relaxed);
+        atomic_store_explicit(&c->state, INCAST_FREE, memory_order_release);
+        n++;
+    }
+    return n;
+}
+
+unsigned ucg_builtin_shm_progress(ucg_builtin_shm_iface_t *it,
+                                  ucg_builtin_am_cb_f cb, void *arg)
+{
+    unsigned src, n = incast_progress(it, cb, arg);
+    for (src = 0; src < it->members; src++) {
+        ring_ctl_t *r;
+        uint64_t tail, head;
+        if (src == it->my) {
+            continue;
+        }
+        r    = ring_ctl(it, src, it->my);
+        tail = atomic_load_explicit(&r->tail, memory_order_relaxed);
+        head = atomic_load_explicit(&r->head, memory_order_acquire);
+        while (tail < head) {
+            cell_t *c = ring_cell(it, r, tail);
+            (void)cb(arg, &c->header, 8 + (size_t)c->length);
+            tail++;
+            /* the cell is free only after the callback returned */
+            atomic_store_explicit(&r->tail, tail, memory_order_release);
+            n++;
+        }
+    }
+    return n;
+}
