@@ -166,6 +166,17 @@ ucs_status_t ucg_builtin_combine_dev_fold(ucg_builtin_combine_t *cmb, void *redu
 /* dst[0:bytes] = src[0:bytes], either side device or peer-mapped memory */
 ucs_status_t ucg_builtin_combine_dev_copy(ucg_builtin_combine_t *cmb, void *dst,
                                           const void *src, size_t bytes);
+/* n copies of `bytes` each in one launch (ucg_builtin_dev_copy_multi), n <= 16 */
+ucs_status_t ucg_builtin_combine_dev_copy_n(ucg_builtin_combine_t *cmb,
+                                            void *const *dsts, const void *const *srcs,
+                                            unsigned n, size_t bytes);
+/* dst = V(self, log2 nsrc) of the recursive-doubling association over the
+ * nsrc operands (ucg_builtin_dev_reduce_multi): the result member `self`
+ * holds after the reference's recursive doubling, in one pass */
+ucs_status_t ucg_builtin_combine_dev_butterfly(ucg_builtin_combine_t *cmb, void *reduce_op,
+                                               void *datatype, void *dst,
+                                               const void *const *srcs, unsigned nsrc,
+                                               unsigned self, size_t count);
 
 /* [0] host calls, [1] host bytes, [2] device calls, [3] device bytes,
  * [4] steps staged on the device, [5] callback errors seen */

@@ -192,21 +192,29 @@ def test_engine_placements_shm_zcopy(spec, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("spec", ["4:4:0:8:2:16", "8:8:0:8:2:16", "6:6:0:8:2:16",
-                                  "12:3:0:2:2:16", "8:8:4:8:2:4", "8:2:0:8:4:16",
-                                  "5:1:0:2:2:16"])
-def test_engine_placements_device_buffers(spec, monkeypatch):
+@pytest.mark.parametrize("spec,oneshot", [
+    ("4:4:0:8:2:16", "y"), ("8:8:0:8:2:16", "y"), ("2:2:0:8:2:16", "y"),
+    ("4:4:0:8:2:16", "n"), ("8:8:0:8:2:16", "n"), ("6:6:0:8:2:16", "y"),
+    ("12:3:0:2:2:16", "y"), ("8:8:4:8:2:4", "y"), ("8:2:0:8:4:16", "y"),
+    ("5:1:0:2:2:16", "y")])
+def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     """Device buffers: the same plans as remote-key steps (the reference's
     rkey exchange + zero-copy reads, builtin_control.c:1014-1076,
     builtin_data.c:326-340) - recursive doubling, the one-host tree, waypoints
     of the inter-host tree and of the socket level, K-ing with K = 4, a
     three-level tree - each member's plan equal to the oracle's and every
-    result bit-exact against its simulation, twice per persistent op."""
+    result bit-exact against its simulation, twice per persistent op. Plain
+    recursive doubling runs as the one-shot reduce-scatter + all-gather
+    unless UCX_BUILTIN_DEVICE_ONESHOT=n: the same bits either way."""
     n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
     monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")   # a lost message fails fast
+    monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT", oneshot)
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)
     assert codes == [0] * n, "\n".join(outs)
+    flat_doubling = spec.split(":")[1] == spec.split(":")[0] and factor == 2 and \
+        (n & (n - 1)) == 0 and 4 <= n <= 16
+    assert ("Executed as: one-shot" in outs[0]) == (flat_doubling and oneshot == "y")
     if factor == 2:
         d = _digests(outs)
         assert all(x == d[0] for x in d), d

@@ -600,6 +600,54 @@ ucs_status_t ucg_builtin_combine_dev_copy(ucg_builtin_combine_t *cmb, void *dst,
     return st;
 }
 
+ucs_status_t ucg_builtin_combine_dev_copy_n(ucg_builtin_combine_t *cmb,
+                                            void *const *dsts, const void *const *srcs,
+                                            unsigned n, size_t bytes)
+{
+    ucs_status_t st;
+    if (cmb == NULL || cmb->dev == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (bytes == 0 || n == 0) {
+        return UCS_OK;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    st = ucg_builtin_dev_copy_multi(cmb->dev, dsts, srcs, n, bytes);
+    if (st == UCS_OK) {
+        st = ucg_builtin_dev_complete(cmb->dev);
+    }
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
+ucs_status_t ucg_builtin_combine_dev_butterfly(ucg_builtin_combine_t *cmb, void *reduce_op,
+                                               void *datatype, void *dst,
+                                               const void *const *srcs, unsigned nsrc,
+                                               unsigned self, size_t count)
+{
+    ucg_dev_op_t op;
+    ucg_dev_dtype_t dt;
+    ucs_status_t st;
+    if (cmb == NULL || cmb->dev == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (!ucg_builtin_combine_classify(cmb, reduce_op, datatype, &op, &dt)) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    if (count == 0) {
+        return UCS_OK;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    st = ucg_builtin_dev_reduce_multi(cmb->dev, op, dt, dst, srcs, nsrc, self, count);
+    if (st == UCS_OK) {
+        cmb->stats[2]++;
+        cmb->stats[3] += count * ucg_builtin_dev_dtype_size(dt) * nsrc;
+        st = ucg_builtin_dev_complete(cmb->dev);
+    }
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
 void ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb, uint64_t out[6])
 {
     int i;

@@ -261,6 +261,8 @@ struct ucg_builtin_lcoll {
     uint8_t      rdy_buf[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
                                   /* ... in arrival order: the fold order */
     int          rma_sent, rma_recvd, rma_final, rma_busy, rma_again;
+    int          oneshot;         /* recursive doubling run as one-shot
+                                     reduce-scatter + all-gather */
     struct rma_msg *outbox;       /* control messages not sent yet */
     unsigned     out_head, out_tail, out_cap;
 };

@@ -905,6 +905,10 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             "senders' buffers in one kernel\n" :
             "Buffers: shared memory; remote keys once per op, every step reads its "
             "senders' buffers in place\n");
+        if (c->oneshot) {
+            PUT("Executed as: one-shot reduce-scatter (every shard of the plan's "
+                "association read from all members) + all-gather\n");
+        }
     }
     for (k = 0; k < c->nsteps; k++) {
         const op_step_t *s = &c->steps[k];

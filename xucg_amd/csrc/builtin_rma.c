@@ -397,6 +397,123 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
     return 1;
 }
 
+/* ---- recursive doubling on device buffers as one exchange ----------------
+ * For an allreduce whose plan is plain recursive doubling (a power-of-two
+ * group on one host, factor 2), every element of the result is
+ * V(self, log2 N) of builtin_recursive.c:158-169 - the same on every member.
+ * On device buffers the whole plan then runs as two remote-key phases over
+ * all xGMI links at once instead of log2 N pairwise ones: (0) every member
+ * exposes its data and computes its 1/N shard of V with one kernel reading
+ * that shard from all N buffers (ucg_builtin_dev_reduce_multi); (1) every
+ * member exposes its reduced shard and copies all N shards into recv.buffer.
+ * Same bits as the steps; UCX_BUILTIN_DEVICE_ONESHOT=n runs the steps. From
+ * 4 to 16 members (reduce_multi's operand limit). */
+static int oneshot_enabled(void)
+{
+    const char *e = getenv("UCX_BUILTIN_DEVICE_ONESHOT");
+    return !(e && (e[0] == 'n' || e[0] == 'N' || e[0] == '0'));
+}
+
+/* shard r of the op: [r * se, min(count, (r + 1) * se)) elements, se a
+ * multiple of 256 bytes so shards start on 256-B boundaries */
+static void oneshot_shard(const ucg_builtin_lcoll_t *c, unsigned r, size_t *lo, size_t *n)
+{
+    const size_t per = 256 / c->dt_len ? 256 / c->dt_len : 1;
+    const size_t cnt = (size_t)c->count, N = c->g->size;
+    size_t se = (cnt + N - 1) / N;
+    se = (se + per - 1) / per * per;
+    *lo = (size_t)r * se < cnt ? (size_t)r * se : cnt;
+    *n  = (*lo + se < cnt ? *lo + se : cnt) - *lo;
+}
+
+static void oneshot_expose(ucg_builtin_lcoll_t *c, unsigned phase)
+{
+    unsigned p;
+    for (p = 0; p < c->g->size; p++) {
+        if (p != c->g->my) {
+            rma_post(c, p, (uint8_t)(phase + 1), phase, NULL, 0);
+        }
+    }
+    c->readers[phase] += c->g->size - 1;
+}
+
+/* the phase's kernel once every peer's READY is in; DONE to all */
+static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
+{
+    const unsigned N = c->g->size, my = c->g->my;
+    const void *srcs[16];
+    void *dsts[16];
+    ucs_status_t st = UCS_OK;
+    size_t lo, n, full_lo, full_n;
+    unsigned r, k;
+
+    if (c->rdy_cnt[phase] < N - 1) {
+        return 0;
+    }
+    for (r = 0; r < N; r++) {
+        if (r != my && c->peer_buf[r][phase] == NULL) {
+            finish(c, UCS_ERR_IO_ERROR);          /* a READY without a key */
+            return 0;
+        }
+    }
+    if (phase == 0) {
+        oneshot_shard(c, my, &lo, &n);
+        for (r = 0; r < N; r++) {
+            srcs[r] = (const char*)(r == my ? c->dbuf[0] : c->peer_buf[r][0]) + lo * c->dt_len;
+        }
+        st = ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype,
+                                               (char*)c->dbuf[1] + lo * c->dt_len, srcs, N,
+                                               my, n);
+    } else {
+        /* every full shard in one launch, the ragged last one in another */
+        oneshot_shard(c, 0, &full_lo, &full_n);
+        for (k = 0, r = 0; r < N && st == UCS_OK; r++) {
+            oneshot_shard(c, r, &lo, &n);
+            if (n == 0) {
+                continue;
+            }
+            srcs[k] = (const char*)(r == my ? c->dbuf[1] : c->peer_buf[r][1]) + lo * c->dt_len;
+            dsts[k] = c->rbuf_user + lo * c->dt_len;
+            if (n != full_n) {
+                st = ucg_builtin_combine_dev_copy_n(c->g->cmb, &dsts[k], &srcs[k], 1,
+                                                    n * c->dt_len);
+            } else {
+                k++;
+            }
+        }
+        if (st == UCS_OK) {
+            st = ucg_builtin_combine_dev_copy_n(c->g->cmb, dsts, srcs, k,
+                                                full_n * c->dt_len);
+        }
+    }
+    if (st != UCS_OK) {
+        finish(c, st);
+        return 0;
+    }
+    for (r = 0; r < N; r++) {
+        if (r != my) {
+            rma_post(c, r, RMA_DONE, phase, NULL, 0);
+        }
+    }
+    return 1;
+}
+
+static void oneshot_advance(ucg_builtin_lcoll_t *c)
+{
+    while (!c->done && c->cur < 2) {
+        if (!c->rma_sent) {
+            oneshot_expose(c, c->cur);
+            c->rma_sent = 1;
+        }
+        if (!oneshot_receive(c, c->cur)) {
+            return;
+        }
+        c->cur++;
+        c->rma_sent = 0;
+    }
+    c->rma_final = 1;                 /* phase 1 wrote recv.buffer */
+}
+
 /* as far as the messages in allow; the op completes once the result is in
  * recv.buffer and nobody reads this member's buffers any more */
 UCG_INTERNAL void rma_advance(ucg_builtin_lcoll_t *c)
@@ -409,7 +526,10 @@ UCG_INTERNAL void rma_advance(ucg_builtin_lcoll_t *c)
     do {
         c->rma_again = 0;
         rma_flush(c);
-        while (!c->done && c->cur < c->nsteps) {
+        if (c->oneshot) {
+            oneshot_advance(c);
+        }
+        while (!c->oneshot && !c->done && c->cur < c->nsteps) {
             const op_step_t *s = &c->steps[c->cur];
             if (!s->recv_first && !c->rma_sent) {
                 rma_expose(c, s);
@@ -484,6 +604,15 @@ UCG_INTERNAL void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *da
             return;
         }
         c->readers[w[1]]--;
+    } else if (c->oneshot) {
+        k = h.step_idx - 1u;              /* phases 0 and 1 */
+        if (k > 1 || w[1] != k || c->rdy_cnt[k] == c->g->size - 1) {
+            finish(c, UCS_ERR_IO_ERROR);
+            return;
+        }
+        c->rdy_peer[k][c->rdy_cnt[k]] = (uint8_t)w[0];
+        c->rdy_buf[k][c->rdy_cnt[k]]  = (uint8_t)w[1];
+        c->rdy_cnt[k]++;
     } else {
         for (k = 0; k < c->nsteps && c->steps[k].step_idx != h.step_idx; k++) {
         }
@@ -510,6 +639,11 @@ UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
         return UCS_ERR_UNSUPPORTED;
     }
     c->rbuf_user = rbuf_user;
+    /* from 4 members on: at 2 the one step moves no more than the exchange
+     * (r02os: 64 MiB, 0.187 ms one-shot against 0.127 ms as the step) */
+    c->oneshot   = c->rma == RMA_DEV && c->kind == 0 && oneshot_enabled() &&
+                   c->g->size >= 4 && c->g->size <= 16 && c->plan &&
+                   strcmp(c->plan, "recursive doubling") == 0;
     for (i = 0; i < 2; i++) {
         int k = rma_pool_get(c->g, c->length ? c->length : 1, c->rma);
         if (k < 0) {
@@ -556,9 +690,13 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     if (!c->keys_sent) {
         /* the keys go to every member that reads from this one */
         uint8_t sent[UCG_BUILTIN_OPS_MAX_MEMBERS] = {0};
-        for (k = 0; k < c->nsteps; k++) {
-            for (e = 0; e < c->steps[k].send_cnt; e++) {
-                unsigned p = c->steps[k].send_peers[e];
+        for (k = 0; k < (c->oneshot ? 1 : c->nsteps); k++) {
+            const unsigned ne = c->oneshot ? c->g->size : c->steps[k].send_cnt;
+            for (e = 0; e < ne; e++) {
+                unsigned p = c->oneshot ? e : c->steps[k].send_peers[e];
+                if (p == c->g->my) {
+                    continue;
+                }
                 if (!sent[p]) {
                     sent[p] = 1;
                     rma_post(c, p, RMA_RKEY, 0, c->key[0], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);

@@ -68,6 +68,10 @@ HOST_API = {
     "ucg_builtin_combine_dev_fold": (_int, [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp), _u,
                                             _sz]),
     "ucg_builtin_combine_dev_copy": (_int, [_vp, _vp, _vp, _sz]),
+    "ucg_builtin_combine_dev_copy_n": (_int, [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp),
+                                              _u, _sz]),
+    "ucg_builtin_combine_dev_butterfly": (_int, [_vp, _vp, _vp, _vp, ctypes.POINTER(_vp), _u,
+                                                 _u, _sz]),
     # include/ucg_builtin_ops.h
     "ucg_builtin_shm_iface_open": (_int, [ctypes.c_char_p, _u, _u, _sz, _u,
                                           ctypes.POINTER(_vp)]),
