@@ -40,7 +40,8 @@ from mock_mpi import MockMPI, OPS, DTYPES, op_classifier, dt_classifier  # noqa:
 
 UCS_ERR_UNSUPPORTED = -22
 CASES = [("int32", "sum", 3001), ("uint8", "bxor", 777), ("int64", "max", 257),
-         ("float64", "sum", 1500), ("uint32", "sum", 64), ("int16", "prod", 33)]
+         ("float64", "sum", 1500), ("uint32", "sum", 64), ("int16", "prod", 33),
+         ("float16", "max", 513), ("bfloat16", "min", 300)]
 STEP_RE = re.compile(r"Step #\d+ \(step_idx (\d+)\): (\w+)"
                      r"(?:, send (?:send|recv)\.buffer to ([\d ]+))?"
                      r"(?:, receive from ([\d ]+))?"
