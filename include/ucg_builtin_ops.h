@@ -194,6 +194,16 @@ int          ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *coll,
 /* Progress until complete (or error); returns the final status. */
 ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *coll);
 void         ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *coll);
+/* ucg_params_t.completion (api/ucg.h:162-171), called where the reference's
+ * ucg_builtin_comp_last_step_cb calls it (builtin_comp_step.inl:8-38): when a
+ * start completes - from lcoll_start itself, or from progress - cb(req,
+ * status) runs; with cb NULL, a 1 byte is written at req + flag_offset and the
+ * status (ucs_status_t) at req + status_offset. Also called with
+ * UCS_ERR_CANCELED when an op still running is destroyed. */
+typedef void (*ucg_builtin_coll_comp_cb_f)(void *req, ucs_status_t status);
+ucs_status_t ucg_builtin_lcoll_set_completion(ucg_builtin_lcoll_t *coll,
+                                              ucg_builtin_coll_comp_cb_f cb, void *req,
+                                              size_t flag_offset, size_t status_offset);
 /* The plan as the builtin planner's print (builtin/builtin.c:750-901):
  * steps, peers, fragment length and count. Returns bytes written. */
 size_t       ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *coll, char *buf,

@@ -91,6 +91,17 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
     assert line["bit_exact"] and line["ranks"] == world
 
 
+@pytest.mark.parametrize("world", [3, 4])
+def test_completion_callback_and_flags(world):
+    """ucg_params_t.completion (api/ucg.h:162-171) as
+    ucg_builtin_comp_last_step_cb calls it (builtin_comp_step.inl:8-38): an
+    allreduce completed by progress alone reports once through the callback
+    with the caller's request, then - with no callback - through a flag byte
+    and the status written into the request at the given offsets."""
+    codes, outs = launch("_worker_comp.py", world, args=(shm_name(),), timeout=120)
+    assert codes == [0] * world, "\n".join(outs)
+
+
 def test_plan_description_and_unsupported_sizes():
     mpi = MockMPI()
     cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))

@@ -263,6 +263,11 @@ struct ucg_builtin_lcoll {
     int          rma_sent, rma_recvd, rma_final, rma_busy, rma_again;
     int          oneshot;         /* recursive doubling run as one-shot
                                      reduce-scatter + all-gather */
+    /* ucg_params_t.completion (api/ucg.h:162-171) */
+    int          comp_set;
+    ucg_builtin_coll_comp_cb_f comp_cb;
+    void        *comp_req;
+    size_t       comp_flag_off, comp_status_off;
     struct rma_msg *outbox;       /* control messages not sent yet */
     unsigned     out_head, out_tail, out_cap;
 };
@@ -289,6 +294,7 @@ enum {
 
 /* builtin_ops.c */
 UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status);
+UCG_INTERNAL void lcoll_notify(ucg_builtin_lcoll_t *c);
 
 /* builtin_plan.c */
 UCG_INTERNAL ucs_status_t plan_ctx_init(ucg_builtin_lgroup_t *g, unsigned root,

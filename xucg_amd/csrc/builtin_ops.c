@@ -76,6 +76,23 @@ UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
     c->step_started = 0;
     slot->req       = NULL;
     slot->expecting = 0;
+    lcoll_notify(c);
+}
+
+/* coll_comp_cb_f, or the completion flag and status in the request
+ * (ucg_builtin_comp_last_step_cb, builtin_comp_step.inl:31-32) */
+UCG_INTERNAL void lcoll_notify(ucg_builtin_lcoll_t *c)
+{
+    if (!c->comp_set) {
+        return;
+    }
+    if (c->comp_cb) {
+        c->comp_cb(c->comp_req, c->status);
+    } else {
+        ucs_status_t st = c->status;
+        memcpy((char*)c->comp_req + c->comp_status_off, &st, sizeof(st));
+        *((volatile uint8_t*)c->comp_req + c->comp_flag_off) = 1;
+    }
 }
 
 /* ucg_builtin_step_check_pending, builtin_comp_step.inl:403-462 */
@@ -827,6 +844,7 @@ ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *c)
     if (c->nsteps == 0 || c->length == 0) {
         c->done   = 1;
         c->status = UCS_OK;
+        lcoll_notify(c);
         return UCS_OK;
     }
     c->active = 1;
@@ -872,6 +890,21 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
         sched_yield();
     }
     return c->status;
+}
+
+ucs_status_t ucg_builtin_lcoll_set_completion(ucg_builtin_lcoll_t *c,
+                                              ucg_builtin_coll_comp_cb_f cb, void *req,
+                                              size_t flag_offset, size_t status_offset)
+{
+    if (c == NULL || c->active || (cb == NULL && req == NULL)) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    c->comp_set        = 1;
+    c->comp_cb         = cb;
+    c->comp_req        = req;
+    c->comp_flag_off   = flag_offset;
+    c->comp_status_off = status_offset;
+    return UCS_OK;
 }
 
 void ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *c)

@@ -672,6 +672,7 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     if (c->length == 0) {
         c->done   = 1;
         c->status = UCS_OK;
+        lcoll_notify(c);
         return UCS_OK;
     }
     /* ucg_builtin_init_reduce (builtin_control.c:43-47): this member's data
@@ -680,6 +681,7 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     if (st != UCS_OK) {
         c->done   = 1;
         c->status = st;
+        lcoll_notify(c);
         return st;
     }
     c->done   = 0;

@@ -8,6 +8,7 @@ _u = ctypes.c_uint
 _u64 = ctypes.c_uint64
 
 REDUCE_CB = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _vp, ctypes.c_uint, _vp)
+COMP_CB = ctypes.CFUNCTYPE(None, _vp, ctypes.c_int)      # coll_comp_cb_f(req, status)
 OP_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp)
 CONVERT_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_size_t))
 IS_INT_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_int))
@@ -97,4 +98,5 @@ HOST_API = {
     "ucg_builtin_lcoll_wait": (_int, [_vp]),
     "ucg_builtin_lcoll_destroy": (None, [_vp]),
     "ucg_builtin_lcoll_describe": (_sz, [_vp, ctypes.c_char_p, _sz]),
+    "ucg_builtin_lcoll_set_completion": (_int, [_vp, _vp, _vp, _sz, _sz]),
 }

@@ -122,6 +122,16 @@ class _Collective:
             st = self.wait()
         return st
 
+    def set_completion(self, cb=None, req=None, flag_offset=0, status_offset=0):
+        """ucg_params_t.completion: cb(req, status) from the completing call,
+        or (cb None) a flag byte and the status written into `req` (an
+        address) at the offsets"""
+        from .host_api import COMP_CB
+        self._comp = COMP_CB(lambda r, st: cb(r, st)) if cb else None
+        return _lib.host().ucg_builtin_lcoll_set_completion(
+            self.handle, ctypes.cast(self._comp, ctypes.c_void_p) if cb else None,
+            req, flag_offset, status_offset)
+
     def describe(self):
         buf = ctypes.create_string_buffer(4096)
         n = _lib.host().ucg_builtin_lcoll_describe(self.handle, buf, len(buf))
