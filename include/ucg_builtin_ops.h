@@ -199,7 +199,9 @@ void         ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *coll);
  * start completes - from lcoll_start itself, or from progress - cb(req,
  * status) runs; with cb NULL, a 1 byte is written at req + flag_offset and the
  * status (ucs_status_t) at req + status_offset. Also called with
- * UCS_ERR_CANCELED when an op still running is destroyed. */
+ * UCS_ERR_CANCELED when an op still running is destroyed. The callback runs
+ * inside the engine: it may record the completion, not restart or destroy
+ * the op. */
 typedef void (*ucg_builtin_coll_comp_cb_f)(void *req, ucs_status_t status);
 ucs_status_t ucg_builtin_lcoll_set_completion(ucg_builtin_lcoll_t *coll,
                                               ucg_builtin_coll_comp_cb_f cb, void *req,
