@@ -186,6 +186,16 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *group,
  * REDUCE step at a time holds the combine's step staging (device mirror);
  * a step that finds it busy combines each fragment on its own through
  * ucg_builtin_combine_reduce (the reference's per-fragment call). */
+/* Registered memory of the group (the memory registration the reference's
+ * zero-copy steps rely on, ucg_builtin_step_zcopy_prep, builtin_control.c:
+ * 276-286): device memory (on_device, needs a device on the combine) or a
+ * POSIX shared-memory segment. Used as an op's send buffer (not in place), a
+ * remote-key step exposes it where it is instead of copying it into the op's
+ * own buffer first. Stays registered until the group is destroyed; mem_free
+ * returns it to the group's pool. NULL on failure. */
+void        *ucg_builtin_lgroup_mem_alloc(ucg_builtin_lgroup_t *group, size_t bytes,
+                                          int on_device);
+void         ucg_builtin_lgroup_mem_free(ucg_builtin_lgroup_t *group, void *ptr);
 /* ucg_collective_start: UCS_OK if complete, UCS_INPROGRESS, or an error */
 ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *coll);
 /* 1 when the last start completed; its status in *status */

@@ -24,6 +24,7 @@ Checks:
   - fp SUM of rounded values: within the SURVEY 8c-style relative bound of
     the fp64 sum, and "digest" lines so the test can check that every member
     of an allreduce holds identical bits."""
+import ctypes
 import hashlib
 import os
 import re
@@ -98,7 +99,37 @@ def main():
         return b
 
     def back(b, like):
+        if isinstance(b, int):             # registered group memory
+            return read_reg(b, like)
         return b if dctx is None else b.download(like.dtype, like.size)
+
+    # TOPO_REGISTERED=1: send buffers from the group's registered memory
+    # (ucg_builtin_lgroup_mem_alloc), exposed in place by remote-key steps
+    registered = os.environ.get("TOPO_REGISTERED") == "1" and mode in ("rma", "shm")
+
+    def read_reg(ptr, like):
+        out = np.empty_like(like)
+        if mode == "rma":
+            _lib.dev().ucg_builtin_dev_memcpy(dctx.handle, out.ctypes.data, ptr, out.nbytes)
+        else:
+            ctypes.memmove(out.ctypes.data, ptr, out.nbytes)
+        return out
+
+    def send_buf(a):
+        if not registered:
+            return buf(a)
+        p = group.mem_alloc(max(a.nbytes, 1), device=(mode == "rma"))
+        if mode == "rma":
+            _lib.dev().ucg_builtin_dev_memcpy(dctx.handle, p, a.ctypes.data, a.nbytes)
+        else:
+            ctypes.memmove(p, a.ctypes.data, a.nbytes)
+        return p
+
+    def free_buf(b):
+        if isinstance(b, int):
+            group.mem_free(b)
+        elif dctx is not None and b is not None:
+            b.free()
 
     iface = ops.ShmIface(name, n, rank, max_short=max_short, ring_cells=16)
     dist = ops.layout_distances(n, rank, ppn, socket or None)
@@ -125,7 +156,7 @@ def main():
                 oplan = P.plan(kind, n, rank, root=root, **cfgkw)
             except P.Unsupported:
                 want = oplan = None
-            sbuf = buf(inputs[rank].copy())
+            sbuf = send_buf(inputs[rank].copy())
             rbuf = buf(np.zeros_like(inputs[rank])) if (kind == "allreduce" or
                                                          rank == root) else None
             coll = (group.allreduce(sbuf, rbuf, count, DTYPES[dt], OPS[op]) if kind == "allreduce"
@@ -163,10 +194,11 @@ def main():
                          f"{got[bad[:3]].tolist()} want {want[rank][bad[:3]].tolist()}")
             if not (O.bits(back(sbuf, inputs[rank])) == O.bits(inputs[rank])).all():
                 fail(f"{kind} {dt} {op}: send buffer modified")
+            if registered and ci == 0 and "Send buffer: registered" not in coll.describe():
+                fail(f"{kind} root={root}: registered send buffer not exposed in place")
             coll.close()
             for b in (sbuf, rbuf):
-                if dctx is not None and b is not None:
-                    b.free()
+                free_buf(b)
 
     # rounded fp32: tolerance against the fp64 sum, digests for identity
     for ci, count in enumerate((4096, 1000)):

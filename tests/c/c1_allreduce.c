@@ -8,7 +8,9 @@
  * C1_DEVICE_STAGING=1 forces every combine onto the GPU (staged steps).
  * C1_DEVICE_BUFFERS=1 gives the engine device buffers (GPU rank % count): the
  * plan runs as remote-key steps, every receive one kernel reading the
- * senders' buffers over IPC.
+ * senders' buffers over IPC. C1_REGISTERED=1 takes the send buffer from the
+ * group's registered memory (device, or shared memory with
+ * UCX_BUILTIN_SHM_ZCOPY_THRESH), exposed in place.
  * C1_PPN=p [C1_SOCKET=s] places the members on hosts of p consecutive
  * members (sockets of s) through ucg_builtin_lgroup_create_ex; the planner
  * knobs come from the environment (UCX_BUILTIN_TREE_RADIX, ...).
@@ -78,7 +80,7 @@ int main(int argc, char **argv)
     double t0, us;
     const int devbufs = getenv("C1_DEVICE_BUFFERS") != NULL;
     ucg_builtin_dev_ctx_t *dev = NULL;
-    void *dsend = NULL, *drecv = NULL;
+    void *dsend = NULL, *drecv = NULL, *inputs_reg = NULL;
 
     if (getenv("C1_DEVICE_STAGING")) {
         /* every step staged on the GPU: the configuration read the way UCX
@@ -125,6 +127,21 @@ int main(int argc, char **argv)
         ucg_oracle_tree_reduce(ORA_SUM, ORA_F32, want, (const void *const*)inputs,
                                world, 0, NULL, count);
     }
+    if (getenv("C1_REGISTERED")) {
+        dev = devbufs ? ucg_builtin_combine_dev_ctx(cmb) : NULL;
+        dsend = ucg_builtin_lgroup_mem_alloc(g, count * sizeof(float), devbufs);
+        if (dsend == NULL) {
+            fprintf(stderr, "rank %u: no registered memory\n", rank);
+            return 1;
+        }
+        if (devbufs) {
+            ucg_builtin_dev_memcpy(dev, dsend, inputs[rank], count * sizeof(float));
+        } else {
+            memcpy(dsend, inputs[rank], count * sizeof(float));
+        }
+        inputs_reg = dsend;
+        dsend = NULL;
+    }
     if (devbufs) {
         dev = ucg_builtin_combine_dev_ctx(cmb);
         dsend = dev ? ucg_builtin_dev_malloc(dev, count * sizeof(float)) : NULL;
@@ -135,7 +152,8 @@ int main(int argc, char **argv)
             return 1;
         }
     }
-    if (ucg_builtin_lcoll_allreduce(g, devbufs ? dsend : (void*)inputs[rank],
+    if (ucg_builtin_lcoll_allreduce(g, inputs_reg ? inputs_reg :
+                                       devbufs ? dsend : (void*)inputs[rank],
                                     devbufs ? drecv : (void*)out, count, (void*)1,
                                     (void*)1, &c) != UCS_OK) {
         fprintf(stderr, "rank %u: allreduce create failed\n", rank);
@@ -182,6 +200,9 @@ int main(int argc, char **argv)
                (unsigned long long)cs[2], (unsigned long long)cs[4]);
     }
     ucg_builtin_lcoll_destroy(c);
+    if (inputs_reg) {
+        ucg_builtin_lgroup_mem_free(g, inputs_reg);
+    }
     ucg_builtin_lgroup_destroy(g);
     if (devbufs) {
         ucg_builtin_dev_free(dev, dsend);

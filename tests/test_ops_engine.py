@@ -49,7 +49,8 @@ def test_c1_harness_bit_exact(max_short, world):
     (4, 256, "tree", "1", "", ""), (5, 64, "tree", "", "", ""),
     (8, 256, "", "", "4", ""), (12, 100, "", "", "3", ""), (8, 256, "tree", "1", "8:4", ""),
     (12, 100, "", "", "3", "y"), (8, 256, "", "", "", "zcopy"),
-    (12, 256, "", "", "3", "zcopy"), (6, 256, "tree", "", "", "zcopy")])
+    (12, 256, "", "", "3", "zcopy"), (6, 256, "tree", "", "", "zcopy"),
+    (8, 256, "", "", "", "zcopy-reg"), (12, 256, "", "", "3", "zcopy-reg")])
 def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast, place,
                                     pipe):
     """The host engine (libucg_builtin.so sources) and the C1 harness rebuilt
@@ -69,8 +70,10 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
         monkeypatch.setenv("UCX_BUILTIN_ALLREDUCE_PLAN", plan)
     if incast:
         monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", incast)
-    if pipe == "zcopy":
+    if pipe.startswith("zcopy"):
         monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", "1")
+        if pipe == "zcopy-reg":
+            monkeypatch.setenv("C1_REGISTERED", "1")
     elif pipe:
         monkeypatch.setenv("UCX_BUILTIN_PIPELINE", pipe)
     if place:

@@ -191,6 +191,36 @@ def test_engine_placements_shm_zcopy(spec, monkeypatch):
         assert all(x == d[0] for x in d), d
 
 
+@pytest.mark.parametrize("spec", ["8:4:0:8:2:16", "12:3:0:2:2:16", "6:2:0:8:2:16",
+                                  "16:4:0:8:4:16", "8:8:4:8:2:4"])
+def test_engine_registered_send_buffers_shm(spec, monkeypatch):
+    """Send buffers from the group's registered memory
+    (ucg_builtin_lgroup_mem_alloc) are exposed in place by the remote-key
+    steps instead of being copied into the op's buffer first: same plans,
+    same bits, the describe line says so."""
+    n = int(spec.split(":")[0])
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    monkeypatch.setenv("TOPO_REGISTERED", "1")
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "shm", 256, spec),
+                         timeout=240)
+    assert codes == [0] * n, "\n".join(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("spec,oneshot", [("8:8:0:8:2:16", "y"), ("4:4:0:8:2:16", "n"),
+                                          ("6:6:0:8:2:16", "y"), ("12:3:0:2:2:16", "y")])
+def test_engine_registered_send_buffers_device(spec, oneshot, monkeypatch):
+    """Registered device send buffers exposed in place (no init copy), through
+    the one-shot execution, the recursive steps, the tree and waypoints."""
+    n = int(spec.split(":")[0])
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
+    monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT", oneshot)
+    monkeypatch.setenv("TOPO_REGISTERED", "1")
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
+                         timeout=150)
+    assert codes == [0] * n, "\n".join(outs)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec,oneshot", [
     ("4:4:0:8:2:16", "y"), ("8:8:0:8:2:16", "y"), ("2:2:0:8:2:16", "y"),

@@ -251,11 +251,15 @@ struct ucg_builtin_lcoll {
                                      reduce's root */
     void        *dbuf[2];         /* this member's exposed device buffers */
     int          pool_idx[2];     /* their entries in the group's pool */
-    uint8_t      key[2][UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+    uint8_t      key[3][UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
+    int          exp_sbuf;        /* send.buffer is registered group memory
+                                     (ucg_builtin_lgroup_mem_alloc): exposed in
+                                     place as buffer 2, no init copy */
     int          keys_sent;       /* the keys go out on the first start only */
-    unsigned     cur_buf;         /* the dbuf holding this member's data */
-    unsigned     readers[2];      /* peers still reading each dbuf */
-    void        *peer_buf[UCG_BUILTIN_OPS_MAX_MEMBERS][2];
+    unsigned     cur_buf;         /* the buffer holding this member's data:
+                                     dbuf 0 / 1, or 2 = send.buffer */
+    unsigned     readers[3];      /* peers still reading each buffer */
+    void        *peer_buf[UCG_BUILTIN_OPS_MAX_MEMBERS][3];
     unsigned     rdy_cnt[OPS_MAX_STEPS];   /* READY messages per step ... */
     uint8_t      rdy_peer[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
     uint8_t      rdy_buf[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];

@@ -942,6 +942,9 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             PUT("Executed as: one-shot reduce-scatter (every shard of the plan's "
                 "association read from all members) + all-gather\n");
         }
+        if (c->exp_sbuf) {
+            PUT("Send buffer: registered group memory, exposed in place\n");
+        }
     }
     for (k = 0; k < c->nsteps; k++) {
         const op_step_t *s = &c->steps[k];

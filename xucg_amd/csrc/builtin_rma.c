@@ -49,6 +49,7 @@ struct rma_pool {
     size_t   bytes;
     int      kind;
     int      busy;
+    int      user;            /* handed out by ucg_builtin_lgroup_mem_alloc */
     uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
 };
 
@@ -154,6 +155,7 @@ static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
     p->bytes = bytes;
     p->kind  = kind;
     p->busy  = 1;
+    p->user  = 0;
     if (kind == RMA_SHM) {
         p->ptr = shm_seg_alloc(bytes, p->key);
         return p->ptr ? (int)g->npool++ : -1;
@@ -273,6 +275,12 @@ static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *cons
     return st;
 }
 
+/* buffer b of this member: dbuf 0 / 1, or 2 = the registered send.buffer */
+static void *rma_local(const ucg_builtin_lcoll_t *c, unsigned b)
+{
+    return b == 2 ? (void*)c->sbuf : c->dbuf[b];
+}
+
 static ucs_status_t rma_copy(ucg_builtin_lcoll_t *c, void *dst, const void *src)
 {
     if (c->rma == RMA_DEV) {
@@ -364,7 +372,11 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
     if (c->rdy_cnt[k] < s->recv_cnt) {
         return 0;
     }
-    out = c->readers[c->cur_buf] ? !c->cur_buf : c->cur_buf;
+    if (c->cur_buf == 2) {
+        out = c->readers[0] ? 1 : 0;      /* never written: the caller's send buffer */
+    } else {
+        out = c->readers[c->cur_buf] ? !c->cur_buf : c->cur_buf;
+    }
     if (!direct && c->readers[out]) {
         return 0;
     }
@@ -377,7 +389,7 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
         }
     }
     if (s->aggregation == AGG_REDUCE) {
-        srcs[0] = c->dbuf[c->cur_buf];
+        srcs[0] = rma_local(c, c->cur_buf);
         st = rma_fold(c, dst, srcs, 1 + s->recv_cnt);
     } else {
         st = (s->recv_cnt == 1) ? rma_copy(c, dst, srcs[1]) : UCS_ERR_IO_ERROR;
@@ -426,15 +438,23 @@ static void oneshot_shard(const ucg_builtin_lcoll_t *c, unsigned r, size_t *lo, 
     *n  = (*lo + se < cnt ? *lo + se : cnt) - *lo;
 }
 
+/* phase 0 exposes this member's data (dbuf 0, or the registered send
+ * buffer), phase 1 its reduced shard in dbuf 1 */
+static unsigned oneshot_buf(const ucg_builtin_lcoll_t *c, unsigned phase)
+{
+    return phase ? 1 : (c->exp_sbuf ? 2 : 0);
+}
+
 static void oneshot_expose(ucg_builtin_lcoll_t *c, unsigned phase)
 {
+    const unsigned b = oneshot_buf(c, phase);
     unsigned p;
     for (p = 0; p < c->g->size; p++) {
         if (p != c->g->my) {
-            rma_post(c, p, (uint8_t)(phase + 1), phase, NULL, 0);
+            rma_post(c, p, (uint8_t)(phase + 1), b, NULL, 0);
         }
     }
-    c->readers[phase] += c->g->size - 1;
+    c->readers[b] += c->g->size - 1;
 }
 
 /* the phase's kernel once every peer's READY is in; DONE to all */
@@ -442,16 +462,20 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
 {
     const unsigned N = c->g->size, my = c->g->my;
     const void *srcs[16];
+    const void *peer[16];               /* each member's exposed buffer */
     void *dsts[16];
     ucs_status_t st = UCS_OK;
     size_t lo, n, full_lo, full_n;
-    unsigned r, k;
+    unsigned r, k, i;
 
     if (c->rdy_cnt[phase] < N - 1) {
         return 0;
     }
-    for (r = 0; r < N; r++) {
-        if (r != my && c->peer_buf[r][phase] == NULL) {
+    peer[my] = rma_local(c, oneshot_buf(c, phase));
+    for (i = 0; i < N - 1; i++) {
+        r = c->rdy_peer[phase][i];
+        peer[r] = c->peer_buf[r][c->rdy_buf[phase][i]];
+        if (peer[r] == NULL) {
             finish(c, UCS_ERR_IO_ERROR);          /* a READY without a key */
             return 0;
         }
@@ -459,7 +483,7 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
     if (phase == 0) {
         oneshot_shard(c, my, &lo, &n);
         for (r = 0; r < N; r++) {
-            srcs[r] = (const char*)(r == my ? c->dbuf[0] : c->peer_buf[r][0]) + lo * c->dt_len;
+            srcs[r] = (const char*)peer[r] + lo * c->dt_len;
         }
         st = ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype,
                                                (char*)c->dbuf[1] + lo * c->dt_len, srcs, N,
@@ -472,7 +496,7 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
             if (n == 0) {
                 continue;
             }
-            srcs[k] = (const char*)(r == my ? c->dbuf[1] : c->peer_buf[r][1]) + lo * c->dt_len;
+            srcs[k] = (const char*)peer[r] + lo * c->dt_len;
             dsts[k] = c->rbuf_user + lo * c->dt_len;
             if (n != full_n) {
                 st = ucg_builtin_combine_dev_copy_n(c->g->cmb, &dsts[k], &srcs[k], 1,
@@ -490,10 +514,8 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
         finish(c, st);
         return 0;
     }
-    for (r = 0; r < N; r++) {
-        if (r != my) {
-            rma_post(c, r, RMA_DONE, phase, NULL, 0);
-        }
+    for (i = 0; i < N - 1; i++) {
+        rma_post(c, c->rdy_peer[phase][i], RMA_DONE, c->rdy_buf[phase][i], NULL, 0);
     }
     return 1;
 }
@@ -550,7 +572,7 @@ UCG_INTERNAL void rma_advance(ucg_builtin_lcoll_t *c)
         }
         if (!c->done && c->cur == c->nsteps && !c->rma_final) {
             ucs_status_t st = c->rbuf_user ?
-                rma_copy(c, c->rbuf_user, c->dbuf[c->cur_buf]) : UCS_OK;
+                rma_copy(c, c->rbuf_user, rma_local(c, c->cur_buf)) : UCS_OK;
             if (st != UCS_OK) {
                 finish(c, st);
             }
@@ -558,7 +580,7 @@ UCG_INTERNAL void rma_advance(ucg_builtin_lcoll_t *c)
         }
         rma_flush(c);
         if (!c->done && c->rma_final && c->out_tail == 0 &&
-            c->readers[0] == 0 && c->readers[1] == 0) {
+            c->readers[0] == 0 && c->readers[1] == 0 && c->readers[2] == 0) {
             finish(c, UCS_OK);
         }
     } while (c->rma_again && !c->done);
@@ -579,7 +601,7 @@ UCG_INTERNAL void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *da
         return;
     }
     memcpy(w, data, 8);
-    if (w[0] >= c->g->size || w[0] == c->g->my || w[1] > 1) {
+    if (w[0] >= c->g->size || w[0] == c->g->my || w[1] > 2) {
         finish(c, UCS_ERR_IO_ERROR);   /* e.g. a member that took the host path */
         return;
     }
@@ -605,8 +627,8 @@ UCG_INTERNAL void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *da
         }
         c->readers[w[1]]--;
     } else if (c->oneshot) {
-        k = h.step_idx - 1u;              /* phases 0 and 1 */
-        if (k > 1 || w[1] != k || c->rdy_cnt[k] == c->g->size - 1) {
+        k = h.step_idx - 1u;              /* phases 0 (buffer 0 or 2) and 1 */
+        if (k > 1 || (w[1] == 1) != (k == 1) || c->rdy_cnt[k] == c->g->size - 1) {
             finish(c, UCS_ERR_IO_ERROR);
             return;
         }
@@ -653,6 +675,20 @@ UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
         c->dbuf[i]     = c->g->pool[k].ptr;
         memcpy(c->key[i], c->g->pool[k].key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
     }
+    /* a send buffer the caller took from the group's registered memory is
+     * exposed where it is (the zcopy send of a registered buffer,
+     * builtin_control.c:276-286, 943-949); in place it is written at the end,
+     * so it is copied as any other */
+    c->exp_sbuf = 0;
+    for (i = 0; c->sbuf && c->sbuf != c->rbuf_user && i < c->g->npool; i++) {
+        const struct rma_pool *p = &c->g->pool[i];
+        if (p->user && p->kind == c->rma && p->ptr == (const void*)c->sbuf &&
+            p->bytes >= c->length) {
+            c->exp_sbuf = 1;
+            memcpy(c->key[2], p->key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+            break;
+        }
+    }
     return UCS_OK;
 }
 
@@ -665,7 +701,7 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     c->cur       = 0;
     c->cur_buf   = 0;
     c->rma_sent  = c->rma_recvd = c->rma_final = 0;
-    c->readers[0] = c->readers[1] = 0;
+    c->readers[0] = c->readers[1] = c->readers[2] = 0;
     c->out_head  = c->out_tail = 0;
     c->send_pending = 0;
     memset(c->rdy_cnt, 0, sizeof(c->rdy_cnt));
@@ -676,8 +712,10 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
         return UCS_OK;
     }
     /* ucg_builtin_init_reduce (builtin_control.c:43-47): this member's data
-     * into its first buffer - every member, since every member exposes it */
-    st = rma_copy(c, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf);
+     * into its first buffer - every member, since every member exposes it -
+     * unless the send buffer is registered and exposed in place */
+    c->cur_buf = c->exp_sbuf ? 2 : 0;
+    st = c->exp_sbuf ? UCS_OK : rma_copy(c, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf);
     if (st != UCS_OK) {
         c->done   = 1;
         c->status = st;
@@ -703,6 +741,10 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
                     sent[p] = 1;
                     rma_post(c, p, RMA_RKEY, 0, c->key[0], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
                     rma_post(c, p, RMA_RKEY, 1, c->key[1], UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+                    if (c->exp_sbuf) {
+                        rma_post(c, p, RMA_RKEY, 2, c->key[2],
+                                 UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+                    }
                 }
             }
         }
@@ -740,4 +782,33 @@ UCG_INTERNAL void rma_free(ucg_builtin_lcoll_t *c)
         }
     }
     free(c->outbox);
+}
+
+/* ---- registered group memory ------------------------------------------- */
+void *ucg_builtin_lgroup_mem_alloc(ucg_builtin_lgroup_t *g, size_t bytes, int on_device)
+{
+    const int kind = on_device ? RMA_DEV : RMA_SHM;
+    int k;
+    if (g == NULL || bytes == 0 ||
+        (on_device && !ucg_builtin_combine_has_device(g->cmb))) {
+        return NULL;
+    }
+    k = rma_pool_get(g, bytes, kind);
+    if (k < 0) {
+        return NULL;
+    }
+    g->pool[k].user = 1;
+    return g->pool[k].ptr;
+}
+
+void ucg_builtin_lgroup_mem_free(ucg_builtin_lgroup_t *g, void *ptr)
+{
+    unsigned i;
+    for (i = 0; g && ptr && i < g->npool; i++) {
+        if (g->pool[i].user && g->pool[i].ptr == ptr) {
+            g->pool[i].user = 0;      /* back to the pool: the memory and its key */
+            g->pool[i].busy = 0;      /* stay valid until the group is destroyed */
+            return;
+        }
+    }
 }

@@ -89,6 +89,8 @@ HOST_API = {
     "ucg_builtin_lgroup_destroy": (None, [_vp]),
     "ucg_builtin_lgroup_progress": (_u, [_vp]),
     "ucg_builtin_lgroup_stats": (None, [_vp, ctypes.POINTER(_u64)]),
+    "ucg_builtin_lgroup_mem_alloc": (_vp, [_vp, _sz, _int]),
+    "ucg_builtin_lgroup_mem_free": (None, [_vp, _vp]),
     "ucg_builtin_lcoll_allreduce": (_int, [_vp, _vp, _vp, _int, _vp, _vp,
                                            ctypes.POINTER(_vp)]),
     "ucg_builtin_lcoll_reduce": (_int, [_vp, _vp, _vp, _int, _vp, _vp, _u,

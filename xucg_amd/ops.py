@@ -82,6 +82,17 @@ class Group:
         _lib.host().ucg_builtin_lgroup_stats(self.handle, out)
         return {"sent": out[0], "direct": out[1], "stashed": out[2], "resends": out[3]}
 
+    def mem_alloc(self, nbytes, device=True):
+        """registered group memory (an address): an op's send buffer taken
+        from here is exposed in place by remote-key steps"""
+        p = _lib.host().ucg_builtin_lgroup_mem_alloc(self.handle, nbytes, int(device))
+        if not p:
+            raise MemoryError(f"ucg_builtin_lgroup_mem_alloc({nbytes}, {device}) failed")
+        return p
+
+    def mem_free(self, ptr):
+        _lib.host().ucg_builtin_lgroup_mem_free(self.handle, ptr)
+
     def allreduce(self, sbuf, rbuf, count, dtype, op):
         return Allreduce(self, sbuf, rbuf, count, dtype, op)
 
