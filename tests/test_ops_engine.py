@@ -29,6 +29,20 @@ def test_allreduce_multiprocess_host(world, max_short, cells):
         print(outs[0])
 
 
+@pytest.mark.parametrize("world,cells", [(4, 64), (8, 64), (2, 64), (4, 3)])
+def test_allreduce_multiprocess_shm_zcopy(world, cells, monkeypatch):
+    """The same worker with every message on the shared-memory remote-key
+    steps (UCX_BUILTIN_SHM_ZCOPY_THRESH=1): every dtype/op case, a persistent
+    op restarted, the empty op, two ops in flight at once on one group (each
+    with its own registered buffers, messages told apart by coll_id), and a
+    3-cell ring whose control messages meet UCS_ERR_NO_RESOURCE."""
+    monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", "1")
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    codes, outs = launch("_worker_ops.py", world,
+                         args=(shm_name(), "host", 256, 100, cells), timeout=240)
+    assert codes == [0] * world, "\n".join(outs)
+
+
 @pytest.mark.parametrize("max_short,world", [(256, 4), (8192, 4), (256, 3)])
 def test_c1_harness_bit_exact(max_short, world):
     """BASELINE config 1 from plain C: 4 processes, 4 KiB fp32 SUM (and the
