@@ -29,9 +29,11 @@
  * builtin_data.c:326-340), after which the reader answers DONE so the sender
  * may write that buffer again. Two buffers per member alternate, so a member
  * never waits for readers of the data it is combining into: step k reads
- * dbuf[cur] and writes dbuf[!cur] unless nobody reads dbuf[cur]. The
- * association is the host path's: the accumulator first, then the peers in
- * the order their READYs arrived (builtin_comp_step.inl:213-221). */
+ * dbuf[cur] and writes dbuf[!cur] unless nobody reads dbuf[cur]. A send
+ * buffer from the group's registered memory is a third, read-only buffer
+ * (index 2) exposed in place of the init copy. The association is the host
+ * path's: the accumulator first, then the peers in the order their READYs
+ * arrived (builtin_comp_step.inl:213-221). */
 #define RMA_DONE 0x40   /* payload {from, buf}: done reading your dbuf[buf] */
 #define RMA_RKEY 0x80   /* payload {from, buf, handle}: the key of my dbuf[buf] */
 #define RMA_MIN_SHORT (8 + 8 + UCG_BUILTIN_DEV_IPC_HANDLE_BYTES)
