@@ -271,3 +271,34 @@ def test_engine_fuzz(seed, world, max_short, cells, env, monkeypatch):
     codes, outs = launch("_worker_fuzz.py", world, args=(shm_name(), seed, max_short, cells),
                          timeout=300)
     assert codes == [0] * world, "\n".join(outs)
+
+
+ZC_FUZZ = [(11, 2, 256, 64), (12, 3, 256, 3), (13, 4, 128, 8), (14, 5, 256, 64),
+           (15, 8, 256, 4), (16, 6, 1024, 64)]
+
+
+@pytest.mark.parametrize("where", ["shm", "shm-reg"])
+@pytest.mark.parametrize("seed,world,max_short,cells", ZC_FUZZ)
+def test_engine_fuzz_shm_zcopy(seed, world, max_short, cells, where, monkeypatch):
+    """The seeded 40-op sequence on the shared-memory remote-key steps: random
+    integer dtype/op or exact fp SUM, count 0-6000, allreduce or reduce to a
+    random root, in place or not, rings of 3-64 cells; with send buffers from
+    the group's registered memory in the -reg runs."""
+    monkeypatch.setenv("FUZZ_BUFFERS", where)
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    codes, outs = launch("_worker_fuzz.py", world, args=(shm_name(), seed, max_short, cells),
+                         timeout=300)
+    assert codes == [0] * world, "\n".join(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("where", ["device", "device-reg"])
+@pytest.mark.parametrize("seed,world,max_short,cells", ZC_FUZZ)
+def test_engine_fuzz_device_buffers(seed, world, max_short, cells, where, monkeypatch):
+    """The same sequence on device buffers: the remote-key steps, the one-shot
+    execution (4 and 8 members), registered send buffers, in place or not."""
+    monkeypatch.setenv("FUZZ_BUFFERS", where)
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
+    codes, outs = launch("_worker_fuzz.py", world, args=(shm_name(), seed, max_short, cells),
+                         timeout=150)
+    assert codes == [0] * world, "\n".join(outs)
