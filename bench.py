@@ -111,27 +111,35 @@ def c1_loopback(ranks=4, iters=20000):
     (tests/c/c1_allreduce.c; host combine, no GPU). Latency per allreduce.
     max_short_*: the reference's plan for 4 members (recursive doubling);
     tree_*: the tree plan forced on 4 members, plain and with the SM-root
-    incast packers; tree_3_ranks: the non-power-of-two case."""
+    incast packers; tree_3_ranks: the non-power-of-two case; device_*: the
+    same harness on device buffers (remote-key steps, the one-shot execution
+    at 4 members) with the send buffer in the group's registered memory, at
+    4 KiB and 64 MiB."""
     import subprocess
     import uuid
     exe = os.path.join(ROOT, "tests", "c", "_build", "c1_allreduce")
+    dev = {"C1_DEVICE_BUFFERS": "1", "C1_REGISTERED": "1", "UCX_BUILTIN_WAIT_TIMEOUT": "60"}
     variants = [("max_short_256", ranks, 256, {}), ("max_short_8192", ranks, 8192, {}),
                 ("tree_max_short_256", ranks, 256, {"UCX_BUILTIN_ALLREDUCE_PLAN": "tree"}),
                 ("tree_incast_max_short_256", ranks, 256,
                  {"UCX_BUILTIN_ALLREDUCE_PLAN": "tree", "UCX_BUILTIN_SM_INCAST": "y"}),
-                ("tree_3_ranks_max_short_256", 3, 256, {})]
+                ("tree_3_ranks_max_short_256", 3, 256, {}),
+                ("device_buffers_4kib", ranks, 256, dev, 1024, 2000),
+                ("device_buffers_64mib", ranks, 256, dev, 1 << 24, 20)]
     # one core per rank, as an MPI launcher binds them: the lowest-numbered
     # allowed CPUs (neighbours on one CCD on EPYC); unpinned ranks land on
     # random cores and the latency moves by 2x between runs
     allowed = sorted(os.sched_getaffinity(0))
     res = {"cpus": allowed[:max(v[1] for v in variants)]}
-    for key, world, max_short, extra_env in variants:
+    for key, world, max_short, extra_env, *size in variants:
         name = f"ucg_bench_c1_{os.getpid()}_{uuid.uuid4().hex[:6]}"
+        count, n_iter = size if size else (1024, iters)
         procs = []
         for r in range(world):
             env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), **extra_env)
             cpu = allowed[r % len(allowed)]
-            procs.append(subprocess.Popen([exe, name, str(iters), str(max_short)], env=env,
+            procs.append(subprocess.Popen([exe, name, str(n_iter), str(max_short), str(count)],
+                                          env=env,
                                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                           text=True,
                                           preexec_fn=lambda c=cpu: os.sched_setaffinity(0, {c})))
