@@ -206,15 +206,22 @@ def test_engine_registered_send_buffers_shm(spec, monkeypatch):
     assert codes == [0] * n, "\n".join(outs)
 
 
+def _oneshot_env(monkeypatch, oneshot):
+    monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT", "n" if oneshot == "n" else "y")
+    if oneshot == "split":
+        monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL", "0")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec,oneshot", [("8:8:0:8:2:16", "y"), ("4:4:0:8:2:16", "n"),
+                                          ("8:8:0:8:2:16", "split"),
                                           ("6:6:0:8:2:16", "y"), ("12:3:0:2:2:16", "y")])
 def test_engine_registered_send_buffers_device(spec, oneshot, monkeypatch):
     """Registered device send buffers exposed in place (no init copy), through
     the one-shot execution, the recursive steps, the tree and waypoints."""
     n = int(spec.split(":")[0])
     monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
-    monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT", oneshot)
+    _oneshot_env(monkeypatch, oneshot)
     monkeypatch.setenv("TOPO_REGISTERED", "1")
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)
@@ -224,7 +231,8 @@ def test_engine_registered_send_buffers_device(spec, oneshot, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("spec,oneshot", [
     ("4:4:0:8:2:16", "y"), ("8:8:0:8:2:16", "y"), ("2:2:0:8:2:16", "y"),
-    ("4:4:0:8:2:16", "n"), ("8:8:0:8:2:16", "n"), ("6:6:0:8:2:16", "y"),
+    ("4:4:0:8:2:16", "n"), ("8:8:0:8:2:16", "n"), ("4:4:0:8:2:16", "split"),
+    ("8:8:0:8:2:16", "split"), ("6:6:0:8:2:16", "y"),
     ("12:3:0:2:2:16", "y"), ("8:8:4:8:2:4", "y"), ("8:2:0:8:4:16", "y"),
     ("5:1:0:2:2:16", "y")])
 def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
@@ -234,17 +242,20 @@ def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     of the inter-host tree and of the socket level, K-ing with K = 4, a
     three-level tree - each member's plan equal to the oracle's and every
     result bit-exact against its simulation, twice per persistent op. Plain
-    recursive doubling runs as the one-shot reduce-scatter + all-gather
-    unless UCX_BUILTIN_DEVICE_ONESHOT=n: the same bits either way."""
+    recursive doubling runs one-shot unless UCX_BUILTIN_DEVICE_ONESHOT=n -
+    these small messages as one pass over all members' data, "split" (the
+    single-pass limit at 0) as reduce-scatter + all-gather: the same bits
+    every way."""
     n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
     monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")   # a lost message fails fast
-    monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT", oneshot)
+    _oneshot_env(monkeypatch, oneshot)
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)
     assert codes == [0] * n, "\n".join(outs)
     flat_doubling = spec.split(":")[1] == spec.split(":")[0] and factor == 2 and \
         (n & (n - 1)) == 0 and 4 <= n <= 16
-    assert ("Executed as: one-shot" in outs[0]) == (flat_doubling and oneshot == "y")
+    assert ("Executed as: one-shot" in outs[0]) == (flat_doubling and oneshot != "n")
+    assert ("one-shot reduce-scatter" in outs[0]) == (flat_doubling and oneshot == "split")
     if factor == 2:
         d = _digests(outs)
         assert all(x == d[0] for x in d), d

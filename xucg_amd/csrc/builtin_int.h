@@ -266,7 +266,9 @@ struct ucg_builtin_lcoll {
                                   /* ... in arrival order: the fold order */
     int          rma_sent, rma_recvd, rma_final, rma_busy, rma_again;
     int          oneshot;         /* recursive doubling run as one-shot
-                                     reduce-scatter + all-gather */
+                                     reduce-scatter + all-gather (1), or - a
+                                     small message - one pass of every member
+                                     over all the data (2) */
     /* ucg_params_t.completion (api/ucg.h:162-171) */
     int          comp_set;
     ucg_builtin_coll_comp_cb_f comp_cb;

@@ -938,9 +938,12 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             "senders' buffers in one kernel\n" :
             "Buffers: shared memory; remote keys once per op, every step reads its "
             "senders' buffers in place\n");
-        if (c->oneshot) {
+        if (c->oneshot == 1) {
             PUT("Executed as: one-shot reduce-scatter (every shard of the plan's "
                 "association read from all members) + all-gather\n");
+        } else if (c->oneshot == 2) {
+            PUT("Executed as: one-shot, every member evaluating the plan's association "
+                "over all members' data\n");
         }
         if (c->exp_sbuf) {
             PUT("Send buffer: registered group memory, exposed in place\n");

@@ -428,6 +428,15 @@ static int oneshot_enabled(void)
     return !(e && (e[0] == 'n' || e[0] == 'N' || e[0] == '0'));
 }
 
+/* messages up to this size skip the all-gather: every member evaluates the
+ * whole of V(self) from all N buffers in one kernel, straight into
+ * recv.buffer (N x the reads, one launch and one wait less) */
+static size_t oneshot_full_bytes(void)
+{
+    const char *e = getenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL");
+    return (e && *e) ? (size_t)strtoull(e, NULL, 0) : ((size_t)1 << 20);
+}
+
 /* shard r of the op: [r * se, min(count, (r + 1) * se)) elements, se a
  * multiple of 256 bytes so shards start on 256-B boundaries */
 static void oneshot_shard(const ucg_builtin_lcoll_t *c, unsigned r, size_t *lo, size_t *n)
@@ -482,7 +491,13 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
             return 0;
         }
     }
-    if (phase == 0) {
+    if (phase == 0 && c->oneshot == 2) {
+        for (r = 0; r < N; r++) {
+            srcs[r] = peer[r];
+        }
+        st = ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype, c->rbuf_user,
+                                               srcs, N, my, (size_t)c->count);
+    } else if (phase == 0) {
         oneshot_shard(c, my, &lo, &n);
         for (r = 0; r < N; r++) {
             srcs[r] = (const char*)peer[r] + lo * c->dt_len;
@@ -524,7 +539,8 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
 
 static void oneshot_advance(ucg_builtin_lcoll_t *c)
 {
-    while (!c->done && c->cur < 2) {
+    const unsigned phases = c->oneshot == 2 ? 1 : 2;
+    while (!c->done && c->cur < phases) {
         if (!c->rma_sent) {
             oneshot_expose(c, c->cur);
             c->rma_sent = 1;
@@ -668,6 +684,9 @@ UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
     c->oneshot   = c->rma == RMA_DEV && c->kind == 0 && oneshot_enabled() &&
                    c->g->size >= 4 && c->g->size <= 16 && c->plan &&
                    strcmp(c->plan, "recursive doubling") == 0;
+    if (c->oneshot && c->length <= oneshot_full_bytes()) {
+        c->oneshot = 2;
+    }
     for (i = 0; i < 2; i++) {
         int k = rma_pool_get(c->g, c->length ? c->length : 1, c->rma);
         if (k < 0) {
