@@ -302,3 +302,25 @@ def test_engine_fuzz_device_buffers(seed, world, max_short, cells, where, monkey
     codes, outs = launch("_worker_fuzz.py", world, args=(shm_name(), seed, max_short, cells),
                          timeout=150)
     assert codes == [0] * world, "\n".join(outs)
+
+
+@pytest.mark.parametrize("thresh,shm", [("8k", True), ("8192", True), ("9k", False),
+                                        ("0.5m", False), ("", False)])
+def test_shm_zcopy_thresh_memunits(thresh, shm, monkeypatch):
+    """UCX_BUILTIN_SHM_ZCOPY_THRESH takes UCX memunits like the other size
+    knobs (k/m/g suffixes, empty = off): an 8 KiB host op takes the
+    shared-memory remote-key steps from 8k down, not from 9k up."""
+    monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", thresh)
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    iface = ops.ShmIface(shm_name(), 1, 0, max_short=256)
+    g = ops.Group(iface, 3, 1, 0, cmb)
+    x = np.arange(2048, dtype=np.int32)
+    y = np.zeros_like(x)
+    c = g.allreduce(x, y, 2048, DTYPES["int32"], OPS["sum"])
+    assert c.status == 0 and c.run() == 0 and (y == x).all()
+    assert ("Buffers: shared memory" in c.describe()) == shm, c.describe()
+    c.close()
+    g.close()
+    iface.close()
+    cmb.close()

@@ -45,7 +45,10 @@ struct ucg_builtin_combine {
 /* ------------------------------------------------------------------------ */
 /* configuration                                                            */
 /* ------------------------------------------------------------------------ */
-static size_t parse_memunits(const char *s, size_t dflt)
+/* a size with an optional k/m/g suffix (UCX memunits), dflt when unset or
+ * unparsable; shared with the remote-key knobs (builtin_int.h) */
+__attribute__((visibility("hidden"))) size_t parse_memunits(const char *s, size_t dflt);
+__attribute__((visibility("hidden"))) size_t parse_memunits(const char *s, size_t dflt)
 {
     char *end;
     double v;

@@ -299,6 +299,7 @@ enum {
 #define RMA_SHM 2       /* host buffers: POSIX shared memory keys, reduce_cb_f */
 
 /* builtin_ops.c */
+UCG_INTERNAL size_t parse_memunits(const char *s, size_t dflt);   /* builtin_combine.c */
 UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status);
 UCG_INTERNAL void lcoll_notify(ucg_builtin_lcoll_t *c);
 

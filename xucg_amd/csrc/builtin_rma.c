@@ -234,8 +234,7 @@ UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
  * knob - the reference hard-codes 100000, builtin_control.c:474) */
 static size_t shm_zcopy_thresh(void)
 {
-    const char *e = getenv("UCX_BUILTIN_SHM_ZCOPY_THRESH");
-    return (e && *e) ? (size_t)strtoull(e, NULL, 0) : 0;
+    return parse_memunits(getenv("UCX_BUILTIN_SHM_ZCOPY_THRESH"), 0);
 }
 
 /* the op's buffers decide: device memory (both, or the one given) ->
@@ -433,8 +432,7 @@ static int oneshot_enabled(void)
  * recv.buffer (N x the reads, one launch and one wait less) */
 static size_t oneshot_full_bytes(void)
 {
-    const char *e = getenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL");
-    return (e && *e) ? (size_t)strtoull(e, NULL, 0) : ((size_t)1 << 20);
+    return parse_memunits(getenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL"), (size_t)1 << 20);
 }
 
 /* shard r of the op: [r * se, min(count, (r + 1) * se)) elements, se a
