@@ -324,3 +324,34 @@ def test_shm_zcopy_thresh_memunits(thresh, shm, monkeypatch):
     g.close()
     iface.close()
     cmb.close()
+
+
+def test_rma_pool_size_classes(monkeypatch):
+    """Ops of many different sizes share the group's registered buffers:
+    the pool grows by size class (eight per power of two, at most twice the
+    class per reuse), not by every distinct message size, since a buffer is
+    only returned when the group is destroyed. 300 shared-memory remote-key
+    ops of random sizes in [64 KiB, 1 MiB] leave at most 2 x 8 x 4 segments."""
+    import glob
+    import os
+    monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", "1")
+    mpi = MockMPI()
+    cmb = host.BuiltinCombine(mpi.callbacks(), host.make_config(dev_enable=0))
+    iface = ops.ShmIface(shm_name(), 1, 0, max_short=256)
+    g = ops.Group(iface, 3, 1, 0, cmb)
+    rng = np.random.default_rng(7)
+    segs = lambda: glob.glob(f"/dev/shm/xucg_rma_{os.getpid()}_*")
+    before = len(segs())
+    for n in rng.integers(1 << 16, 1 << 20, 300):
+        x = rng.integers(0, 255, int(n), dtype=np.uint8)
+        y = np.zeros_like(x)
+        c = g.allreduce(x, y, int(n), DTYPES["uint8"], OPS["sum"])
+        assert c.status == 0 and c.run() == 0 and (y == x).all()
+        assert "Buffers: shared memory" in c.describe()
+        c.close()
+    grown = len(segs()) - before
+    assert 2 <= grown <= 64, grown
+    g.close()
+    assert len(segs()) == before
+    iface.close()
+    cmb.close()

@@ -111,6 +111,7 @@ static void *shm_seg_alloc(size_t bytes, void *key)
 static ucs_status_t shm_seg_import(const void *key, void **ptr)
 {
     shm_key_t k;
+    struct stat sb;
     void *p;
     int fd;
     memcpy(&k, key, sizeof(k));
@@ -120,6 +121,11 @@ static ucs_status_t shm_seg_import(const void *key, void **ptr)
     fd = shm_open(k.name, O_RDWR, 0);
     if (fd < 0) {
         return UCS_ERR_IO_ERROR;
+    }
+    /* a key that claims more than the segment holds would fault on access */
+    if (fstat(fd, &sb) != 0 || (uint64_t)sb.st_size < k.bytes || k.bytes == 0) {
+        close(fd);
+        return UCS_ERR_INVALID_PARAM;
     }
     p = mmap(NULL, k.bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
@@ -137,17 +143,41 @@ static size_t shm_key_bytes(const void *key)
     return (size_t)k.bytes;
 }
 
-/* a free registered buffer of exactly `bytes`, or a new one */
+/* registered buffers come in size classes - at least 64 KiB, eight per
+ * power of two (at most 12.5 % over the request) - so that ops of many
+ * different sizes share buffers: pool memory is never returned before the
+ * group is destroyed (peers keep their mappings, keyed by the buffer's key) */
+static size_t rma_pool_class(size_t bytes)
+{
+    size_t c = bytes < ((size_t)64 << 10) ? ((size_t)64 << 10) : bytes, step;
+    unsigned lg = 0;
+    while (((size_t)2 << lg) <= c) {
+        lg++;
+    }
+    step = (size_t)1 << (lg - 3);
+    return (c + step - 1) / step * step;
+}
+
+/* the smallest free registered buffer that holds `bytes` and is less than
+ * twice its class, or a new one of the class */
 static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
 {
+    const size_t cls = rma_pool_class(bytes);
     struct rma_pool *p;
     unsigned i;
+    int best = -1;
     for (i = 0; i < g->npool; i++) {
-        if (!g->pool[i].busy && g->pool[i].bytes == bytes && g->pool[i].kind == kind) {
-            g->pool[i].busy = 1;
-            return (int)i;
+        if (!g->pool[i].busy && g->pool[i].kind == kind && g->pool[i].bytes >= cls &&
+            g->pool[i].bytes < 2 * cls &&
+            (best < 0 || g->pool[i].bytes < g->pool[best].bytes)) {
+            best = (int)i;
         }
     }
+    if (best >= 0) {
+        g->pool[best].busy = 1;
+        return best;
+    }
+    bytes = cls;
     p = realloc(g->pool, (g->npool + 1) * sizeof(*p));
     if (p == NULL) {
         return -1;
