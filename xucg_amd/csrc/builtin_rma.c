@@ -449,8 +449,10 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
  * exposes its data and computes its 1/N shard of V with one kernel reading
  * that shard from all N buffers (ucg_builtin_dev_reduce_multi); (1) every
  * member exposes its reduced shard and copies all N shards into recv.buffer.
- * Same bits as the steps; UCX_BUILTIN_DEVICE_ONESHOT=n runs the steps. From
- * 4 to 16 members (reduce_multi's operand limit). */
+ * A small message (oneshot 2) skips phase 1: phase 0 reads all of every
+ * member's buffer and writes the whole of V into recv.buffer. Same bits as
+ * the steps; UCX_BUILTIN_DEVICE_ONESHOT=n runs the steps. From 4 to 16
+ * members (reduce_multi's operand limit). */
 static int oneshot_enabled(void)
 {
     const char *e = getenv("UCX_BUILTIN_DEVICE_ONESHOT");
