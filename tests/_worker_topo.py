@@ -63,6 +63,27 @@ def digest(a):
     return hashlib.sha1(np.ascontiguousarray(a).view(np.uint8).tobytes()).hexdigest()[:16]
 
 
+def identify(bad, good, candidates):
+    """Where the bytes of a corrupted buffer differ from what it should hold:
+    the byte range, and which recently seen arrays (candidates: name -> array)
+    hold the corrupted bytes at the same offsets - a diagnosis, not a check."""
+    b, g = np.ascontiguousarray(bad).view(np.uint8), np.ascontiguousarray(good).view(np.uint8)
+    pos = np.nonzero(b != g)[0]
+    if pos.size == 0:
+        return "no byte differs"
+    out = [f"{pos.size} bytes differ in [{pos[0]}, {pos[-1]}] "
+           f"(128-B lines {pos[0] // 128}..{pos[-1] // 128})"]
+    scores = []
+    for nm, arr in candidates.items():
+        c = np.ascontiguousarray(arr).view(np.uint8)
+        inr = pos[pos < c.size]
+        if inr.size:
+            scores.append((float((c[inr] == b[inr]).mean()) * inr.size / pos.size, nm))
+    scores.sort(reverse=True)
+    out.append("best matches: " + ", ".join(f"{nm} {sc:.2f}" for sc, nm in scores[:4]))
+    return "; ".join(out)
+
+
 def main():
     name, mode, max_short = sys.argv[1], sys.argv[2], int(sys.argv[3])
     n, ppn, socket, radix, factor, thresh = map(int, sys.argv[4].split(":"))
@@ -146,16 +167,22 @@ def main():
         rc = 1
 
     kinds = [("allreduce", 0)] + [("reduce", r) for r in sorted({0, n - 1, n // 2})]
+    seen = {}          # recent arrays, for identify() on a mismatch
     # TOPO_REPEAT=k runs the case list k times (a stress knob for races)
     for ci, (dt, op, count) in enumerate(CASES * int(os.environ.get("TOPO_REPEAT", "1"))):
         dist_kind = "exact" if dt.startswith("float") else "round"
         inputs = [O.fill(dt, dist_kind, 5000 + 31 * ci + m, count) for m in range(n)]
+        seen = {k: v for k, v in seen.items() if k.startswith(f"c{ci - 1} ")}
+        seen.update({f"c{ci} input{m}": x for m, x in enumerate(inputs)})
         for kind, root in kinds:
             try:
                 want = P.simulate(kind, op, dt, inputs, root=root, **cfgkw)
                 oplan = P.plan(kind, n, rank, root=root, **cfgkw)
             except P.Unsupported:
                 want = oplan = None
+            if want is not None:
+                seen.update({f"c{ci} {kind}{root} want{m}": w for m, w in enumerate(want)
+                             if w is not None})
             sbuf = send_buf(inputs[rank].copy())
             rbuf = buf(np.zeros_like(inputs[rank])) if (kind == "allreduce" or
                                                          rank == root) else None
@@ -191,9 +218,12 @@ def main():
                     bad = np.nonzero(O.bits(got) != O.bits(want[rank]))[0]
                     fail(f"{kind} {dt} {op} n={count} root={root} start {rep}: "
                          f"{bad.size} elements differ, first {bad[:6].tolist()}: got "
-                         f"{got[bad[:3]].tolist()} want {want[rank][bad[:3]].tolist()}")
-            if not (O.bits(back(sbuf, inputs[rank])) == O.bits(inputs[rank])).all():
-                fail(f"{kind} {dt} {op}: send buffer modified")
+                         f"{got[bad[:3]].tolist()} want {want[rank][bad[:3]].tolist()}; "
+                         f"{identify(got, want[rank], seen)}")
+            sgot = back(sbuf, inputs[rank])
+            if not (O.bits(sgot) == O.bits(inputs[rank])).all():
+                fail(f"{kind} {dt} {op}: send buffer modified; "
+                     f"{identify(sgot, inputs[rank], seen)}")
             if registered and ci == 0 and "Send buffer: registered" not in coll.describe():
                 fail(f"{kind} root={root}: registered send buffer not exposed in place")
             coll.close()

@@ -234,7 +234,8 @@ def test_engine_registered_send_buffers_device(spec, oneshot, monkeypatch):
     ("4:4:0:8:2:16", "n"), ("8:8:0:8:2:16", "n"), ("4:4:0:8:2:16", "split"),
     ("8:8:0:8:2:16", "split"), ("6:6:0:8:2:16", "y"),
     ("12:3:0:2:2:16", "y"), ("8:8:4:8:2:4", "y"), ("8:2:0:8:4:16", "y"),
-    ("5:1:0:2:2:16", "y")])
+    ("5:1:0:2:2:16", "y"), ("6:6:0:8:2:16", "n"), ("3:3:0:8:2:16", "y"),
+    ("12:12:0:8:2:16", "y"), ("12:12:6:8:2:4", "y")])
 def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     """Device buffers: the same plans as remote-key steps (the reference's
     rkey exchange + zero-copy reads, builtin_control.c:1014-1076,
@@ -252,10 +253,15 @@ def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)
     assert codes == [0] * n, "\n".join(outs)
-    flat_doubling = spec.split(":")[1] == spec.split(":")[0] and factor == 2 and \
-        (n & (n - 1)) == 0 and 4 <= n <= 16
-    assert ("Executed as: one-shot" in outs[0]) == (flat_doubling and oneshot != "n")
+    one_host = spec.split(":")[1] == spec.split(":")[0]
+    flat_doubling = one_host and factor == 2 and (n & (n - 1)) == 0 and 4 <= n <= 16
+    # a one-host tree without a socket level (below the threshold or no sockets)
+    flat_tree = one_host and (n & (n - 1)) != 0 and 3 <= n <= 16 and \
+        (spec.split(":")[2] == "0" or n < int(spec.split(":")[5]))
+    assert ("Executed as: one-shot" in outs[0]) == \
+        ((flat_doubling and oneshot != "n") or (flat_tree and oneshot == "y"))
     assert ("one-shot reduce-scatter" in outs[0]) == (flat_doubling and oneshot == "split")
+    assert ("as the tree's root does" in outs[0]) == (flat_tree and oneshot == "y")
     if factor == 2:
         d = _digests(outs)
         assert all(x == d[0] for x in d), d

@@ -268,7 +268,8 @@ struct ucg_builtin_lcoll {
     int          oneshot;         /* recursive doubling run as one-shot
                                      reduce-scatter + all-gather (1), or - a
                                      small message - one pass of every member
-                                     over all the data (2) */
+                                     over all the data (2), or a one-host
+                                     tree's fold in one pass (3) */
     /* ucg_params_t.completion (api/ucg.h:162-171) */
     int          comp_set;
     ucg_builtin_coll_comp_cb_f comp_cb;

@@ -944,6 +944,9 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
         } else if (c->oneshot == 2) {
             PUT("Executed as: one-shot, every member evaluating the plan's association "
                 "over all members' data\n");
+        } else if (c->oneshot == 3) {
+            PUT("Executed as: one-shot, every member folding all members' data as the "
+                "tree's root does (children in index order)\n");
         }
         if (c->exp_sbuf) {
             PUT("Send buffer: registered group memory, exposed in place\n");

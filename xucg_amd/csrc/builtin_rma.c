@@ -452,7 +452,8 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
  * A small message (oneshot 2) skips phase 1: phase 0 reads all of every
  * member's buffer and writes the whole of V into recv.buffer. Same bits as
  * the steps; UCX_BUILTIN_DEVICE_ONESHOT=n runs the steps. From 4 to 16
- * members (reduce_multi's operand limit). */
+ * members (reduce_multi's operand limit). A small allreduce over a one-host
+ * tree (oneshot 3) is the same single pass with the root's fold. */
 static int oneshot_enabled(void)
 {
     const char *e = getenv("UCX_BUILTIN_DEVICE_ONESHOT");
@@ -465,6 +466,25 @@ static int oneshot_enabled(void)
 static size_t oneshot_full_bytes(void)
 {
     return parse_memunits(getenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL"), (size_t)1 << 20);
+}
+
+/* every other member on this host and, below the socket-level threshold or
+ * without sockets, at one level: the intra-host tree of a one-host group is
+ * then member 0 with all others as children (every member sees the same, as
+ * the planner assumes symmetric layouts) */
+static int flat_host_tree(const ucg_builtin_lgroup_t *g)
+{
+    unsigned m;
+    for (m = 0; m < g->size; m++) {
+        const uint8_t d = g->distance[m];
+        if (m == g->my) {
+            continue;
+        }
+        if (d > D_HOST || d < D_SOCKET || (d == D_SOCKET && g->size >= g->sock_thresh)) {
+            return 0;
+        }
+    }
+    return 1;
 }
 
 /* shard r of the op: [r * se, min(count, (r + 1) * se)) elements, se a
@@ -521,7 +541,11 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
             return 0;
         }
     }
-    if (phase == 0 && c->oneshot == 2) {
+    if (c->oneshot == 3) {
+        /* ucg_builtin_step_recv_handle_chunk at the tree's root, member 0:
+         * its data first, then every child's (builtin_comp_step.inl:213-221) */
+        st = rma_fold(c, c->rbuf_user, peer, N);
+    } else if (phase == 0 && c->oneshot == 2) {
         for (r = 0; r < N; r++) {
             srcs[r] = peer[r];
         }
@@ -569,7 +593,7 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
 
 static void oneshot_advance(ucg_builtin_lcoll_t *c)
 {
-    const unsigned phases = c->oneshot == 2 ? 1 : 2;
+    const unsigned phases = c->oneshot >= 2 ? 1 : 2;
     while (!c->done && c->cur < phases) {
         if (!c->rma_sent) {
             oneshot_expose(c, c->cur);
@@ -716,6 +740,15 @@ UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
                    strcmp(c->plan, "recursive doubling") == 0;
     if (c->oneshot && c->length <= oneshot_full_bytes()) {
         c->oneshot = 2;
+    }
+    /* a one-host allreduce tree is flat (tree_add_intra: every member's parent
+     * is member 0), so a small message runs as one pass too: the root's fold,
+     * children in index order - one arrival order the steps may see */
+    if (!c->oneshot && c->rma == RMA_DEV && c->kind == 0 && oneshot_enabled() &&
+        c->g->size >= 3 && c->g->size <= 16 &&
+        c->length <= oneshot_full_bytes() && c->plan && strcmp(c->plan, "tree") == 0 &&
+        flat_host_tree(c->g)) {
+        c->oneshot = 3;
     }
     for (i = 0; i < 2; i++) {
         int k = rma_pool_get(c->g, c->length ? c->length : 1, c->rma);
