@@ -64,14 +64,18 @@ def test_c1_harness_bit_exact(max_short, world):
     (8, 256, "", "", "4", ""), (12, 100, "", "", "3", ""), (8, 256, "tree", "1", "8:4", ""),
     (12, 100, "", "", "3", "y"), (8, 256, "", "", "", "zcopy"),
     (12, 256, "", "", "3", "zcopy"), (6, 256, "tree", "", "", "zcopy"),
-    (8, 256, "", "", "", "zcopy-reg"), (12, 256, "", "", "3", "zcopy-reg")])
+    (8, 256, "", "", "", "zcopy-reg"), (12, 256, "", "", "3", "zcopy-reg"),
+    (8, 256, "", "", "", "zcopy-single"), (6, 256, "tree", "", "", "zcopy-single"),
+    (4, 256, "", "", "", "zcopy-steps")])
 def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast, place,
                                     pipe):
     """The host engine (libucg_builtin.so sources) and the C1 harness rebuilt
     with ASan + UBSan (tests/c/Makefile, target asan): recursive and tree
     plans, fragmenting and resend-heavy sizes, the incast fan-in, waypoints
     forwarding fragment by fragment, the shared-memory remote-key steps
-    (pipe = "zcopy"). Any sanitizer report (invalid access, UB, leak at exit)
+    (pipe = "zcopy"; at 8 members the one-shot reduce-scatter + all-gather,
+    "zcopy-single" one pass over all buffers (at 6, the tree's), "zcopy-steps"
+    the plan's steps). Any sanitizer report (invalid access, UB, leak at exit)
     fails the rank."""
     import json
     import subprocess
@@ -88,6 +92,10 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
         monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", "1")
         if pipe == "zcopy-reg":
             monkeypatch.setenv("C1_REGISTERED", "1")
+        if pipe == "zcopy-single":
+            monkeypatch.setenv("UCX_BUILTIN_SHM_ONESHOT_FULL", "1g")
+        if pipe == "zcopy-steps":
+            monkeypatch.setenv("UCX_BUILTIN_SHM_ONESHOT", "n")
     elif pipe:
         monkeypatch.setenv("UCX_BUILTIN_PIPELINE", pipe)
     if place:

@@ -206,10 +206,57 @@ def test_engine_registered_send_buffers_shm(spec, monkeypatch):
     assert codes == [0] * n, "\n".join(outs)
 
 
-def _oneshot_env(monkeypatch, oneshot):
-    monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT", "n" if oneshot == "n" else "y")
-    if oneshot == "split":
-        monkeypatch.setenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL", "0")
+def _oneshot_env(monkeypatch, oneshot, where="DEVICE"):
+    """oneshot: "y" (the defaults), "n" (the plan's steps), "split" (the
+    single-pass limit at 0), "single" (the limit at 1 GiB)"""
+    monkeypatch.setenv(f"UCX_BUILTIN_{where}_ONESHOT", "n" if oneshot == "n" else "y")
+    if oneshot in ("split", "single"):
+        monkeypatch.setenv(f"UCX_BUILTIN_{where}_ONESHOT_FULL",
+                           "0" if oneshot == "split" else "1g")
+
+
+def _check_executed_as(spec, oneshot, text, where="DEVICE"):
+    """The describe line of the one-shot executions: recursive doubling of a
+    power-of-two group on one host (4-16 members) runs as reduce-scatter +
+    all-gather or, below the single-pass limit, as one pass; a one-host tree
+    without a socket level (3-16 members), below the limit, as one pass. The
+    limit's default is 1 MiB on device buffers and 0 on host memory; these
+    messages are all far below 1 MiB."""
+    n, ppn, socket, _, factor, thresh = map(int, spec.split(":"))
+    one_host = n == ppn
+    flat_doubling = one_host and factor == 2 and (n & (n - 1)) == 0 and 4 <= n <= 16
+    flat_tree = one_host and (n & (n - 1)) != 0 and 3 <= n <= 16 and \
+        (socket == 0 or n < thresh)
+    single = oneshot == "single" or (oneshot == "y" and where == "DEVICE")
+    assert ("Executed as: one-shot" in text) == \
+        ((flat_doubling and oneshot != "n") or (flat_tree and single)), text
+    assert ("one-shot reduce-scatter" in text) == \
+        (flat_doubling and oneshot != "n" and not single)
+    assert ("as the tree's root does" in text) == (flat_tree and single)
+
+
+@pytest.mark.parametrize("spec,oneshot", [
+    ("4:4:0:8:2:16", "y"), ("8:8:0:8:2:16", "y"), ("8:8:0:8:2:16", "single"),
+    ("8:8:0:8:2:16", "n"), ("16:16:0:8:2:16", "y"), ("8:8:4:8:2:4", "single"),
+    ("6:6:0:8:2:16", "y"), ("6:6:0:8:2:16", "single"), ("3:3:0:8:2:16", "single"),
+    ("12:12:6:8:2:4", "single")])
+def test_engine_oneshot_shm(spec, oneshot, monkeypatch):
+    """The one-shot executions on host memory (shared-memory keys): the
+    butterfly of recursive doubling as reduce_cb_f calls, over every member's
+    shard (reduce-scatter + all-gather, the default) or, below
+    UCX_BUILTIN_SHM_ONESHOT_FULL (0 by default), over the whole buffer; below
+    the same limit the flat tree's fold in one pass. Same phases and
+    messages as on device buffers, bit-exact against the oracle's simulation,
+    identical bits on every member."""
+    n = int(spec.split(":")[0])
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    _oneshot_env(monkeypatch, oneshot, "SHM")
+    codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "shm", 256, spec),
+                         timeout=240)
+    assert codes == [0] * n, "\n".join(outs)
+    _check_executed_as(spec, oneshot, outs[0], "SHM")
+    d = _digests(outs)
+    assert all(x == d[0] for x in d), d
 
 
 @pytest.mark.gpu
@@ -253,15 +300,7 @@ def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)
     assert codes == [0] * n, "\n".join(outs)
-    one_host = spec.split(":")[1] == spec.split(":")[0]
-    flat_doubling = one_host and factor == 2 and (n & (n - 1)) == 0 and 4 <= n <= 16
-    # a one-host tree without a socket level (below the threshold or no sockets)
-    flat_tree = one_host and (n & (n - 1)) != 0 and 3 <= n <= 16 and \
-        (spec.split(":")[2] == "0" or n < int(spec.split(":")[5]))
-    assert ("Executed as: one-shot" in outs[0]) == \
-        ((flat_doubling and oneshot != "n") or (flat_tree and oneshot == "y"))
-    assert ("one-shot reduce-scatter" in outs[0]) == (flat_doubling and oneshot == "split")
-    assert ("as the tree's root does" in outs[0]) == (flat_tree and oneshot == "y")
+    _check_executed_as(spec, oneshot, outs[0])
     if factor == 2:
         d = _digests(outs)
         assert all(x == d[0] for x in d), d

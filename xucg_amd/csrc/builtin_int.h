@@ -265,6 +265,8 @@ struct ucg_builtin_lcoll {
     uint8_t      rdy_buf[OPS_MAX_STEPS][UCG_BUILTIN_OPS_MAX_MEMBERS];
                                   /* ... in arrival order: the fold order */
     int          rma_sent, rma_recvd, rma_final, rma_busy, rma_again;
+    void        *bf_scratch;      /* host one-shot: the butterfly's partial sums */
+    size_t       bf_bytes;
     int          oneshot;         /* recursive doubling run as one-shot
                                      reduce-scatter + all-gather (1), or - a
                                      small message - one pass of every member

@@ -454,18 +454,106 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
  * the steps; UCX_BUILTIN_DEVICE_ONESHOT=n runs the steps. From 4 to 16
  * members (reduce_multi's operand limit). A small allreduce over a one-host
  * tree (oneshot 3) is the same single pass with the root's fold. */
-static int oneshot_enabled(void)
+static int oneshot_enabled(int kind)
 {
-    const char *e = getenv("UCX_BUILTIN_DEVICE_ONESHOT");
+    const char *e = getenv(kind == RMA_DEV ? "UCX_BUILTIN_DEVICE_ONESHOT" :
+                                             "UCX_BUILTIN_SHM_ONESHOT");
     return !(e && (e[0] == 'n' || e[0] == 'N' || e[0] == '0'));
 }
 
 /* messages up to this size skip the all-gather: every member evaluates the
  * whole of V(self) from all N buffers in one kernel, straight into
- * recv.buffer (N x the reads, one launch and one wait less) */
-static size_t oneshot_full_bytes(void)
+ * recv.buffer (N x the reads, one launch and one wait less). On host memory
+ * the N x reads are reduce_cb_f work on every member's core and lost on
+ * every size measured, so there it is off unless asked for. */
+static size_t oneshot_full_bytes(int kind)
 {
-    return parse_memunits(getenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL"), (size_t)1 << 20);
+    return kind == RMA_DEV ?
+           parse_memunits(getenv("UCX_BUILTIN_DEVICE_ONESHOT_FULL"), (size_t)1 << 20) :
+           parse_memunits(getenv("UCX_BUILTIN_SHM_ONESHOT_FULL"), 0);
+}
+
+/* The two-phase one-shot gives every member the same bits: shard r is V(r)
+ * on every member. The steps give member s V(s) everywhere, and V(r) and V(s)
+ * differ where the op does not commute bit for bit on the data: on floats,
+ * two NaNs of different payloads in SUM / PROD (which payload survives follows
+ * the operand order), and MAX / MIN of MPI's (dst > src) ? dst : src form
+ * meeting NaN or +0 / -0 (builtin_recursive.c:158-169 fixes the operand
+ * order per member). Integer ops commute exactly. So by default floats
+ * split only with UCX_BUILTIN_ONESHOT_FLOAT_SPLIT=y; otherwise a float op
+ * runs the single pass (V(self) on every member, exact) below the
+ * single-pass limit and the plan's steps above it. */
+static int oneshot_split_allowed(ucg_builtin_lcoll_t *c)
+{
+    const char *e = getenv("UCX_BUILTIN_ONESHOT_FLOAT_SPLIT");
+    ucg_dev_op_t o;
+    ucg_dev_dtype_t d;
+    if (e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1')) {
+        return 1;
+    }
+    if (!ucg_builtin_combine_classify(c->g->cmb, c->op, c->dtype, &o, &d)) {
+        return 0;                       /* unknown: assume it may not commute */
+    }
+    return d != UCG_DEV_DT_FLOAT16 && d != UCG_DEV_DT_BFLOAT16 &&
+           d != UCG_DEV_DT_FLOAT32 && d != UCG_DEV_DT_FLOAT64;
+}
+
+/* dst = V(self, log2 N) of srcs[0..N) (member r's data at srcs[r]) over n
+ * elements: the device kernel, or on host memory the same tree of
+ * reduce_cb_f calls (level h folds val[m + h] into val[m], val[m] holding
+ * member self ^ m), the first level into dst and scratch */
+static ucs_status_t rma_butterfly(ucg_builtin_lcoll_t *c, void *dst, const void *const *srcs,
+                                  unsigned N, unsigned self, size_t n)
+{
+    const size_t bytes = n * c->dt_len;
+    const void *val[16];
+    unsigned h, m;
+    ucs_status_t st = UCS_OK;
+    if (c->rma == RMA_DEV) {
+        return ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype, dst, srcs, N,
+                                                 self, n);
+    }
+    if (n == 0) {
+        return UCS_OK;
+    }
+    if (N > 2 && c->bf_bytes < (N / 2 - 1) * bytes) {
+        void *p = realloc(c->bf_scratch, (N / 2 - 1) * bytes);
+        if (p == NULL) {
+            return UCS_ERR_NO_MEMORY;
+        }
+        c->bf_scratch = p;
+        c->bf_bytes   = (N / 2 - 1) * bytes;
+    }
+    for (m = 0; m < N; m++) {
+        val[m] = srcs[self ^ m];
+    }
+    for (h = 1; h < N && st == UCS_OK; h <<= 1) {
+        for (m = 0; m < N && st == UCS_OK; m += 2 * h) {
+            void *acc = (void*)val[m];
+            if (h == 1) {
+                acc = m ? (char*)c->bf_scratch + (m / 2 - 1) * bytes : dst;
+                memcpy(acc, val[m], bytes);
+            }
+            st = ucg_builtin_combine_reduce(c->g->cmb, c->op, (void*)val[m + h], acc,
+                                            (int)n, c->dtype);
+            val[m] = acc;
+        }
+    }
+    return st;
+}
+
+/* dsts[i][0:bytes] = srcs[i][0:bytes] for every i */
+static ucs_status_t rma_copy_n(ucg_builtin_lcoll_t *c, void *const *dsts,
+                               const void *const *srcs, unsigned k, size_t bytes)
+{
+    unsigned i;
+    if (c->rma == RMA_DEV) {
+        return ucg_builtin_combine_dev_copy_n(c->g->cmb, dsts, srcs, k, bytes);
+    }
+    for (i = 0; i < k; i++) {
+        memcpy(dsts[i], srcs[i], bytes);
+    }
+    return UCS_OK;
 }
 
 /* every other member on this host and, below the socket-level threshold or
@@ -549,16 +637,13 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
         for (r = 0; r < N; r++) {
             srcs[r] = peer[r];
         }
-        st = ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype, c->rbuf_user,
-                                               srcs, N, my, (size_t)c->count);
+        st = rma_butterfly(c, c->rbuf_user, srcs, N, my, (size_t)c->count);
     } else if (phase == 0) {
         oneshot_shard(c, my, &lo, &n);
         for (r = 0; r < N; r++) {
             srcs[r] = (const char*)peer[r] + lo * c->dt_len;
         }
-        st = ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype,
-                                               (char*)c->dbuf[1] + lo * c->dt_len, srcs, N,
-                                               my, n);
+        st = rma_butterfly(c, (char*)c->dbuf[1] + lo * c->dt_len, srcs, N, my, n);
     } else {
         /* every full shard in one launch, the ragged last one in another */
         oneshot_shard(c, 0, &full_lo, &full_n);
@@ -570,15 +655,13 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
             srcs[k] = (const char*)peer[r] + lo * c->dt_len;
             dsts[k] = c->rbuf_user + lo * c->dt_len;
             if (n != full_n) {
-                st = ucg_builtin_combine_dev_copy_n(c->g->cmb, &dsts[k], &srcs[k], 1,
-                                                    n * c->dt_len);
+                st = rma_copy_n(c, &dsts[k], &srcs[k], 1, n * c->dt_len);
             } else {
                 k++;
             }
         }
         if (st == UCS_OK) {
-            st = ucg_builtin_combine_dev_copy_n(c->g->cmb, dsts, srcs, k,
-                                                full_n * c->dt_len);
+            st = rma_copy_n(c, dsts, srcs, k, full_n * c->dt_len);
         }
     }
     if (st != UCS_OK) {
@@ -735,18 +818,20 @@ UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
     c->rbuf_user = rbuf_user;
     /* from 4 members on: at 2 the one step moves no more than the exchange
      * (r02os: 64 MiB, 0.187 ms one-shot against 0.127 ms as the step) */
-    c->oneshot   = c->rma == RMA_DEV && c->kind == 0 && oneshot_enabled() &&
+    c->oneshot   = c->kind == 0 && oneshot_enabled(c->rma) &&
                    c->g->size >= 4 && c->g->size <= 16 && c->plan &&
                    strcmp(c->plan, "recursive doubling") == 0;
-    if (c->oneshot && c->length <= oneshot_full_bytes()) {
+    if (c->oneshot && c->length <= oneshot_full_bytes(c->rma)) {
         c->oneshot = 2;
+    } else if (c->oneshot && !oneshot_split_allowed(c)) {
+        c->oneshot = 0;
     }
     /* a one-host allreduce tree is flat (tree_add_intra: every member's parent
      * is member 0), so a small message runs as one pass too: the root's fold,
      * children in index order - one arrival order the steps may see */
-    if (!c->oneshot && c->rma == RMA_DEV && c->kind == 0 && oneshot_enabled() &&
+    if (!c->oneshot && c->kind == 0 && oneshot_enabled(c->rma) &&
         c->g->size >= 3 && c->g->size <= 16 &&
-        c->length <= oneshot_full_bytes() && c->plan && strcmp(c->plan, "tree") == 0 &&
+        c->length <= oneshot_full_bytes(c->rma) && c->plan && strcmp(c->plan, "tree") == 0 &&
         flat_host_tree(c->g)) {
         c->oneshot = 3;
     }
@@ -866,6 +951,7 @@ UCG_INTERNAL void rma_free(ucg_builtin_lcoll_t *c)
         }
     }
     free(c->outbox);
+    free(c->bf_scratch);
 }
 
 /* ---- registered group memory ------------------------------------------- */
