@@ -582,15 +582,15 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 dist.barrier()
                 eng.close()
                 dist.barrier()      # every rank closed before the name is reused
-        # the default: fp64 keeps every member's own association (the steps, or
-        # the single pass below 1 MiB); UCX_BUILTIN_ONESHOT_FLOAT_SPLIT=y lets it
-        # run the two-phase one-shot over all links (same bits on every member,
-        # equal to the steps' here: no NaN or signed zero in these inputs)
+        # the default (fp64 SUM: the two-phase one-shot over all links from 4
+        # GPUs on), and UCX_BUILTIN_ONESHOT_FLOAT_SPLIT=n: every member's own
+        # association, i.e. the plan's recursive-doubling steps (same bits here:
+        # no NaN in these inputs)
         res = measure()
         if 4 <= world <= 16:
-            os.environ["UCX_BUILTIN_ONESHOT_FLOAT_SPLIT"] = "y"
+            os.environ["UCX_BUILTIN_ONESHOT_FLOAT_SPLIT"] = "n"
             try:
-                res["float_split"] = measure()
+                res["steps"] = measure()
             finally:
                 del os.environ["UCX_BUILTIN_ONESHOT_FLOAT_SPLIT"]
         return res

@@ -38,6 +38,9 @@ def test_allreduce_multiprocess_shm_zcopy(world, cells, monkeypatch):
     3-cell ring whose control messages meet UCS_ERR_NO_RESOURCE."""
     monkeypatch.setenv("UCX_BUILTIN_SHM_ZCOPY_THRESH", "1")
     monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    # every member's own bits on the special values (NaN payloads): no float
+    # op takes the two-phase one-shot (builtin_rma.c, oneshot_split_allowed)
+    monkeypatch.setenv("UCX_BUILTIN_ONESHOT_FLOAT_SPLIT", "n")
     codes, outs = launch("_worker_ops.py", world,
                          args=(shm_name(), "host", 256, 100, cells), timeout=240)
     assert codes == [0] * world, "\n".join(outs)

@@ -479,23 +479,32 @@ static size_t oneshot_full_bytes(int kind)
  * two NaNs of different payloads in SUM / PROD (which payload survives follows
  * the operand order), and MAX / MIN of MPI's (dst > src) ? dst : src form
  * meeting NaN or +0 / -0 (builtin_recursive.c:158-169 fixes the operand
- * order per member). Integer ops commute exactly. So by default floats
- * split only with UCX_BUILTIN_ONESHOT_FLOAT_SPLIT=y; otherwise a float op
- * runs the single pass (V(self) on every member, exact) below the
- * single-pass limit and the plan's steps above it. */
+ * order per member). Integer ops commute exactly. Which NaN payload a SUM
+ * keeps is not even fixed by the reference: `b[i] = a[i] + b[i]` in the MPI
+ * library may compile with either operand first. MAX / MIN's comparison is
+ * fixed by the source. So UCX_BUILTIN_ONESHOT_FLOAT_SPLIT = "sum" (the
+ * default) splits float SUM / PROD, "y" every float op, "n" none; a float op
+ * that may not split runs the single pass (V(self) on every member, exact)
+ * below the single-pass limit and the plan's steps above it. */
 static int oneshot_split_allowed(ucg_builtin_lcoll_t *c)
 {
     const char *e = getenv("UCX_BUILTIN_ONESHOT_FLOAT_SPLIT");
     ucg_dev_op_t o;
     ucg_dev_dtype_t d;
-    if (e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1')) {
-        return 1;
-    }
     if (!ucg_builtin_combine_classify(c->g->cmb, c->op, c->dtype, &o, &d)) {
         return 0;                       /* unknown: assume it may not commute */
     }
-    return d != UCG_DEV_DT_FLOAT16 && d != UCG_DEV_DT_BFLOAT16 &&
-           d != UCG_DEV_DT_FLOAT32 && d != UCG_DEV_DT_FLOAT64;
+    if (d != UCG_DEV_DT_FLOAT16 && d != UCG_DEV_DT_BFLOAT16 &&
+        d != UCG_DEV_DT_FLOAT32 && d != UCG_DEV_DT_FLOAT64) {
+        return 1;
+    }
+    if (e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1')) {
+        return 1;
+    }
+    if (e && (e[0] == 'n' || e[0] == 'N' || e[0] == '0')) {
+        return 0;
+    }
+    return o == UCG_DEV_OP_SUM || o == UCG_DEV_OP_PROD;
 }
 
 /* dst = V(self, log2 N) of srcs[0..N) (member r's data at srcs[r]) over n
