@@ -7,6 +7,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -36,10 +37,13 @@ def launch_exe(exe, world, args=(), timeout=240, python=False):
         cmd = ([sys.executable] if python else []) + [exe, *map(str, args)]
         procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
+    # one deadline for the whole group: a hung group ends after `timeout`,
+    # not after world x timeout
+    deadline = time.monotonic() + timeout
     outs, codes = [], []
     for p in procs:
         try:
-            out, _ = p.communicate(timeout=timeout)
+            out, _ = p.communicate(timeout=max(1.0, deadline - time.monotonic()))
         except subprocess.TimeoutExpired:
             p.kill()
             out, _ = p.communicate()
