@@ -6,6 +6,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# a timed-out engine wait prints the op's state and the stash (builtin_ops.c,
+# timeout_dump) into the worker's output, which a failing test shows
+os.environ.setdefault("UCX_BUILTIN_TIMEOUT_DUMP", "y")
 
 
 def pytest_configure(config):

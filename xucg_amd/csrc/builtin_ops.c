@@ -861,6 +861,39 @@ int ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *c, ucs_status_t *status)
     return c->done;
 }
 
+/* UCX_BUILTIN_TIMEOUT_DUMP=y: on a timed-out wait, the op's state and what
+ * sits in the group's stash, on stderr (a diagnosis aid) */
+static void timeout_dump(const ucg_builtin_lcoll_t *c)
+{
+    const ucg_builtin_lgroup_t *g = c->g;
+    const char *e = getenv("UCX_BUILTIN_TIMEOUT_DUMP");
+    unsigned k, n = 0;
+    if (!(e && (e[0] == 'y' || e[0] == '1'))) {
+        return;
+    }
+    fprintf(stderr, "[ucg timeout] member %u coll_id %u plan %s rma %d oneshot %d cur %u/%u "
+            "cur_buf %u readers %u/%u/%u rdy %u/%u/%u final %d sent %d recvd %d "
+            "outbox %u..%u pending %d stats %llu/%llu/%llu/%llu\n",
+            g->my, c->coll_id, c->plan ? c->plan : "-", c->rma, c->oneshot, c->cur,
+            c->nsteps, c->cur_buf, c->readers[0], c->readers[1], c->readers[2],
+            c->rdy_cnt[0], c->rdy_cnt[1], c->rdy_cnt[2], c->rma_final, c->rma_sent,
+            c->rma_recvd, c->out_head, c->out_tail, c->send_pending,
+            (unsigned long long)g->stats[0], (unsigned long long)g->stats[1],
+            (unsigned long long)g->stats[2], (unsigned long long)g->stats[3]);
+    for (k = 0; k < UCG_BUILTIN_OPS_MAX_CONCURRENT; k++) {
+        const stash_t *m;
+        for (m = g->slots[k].msgs; m && n < 64; m = m->next, n++) {
+            ops_header_t h;
+            uint32_t w[2] = {0, 0};
+            h.header = m->header;
+            memcpy(w, m->data, m->length < 8 ? m->length : 8);
+            fprintf(stderr, "[ucg timeout]   stashed slot %u coll_id %u step_idx 0x%x "
+                    "from %u buf %u len %zu\n", k, h.coll_id, h.step_idx, w[0], w[1],
+                    m->length);
+        }
+    }
+}
+
 ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
 {
     static double lim = -1.0;
@@ -884,6 +917,7 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
             continue;
         }
         if (now_s() - t0 > lim) {
+            timeout_dump(c);
             finish(c, UCS_ERR_TIMED_OUT);
             break;
         }
