@@ -309,7 +309,7 @@ def test_engine_fuzz_device_buffers(seed, world, max_short, cells, where, monkey
     """The same sequence on device buffers: the remote-key steps, the one-shot
     execution (4 and 8 members), registered send buffers, in place or not."""
     monkeypatch.setenv("FUZZ_BUFFERS", where)
-    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "90")
     codes, outs = launch("_worker_fuzz.py", world, args=(shm_name(), seed, max_short, cells),
                          timeout=150)
     assert codes == [0] * world, "\n".join(outs)

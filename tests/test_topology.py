@@ -267,7 +267,7 @@ def test_engine_registered_send_buffers_device(spec, oneshot, monkeypatch):
     """Registered device send buffers exposed in place (no init copy), through
     the one-shot execution, the recursive steps, the tree and waypoints."""
     n = int(spec.split(":")[0])
-    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "90")
     _oneshot_env(monkeypatch, oneshot)
     monkeypatch.setenv("TOPO_REGISTERED", "1")
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
@@ -295,7 +295,7 @@ def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     single-pass limit at 0) as reduce-scatter + all-gather: the same bits
     every way."""
     n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
-    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")   # a lost message fails fast
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "90")   # a lost message fails inside the deadline
     _oneshot_env(monkeypatch, oneshot)
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)
