@@ -286,6 +286,20 @@ UCG_INTERNAL int rma_kind(ucg_builtin_lgroup_t *g, const void *sbuf, const void 
     return (thresh && length >= thresh) ? RMA_SHM : 0;
 }
 
+/* a device call of this op that blocked for seconds (a key import, the
+ * first launch of a kernel, a fold) is named on stderr: peers waiting on this
+ * member time out meanwhile, and the note says where it stood */
+static ucs_status_t slow_note(const ucg_builtin_lcoll_t *c, const char *what, double t0,
+                              ucs_status_t st)
+{
+    const double dt = now_s() - t0;
+    if (dt > 2.0) {
+        fprintf(stderr, "[ucg slow] member %u coll_id %u: %s took %.1f s (status %d)\n",
+                c->g->my, c->coll_id, what, dt, (int)st);
+    }
+    return st;
+}
+
 /* the receive's combine: dst = srcs[n-1] (op) (... (srcs[1] (op) srcs[0])) */
 static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *const *srcs,
                              unsigned n)
@@ -293,8 +307,10 @@ static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *cons
     unsigned m;
     ucs_status_t st = UCS_OK;
     if (c->rma == RMA_DEV) {
-        return ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst, srcs, n,
-                                            (size_t)c->count);
+        const double t0 = now_s();
+        return slow_note(c, "fold", t0,
+                         ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst,
+                                                      srcs, n, (size_t)c->count));
     }
     if (dst != srcs[0]) {
         memcpy(dst, srcs[0], c->length);
@@ -315,7 +331,9 @@ static void *rma_local(const ucg_builtin_lcoll_t *c, unsigned b)
 static ucs_status_t rma_copy(ucg_builtin_lcoll_t *c, void *dst, const void *src)
 {
     if (c->rma == RMA_DEV) {
-        return ucg_builtin_combine_dev_copy(c->g->cmb, dst, src, c->length);
+        const double t0 = now_s();
+        return slow_note(c, "copy", t0,
+                         ucg_builtin_combine_dev_copy(c->g->cmb, dst, src, c->length));
     }
     if (dst != src) {
         memcpy(dst, src, c->length);
@@ -519,8 +537,10 @@ static ucs_status_t rma_butterfly(ucg_builtin_lcoll_t *c, void *dst, const void 
     unsigned h, m;
     ucs_status_t st = UCS_OK;
     if (c->rma == RMA_DEV) {
-        return ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype, dst, srcs, N,
-                                                 self, n);
+        const double t0 = now_s();
+        return slow_note(c, "butterfly", t0,
+                         ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype, dst,
+                                                           srcs, N, self, n));
     }
     if (n == 0) {
         return UCS_OK;
@@ -557,7 +577,9 @@ static ucs_status_t rma_copy_n(ucg_builtin_lcoll_t *c, void *const *dsts,
 {
     unsigned i;
     if (c->rma == RMA_DEV) {
-        return ucg_builtin_combine_dev_copy_n(c->g->cmb, dsts, srcs, k, bytes);
+        const double t0 = now_s();
+        return slow_note(c, "copy_n", t0,
+                         ucg_builtin_combine_dev_copy_n(c->g->cmb, dsts, srcs, k, bytes));
     }
     for (i = 0; i < k; i++) {
         memcpy(dsts[i], srcs[i], bytes);
@@ -776,7 +798,9 @@ UCG_INTERNAL void rma_msg(ucg_builtin_lcoll_t *c, ops_header_t h, const void *da
             finish(c, UCS_ERR_IO_ERROR);
             return;
         }
-        st = rma_import(c->g, w[0], c->rma, (const char*)data + 8, &p);
+        const double t0 = now_s();
+        st = slow_note(c, "key import", t0,
+                       rma_import(c->g, w[0], c->rma, (const char*)data + 8, &p));
         if (st != UCS_OK) {
             finish(c, st);
             return;
