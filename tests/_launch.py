@@ -50,4 +50,13 @@ def launch_exe(exe, world, args=(), timeout=240, python=False):
             out += "\n<killed: timeout>"
         outs.append(out)
         codes.append(p.returncode)
+    # XUCG_LAUNCH_LOG=<file>: every rank's output appended there, passing
+    # groups included (slow-call notes of a run that still passed)
+    log = os.environ.get("XUCG_LAUNCH_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(f"=== {os.path.basename(exe)} {' '.join(map(str, args))} "
+                    f"codes {codes}\n")
+            for r, out in enumerate(outs):
+                f.write("".join(f"[{r}] {line}\n" for line in out.splitlines()))
     return codes, outs
