@@ -83,7 +83,12 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
     import json
     import subprocess
     cdir = os.path.join(os.path.dirname(__file__), "c")
-    subprocess.run(["make", "-s", "-C", cdir, "asan"], check=True)
+    # one make at a time: pytest-xdist workers would otherwise rebuild the
+    # same objects at once after a source change
+    import fcntl
+    with open(os.path.join(cdir, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", cdir, "asan"], check=True)
     exe = os.path.join(cdir, "_build", "asan", "c1_allreduce")
     monkeypatch.setenv("ASAN_OPTIONS", "detect_leaks=1:abort_on_error=0")
     monkeypatch.setenv("UBSAN_OPTIONS", "print_stacktrace=1")
