@@ -13,6 +13,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 /* ------------------------------------------------------------------------ */
@@ -294,8 +295,11 @@ static ucs_status_t slow_note(const ucg_builtin_lcoll_t *c, const char *what, do
 {
     const double dt = now_s() - t0;
     if (dt > 2.0) {
-        fprintf(stderr, "[ucg slow] member %u coll_id %u: %s took %.1f s (status %d)\n",
-                c->g->my, c->coll_id, what, dt, (int)st);
+        struct timespec ts;
+        clock_gettime(CLOCK_REALTIME, &ts);
+        fprintf(stderr, "[ucg slow] member %u coll_id %u: %s took %.1f s (status %d), "
+                "ended at %.3f\n", c->g->my, c->coll_id, what, dt, (int)st,
+                ts.tv_sec + ts.tv_nsec * 1e-9);
     }
     return st;
 }
