@@ -1,0 +1,38 @@
+"""Do the 5-member device-buffer workers stall because their parent process
+holds an initialised GPU context? Times the same worker group launched from
+this process (1) before it touches the GPU, (2) after a device context was
+created and closed, (3) with a device context open, (4) after 2 more
+groups. A group that needs more than its deadline is reported as such."""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from _launch import launch  # noqa: E402
+
+os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "90")
+spec = sys.argv[1] if len(sys.argv) > 1 else "5:1:0:2:2:16"
+n = int(spec.split(":")[0])
+
+
+def group(tag):
+    t0 = time.time()
+    codes, outs = launch("_worker_topo.py", n, args=(f"probe_{os.getpid()}_{tag}", "rma", 256,
+                                                     spec), timeout=60)
+    slow = [l for o in outs for l in o.splitlines() if "ucg slow" in l]
+    print(f"{tag}: {time.time() - t0:.1f} s codes {codes} slow notes {len(slow)}", flush=True)
+    for l in slow[:6]:
+        print("   ", l, flush=True)
+
+
+group("fresh-parent")
+import xucg_amd  # noqa: E402
+ctx = xucg_amd.DevContext(device=0)
+ctx.close()
+group("after-closed-context")
+ctx = xucg_amd.DevContext(device=0)
+group("open-context")
+ctx.close()
+group("again")

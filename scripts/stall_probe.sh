@@ -17,18 +17,25 @@ CG=/sys/fs/cgroup$(cut -d: -f3 /proc/self/cgroup | head -1)
     sleep 0.5
   done ) > $OUT/samples.log 2>&1 &
 SAMPLER=$!
-run() { # tag spec extra-env...
-    local tag=$1 spec=$2; shift 2
-    env "$@" XUCG_LAUNCH_LOG=$PWD/$OUT/ranks_$tag.log timeout -k 10 200 python -u -m pytest -q \
-        --timeout 180 --timeout-method thread --durations=5 \
-        "tests/test_topology.py::test_engine_placements_device_buffers[$spec]" > $OUT/pytest_$tag.log 2>&1
+run() { # tag test-ids... (env from STALL_ENV)
+    local tag=$1; shift
+    env $STALL_ENV XUCG_LAUNCH_LOG=$PWD/$OUT/ranks_$tag.log timeout -k 10 400 python -u -m pytest -v \
+        --timeout 180 --timeout-method thread --durations=8 "$@" > $OUT/pytest_$tag.log 2>&1
     local rc=$?
     echo "$tag rc=$rc $(date +%s.%N) $(tail -1 $OUT/pytest_$tag.log)" | tee -a $OUT/steps.log
+    grep -h "s call" $OUT/pytest_$tag.log | head -8 | tee -a $OUT/steps.log
     grep -h "ucg slow" $OUT/ranks_$tag.log | head -20 | tee -a $OUT/steps.log
     return $rc
 }
-run a "5:1:0:2:2:16-y"
-[ $? -lt 124 ] && run b "5:1:0:2:2:16-y" UCX_BUILTIN_WAIT_SPIN=64
-[ $? -lt 124 ] && run c "8:8:0:8:2:16-y"
+P5="tests/test_topology.py::test_engine_placements_device_buffers[5:1:0:2:2:16-y]"
+F5="tests/test_ops_engine.py::test_engine_fuzz_device_buffers[14-5-256-64-device-reg]"
+INPROC="tests/test_gpu_combine.py::test_stage_end_completion_word tests/test_host_combine.py::test_staged_step_on_device_matches_host_fallback tests/test_host_combine.py::test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu tests/test_host_combine.py::test_staged_step_into_device_resident_recv_buffer"
+STALL_ENV=""
+case "${2:-order}" in
+order)
+  run multi $F5 $P5
+  [ $? -lt 124 ] && run inproc $INPROC $P5 $F5
+  ;;
+esac
 kill $SAMPLER
 cat $OUT/box_cpu.txt
