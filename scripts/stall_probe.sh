@@ -30,11 +30,16 @@ run() { # tag test-ids... (env from STALL_ENV)
 P5="tests/test_topology.py::test_engine_placements_device_buffers[5:1:0:2:2:16-y]"
 F5="tests/test_ops_engine.py::test_engine_fuzz_device_buffers[14-5-256-64-device-reg]"
 INPROC="tests/test_gpu_combine.py::test_stage_end_completion_word tests/test_host_combine.py::test_staged_step_on_device_matches_host_fallback tests/test_host_combine.py::test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu tests/test_host_combine.py::test_staged_step_into_device_resident_recv_buffer"
-STALL_ENV=""
+STALL_ENV="XUCG_TEST_ORDER=as-given"
 case "${2:-order}" in
 order)
   run multi $F5 $P5
   [ $? -lt 124 ] && run inproc $INPROC $P5 $F5
+  ;;
+split)
+  # which in-process test leaves the parent in the state that stalls the workers
+  run sig tests/test_gpu_combine.py::test_stage_end_completion_word $P5
+  [ $? -lt 124 ] && run host tests/test_host_combine.py::test_staged_step_on_device_matches_host_fallback tests/test_host_combine.py::test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu tests/test_host_combine.py::test_staged_step_into_device_resident_recv_buffer $P5
   ;;
 esac
 kill $SAMPLER

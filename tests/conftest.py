@@ -42,6 +42,8 @@ def pytest_collection_modifyitems(session, config, items):
     stalled for 10-46 s per device call (profiles/r02/r02s6: 2.98 s for the
     5-member placement test from a fresh pytest, 154 s and a timeout after the
     in-process tests); each worker group stays bounded by its own deadline."""
+    if os.environ.get("XUCG_TEST_ORDER") == "as-given":    # scripts/stall_probe.sh
+        return
     first = [it for it in items if it.get_closest_marker("gpu") and _launches_workers(it)]
     if first:
         keep = set(map(id, first))
