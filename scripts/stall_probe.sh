@@ -41,6 +41,12 @@ split)
   run sig tests/test_gpu_combine.py::test_stage_end_completion_word $P5
   [ $? -lt 124 ] && run host tests/test_host_combine.py::test_staged_step_on_device_matches_host_fallback tests/test_host_combine.py::test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu tests/test_host_combine.py::test_staged_step_into_device_resident_recv_buffer $P5
   ;;
+each)
+  # one in-process test at a time, then the 5-member fuzz (3 s fresh, 30 s stalled)
+  run t1 tests/test_host_combine.py::test_staged_step_on_device_matches_host_fallback $F5
+  [ $? -lt 124 ] && run t2 tests/test_host_combine.py::test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu $F5
+  [ $? -lt 124 ] && run t3 tests/test_host_combine.py::test_staged_step_into_device_resident_recv_buffer $F5
+  ;;
 esac
 kill $SAMPLER
 cat $OUT/box_cpu.txt
