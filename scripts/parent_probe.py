@@ -28,6 +28,17 @@ def group(tag):
 
 
 group("fresh-parent")
+if len(sys.argv) > 2 and sys.argv[2] == "torch":
+    # only torch's device context in the parent (test_host_combine.py's t2 / t3
+    # use torch tensors; r02s14)
+    import torch
+    x = torch.zeros(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    group("torch-tensor-alive")
+    del x
+    torch.cuda.empty_cache()
+    group("torch-tensor-freed")
+    sys.exit(0)
 import xucg_amd  # noqa: E402
 ctx = xucg_amd.DevContext(device=0)
 ctx.close()
