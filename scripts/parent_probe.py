@@ -39,6 +39,30 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] == "torch-xucg":
+    # bench.py's parent: torch imported first (its bundled runtime serves
+    # both), a device context running the combine on its own buffers, and a
+    # combine on torch tensors as test_host_combine.py's t2 does
+    import torch
+    import xucg_amd
+    ctx = xucg_amd.DevContext(device=0)
+    nn = 1 << 22
+    s_, d_ = ctx.alloc(nn * 4), ctx.alloc(nn * 4)
+    ctx.profile_reduce("sum", "float32", d_.ptr, s_.ptr, nn, 20)
+    s_.free()
+    d_.free()
+    ctx.close()
+    group("torch-then-xucg-buffers")
+    from mock_mpi import MockMPI, OPS, DTYPES
+    from xucg_amd import host
+    cmb = host.BuiltinCombine(MockMPI().callbacks(), host.make_config())
+    a = torch.ones(1 << 20, device="cuda")
+    b = torch.ones(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    assert cmb.reduce(OPS["sum"], a, b, 1 << 20, DTYPES["float32"]) == 0
+    cmb.close()
+    group("combine-on-torch-tensors")
+    sys.exit(0)
 import xucg_amd  # noqa: E402
 ctx = xucg_amd.DevContext(device=0)
 ctx.close()
