@@ -39,6 +39,30 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] in ("devctx-on-torch", "combine-on-own"):
+    # which half of torch-xucg sets it off: (devctx-on-torch) the device
+    # shim's own context combining two torch tensors, or (combine-on-own)
+    # BuiltinCombine.reduce on two buffers of the shim's allocator
+    import torch
+    import xucg_amd
+    if sys.argv[2] == "devctx-on-torch":
+        a = torch.ones(1 << 20, device="cuda")
+        b = torch.ones(1 << 20, device="cuda")
+        torch.cuda.synchronize()
+        ctx = xucg_amd.DevContext(device=0)
+        ctx.reduce_checked("sum", "float32", b, a, 1 << 20)
+        ctx.sync()
+        ctx.close()
+    else:
+        from mock_mpi import MockMPI, OPS, DTYPES
+        from xucg_amd import host
+        ctx = xucg_amd.DevContext(device=0)
+        a, b = ctx.alloc(4 << 20), ctx.alloc(4 << 20)
+        cmb = host.BuiltinCombine(MockMPI().callbacks(), host.make_config())
+        assert cmb.reduce(OPS["sum"], a.ptr, b.ptr, 1 << 20, DTYPES["float32"]) == 0
+        cmb.close()
+    group(sys.argv[2])
+    sys.exit(0)
 if len(sys.argv) > 2 and sys.argv[2] == "torch-xucg":
     # bench.py's parent: torch imported first (its bundled runtime serves
     # both), a device context running the combine on its own buffers, and a
