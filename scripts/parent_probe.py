@@ -39,6 +39,22 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] in ("devctx-on-torch-keep", "torchstream-on-torch"):
+    # devctx-on-torch with the context left open, or with the context on
+    # torch's current stream (DevContext.on_torch_stream) instead of its own
+    import torch
+    import xucg_amd
+    a = torch.ones(1 << 20, device="cuda")
+    b = torch.ones(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    ctx = (xucg_amd.DevContext(device=0) if sys.argv[2] == "devctx-on-torch-keep"
+           else xucg_amd.DevContext.on_torch_stream(0))
+    ctx.reduce_checked("sum", "float32", b, a, 1 << 20)
+    ctx.sync()
+    torch.cuda.synchronize()
+    group(sys.argv[2])
+    ctx.close()
+    sys.exit(0)
 if len(sys.argv) > 2 and sys.argv[2] in ("devctx-on-torch", "combine-on-own"):
     # which half of torch-xucg sets it off: (devctx-on-torch) the device
     # shim's own context combining two torch tensors, or (combine-on-own)
