@@ -39,6 +39,18 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] == "torchinit-own":
+    # torch's device context initialised, the combine on the shim's own buffers
+    import torch
+    import xucg_amd
+    x = torch.zeros(16, device="cuda")
+    torch.cuda.synchronize()
+    ctx = xucg_amd.DevContext(device=0)
+    a, b = ctx.alloc(4 << 20), ctx.alloc(4 << 20)
+    ctx.reduce_checked("sum", "float32", b, a, 1 << 20)
+    ctx.sync()
+    group(sys.argv[2])
+    sys.exit(0)
 if len(sys.argv) > 2 and sys.argv[2] in ("devctx-on-torch-keep", "torchstream-on-torch"):
     # devctx-on-torch with the context left open, or with the context on
     # torch's current stream (DevContext.on_torch_stream) instead of its own
