@@ -39,6 +39,15 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] == "rocm-first-torchinit-own":
+    # torchinit-own with this build's library (and /opt/rocm's HIP runtime)
+    # loaded before torch, so one runtime, /opt/rocm's, serves both
+    from xucg_amd import _lib
+    _lib.dev()
+    sys.argv[2] = "torchinit-own"
+    import torch
+    with open("/proc/self/maps") as f:
+        print(sorted({l.split()[-1] for l in f if "amdhip64" in l}), flush=True)
 if len(sys.argv) > 2 and sys.argv[2] == "torchinit-own":
     # torch's device context initialised, the combine on the shim's own buffers
     import torch
