@@ -32,11 +32,12 @@ def _launches_workers(item):
         src = inspect.getsource(fn) if fn else ""
     except (OSError, TypeError):
         return False
-    return "launch(" in src or "launch_exe(" in src
+    return any(k in src for k in ("launch(", "launch_exe(", "subprocess"))
 
 
 def pytest_collection_modifyitems(session, config, items):
-    """GPU tests that run their ranks as worker processes go first, before any
+    """GPU tests that run their ranks as worker processes (or a C harness or
+    bench.py in a subprocess) go first, before any
     test initialises the GPU inside the pytest process itself. On the one-GPU
     box, 5-member device groups launched after the in-process device tests
     stalled for 10-46 s per device call (profiles/r02/r02s6: 2.98 s for the
