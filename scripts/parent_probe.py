@@ -39,6 +39,21 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] == "torchinit-tiny":
+    # torch's device context initialised, then one kernel of a separate
+    # one-kernel code object (scripts/tiny_kernel.hip -> tools/libtiny_kernel.so),
+    # none of this build's: is it any foreign code object, or this build's?
+    import ctypes
+    import torch
+    x = torch.ones(1 << 20, device="cuda")
+    y = torch.ones(1 << 20, device="cuda")
+    torch.cuda.synchronize()
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libtiny_kernel.so"))
+    lib.tiny_add.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong]
+    assert lib.tiny_add(x.data_ptr(), y.data_ptr(), 1 << 20) == 0
+    assert float(x[0]) == 2.0
+    group(sys.argv[2])
+    sys.exit(0)
 if len(sys.argv) > 2 and sys.argv[2] == "rocm-first-torchinit-own":
     # torchinit-own with this build's library (and /opt/rocm's HIP runtime)
     # loaded before torch, so one runtime, /opt/rocm's, serves both
