@@ -39,7 +39,18 @@ if len(sys.argv) > 2 and sys.argv[2] == "torch":
     torch.cuda.empty_cache()
     group("torch-tensor-freed")
     sys.exit(0)
-if len(sys.argv) > 2 and sys.argv[2] == "torchinit-tiny":
+if len(sys.argv) > 2 and sys.argv[2] == "torchinit-ctx-nolaunch":
+    # torch's device context, then this build's library loaded and a device
+    # context created (streams, pinned words) with no kernel launched
+    import torch
+    import xucg_amd
+    x = torch.ones(16, device="cuda")
+    torch.cuda.synchronize()
+    ctx = xucg_amd.DevContext(device=0)
+    group(sys.argv[2])
+    ctx.close()
+    sys.exit(0)
+if len(sys.argv) > 2 and sys.argv[2] in ("torchinit-tiny", "torchinit-tiny-nt"):
     # torch's device context initialised, then one kernel of a separate
     # one-kernel code object (scripts/tiny_kernel.hip -> tools/libtiny_kernel.so),
     # none of this build's: is it any foreign code object, or this build's?
@@ -49,8 +60,9 @@ if len(sys.argv) > 2 and sys.argv[2] == "torchinit-tiny":
     y = torch.ones(1 << 20, device="cuda")
     torch.cuda.synchronize()
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libtiny_kernel.so"))
-    lib.tiny_add.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong]
-    assert lib.tiny_add(x.data_ptr(), y.data_ptr(), 1 << 20) == 0
+    fn = lib.tiny_add_nt if sys.argv[2].endswith("-nt") else lib.tiny_add
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong]
+    assert fn(x.data_ptr(), y.data_ptr(), 1 << 20) == 0
     assert float(x[0]) == 2.0
     group(sys.argv[2])
     sys.exit(0)
