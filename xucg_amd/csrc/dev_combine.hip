@@ -140,7 +140,7 @@ static const size_t kDtSize[UCG_DEV_DT_LAST] = {1, 1, 2, 2, 4, 4, 8, 8, 2, 2, 4,
 struct ucg_builtin_dev_ctx {
     int          device;
     hipStream_t  stream;       /* compute + H2D (owned unless passed in) */
-    hipStream_t  stream_d2h;   /* D2H of the host pipeline (always owned) */
+    hipStream_t  stream_d2h;   /* D2H of the host pipeline (owned, made on first use) */
     bool         own_stream;
 
     /* pinned staging ring (lazy) */
@@ -468,9 +468,9 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
             e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
         }
     }
-    if (e == hipSuccess) {
-        e = hipStreamCreateWithFlags(&ctx->stream_d2h, hipStreamNonBlocking);
-    }
+    /* stream_d2h is created on first use (d2h_stream): only the pipeline of
+     * a host-resident dst needs it, and every stream can take a hardware
+     * queue of the GPU that other processes share (stalls) */
     if (e != hipSuccess) {
         st = hip_status(e, "ctx_create");
         ucg_builtin_dev_ctx_destroy(ctx);
@@ -523,6 +523,16 @@ void ucg_builtin_dev_ctx_destroy(ucg_builtin_dev_ctx_t *ctx)
     delete ctx;
 }
 
+/* the D2H stream of the host pipeline, created on first use */
+static ucs_status_t d2h_stream(ucg_builtin_dev_ctx_t *ctx)
+{
+    if (ctx->stream_d2h == nullptr) {
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipStreamCreateWithFlags(&ctx->stream_d2h, hipStreamNonBlocking));
+    }
+    return UCS_OK;
+}
+
 void *ucg_builtin_dev_ctx_stream(ucg_builtin_dev_ctx_t *ctx)
 {
     return ctx ? (void*)ctx->stream : nullptr;
@@ -534,7 +544,9 @@ ucs_status_t ucg_builtin_dev_sync(ucg_builtin_dev_ctx_t *ctx)
         return set_error(UCS_ERR_INVALID_PARAM, "sync", "ctx is NULL");
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    if (ctx->stream_d2h) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    }
     return UCS_OK;
 }
 
@@ -941,7 +953,8 @@ ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
      * combining per fragment while a step is staged, builtin_ops.c): flush
      * them first, so the slots this call takes - and frees at its end - hold
      * no pending data */
-    if ((st = runs_flush_all(ctx)) != UCS_OK || (st = record_deferred(ctx)) != UCS_OK) {
+    if ((st = runs_flush_all(ctx)) != UCS_OK || (st = record_deferred(ctx)) != UCS_OK ||
+        (!dst_dev && (st = d2h_stream(ctx)) != UCS_OK)) {
         return st;
     }
     ctx->queued = true;
@@ -978,7 +991,9 @@ ucs_status_t ucg_builtin_dev_combine_host(ucg_builtin_dev_ctx_t *ctx,
         }
     }
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    if (ctx->stream_d2h) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    }
     for (unsigned i = 0; i < ctx->nslots; i++) {
         ctx->slot_used[i] = false;
     }
