@@ -1,6 +1,8 @@
 // A one-kernel code object for scripts/parent_probe.py (mode torchinit-tiny):
 // does launching ANY kernel outside torch's own code objects, in a process
 // where torch initialised the device, set off the multi-process stalls?
+// Build (in-tree, tools/ is git-ignored but travels with gpurun):
+//   hipcc --offload-arch=gfx950 -O2 -shared -fPIC -o tools/libtiny_kernel.so scripts/tiny_kernel.hip
 #include <hip/hip_runtime.h>
 
 __global__ void k_tiny_add(float *d, const float *s, unsigned long n)
