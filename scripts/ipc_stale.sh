@@ -18,3 +18,8 @@ run() { # name iters bytes read
 run k64k 2000 65536 kernel
 run d64k 2000 65536 dma
 run k8m 300 8388608 kernel
+# the writer waits on the engine's completion word instead of the runtime
+export IPC_STALE_WAIT=signal
+run k64k_sig 2000 65536 kernel
+run d64k_sig 2000 65536 dma
+run k8m_sig 300 8388608 kernel

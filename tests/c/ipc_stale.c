@@ -71,6 +71,8 @@ int main(int argc, char **argv)
         return 1;
     }
     if (rank == 0) {
+        const char *we = getenv("IPC_STALE_WAIT");
+        const int wait_signal = we && strcmp(we, "signal") == 0;
         void *x = ucg_builtin_dev_malloc(ctx, bytes);
         if (x == NULL || ucg_builtin_dev_ipc_export(ctx, x, key) != UCS_OK) {
             return 1;
@@ -79,7 +81,13 @@ int main(int argc, char **argv)
         for (i = 0; i < iters; i++) {
             ucg_builtin_dev_fill(ctx, UCG_DEV_DT_UINT32, UCG_DEV_DIST_ROUND,
                                  0x5A1E0000u + i, x, n);
-            ucg_builtin_dev_sync(ctx);
+            /* IPC_STALE_WAIT=signal: the engine's wait (the pinned completion
+             * word), else the runtime's hipStreamSynchronize */
+            if (wait_signal) {
+                ucg_builtin_dev_complete(ctx);
+            } else {
+                ucg_builtin_dev_sync(ctx);
+            }
             send_msg(it, 1, 2 + (uint64_t)i, NULL, 0);
             if (wait_msg(it) != 2 + (uint64_t)i) {
                 fprintf(stderr, "rank 0: out of step at %d\n", i);
