@@ -84,6 +84,41 @@ def identify(bad, good, candidates):
     return "; ".join(out)
 
 
+GUARD = 4096          # guard zone before and after every per-case device buffer
+GUARD_BYTE = 0xA5
+
+
+class Guarded:
+    """A device buffer between two guard zones of a known pattern: a write
+    past either end of the buffer is found when it is freed."""
+
+    def __init__(self, dctx, nbytes):
+        self.raw = dctx.alloc(nbytes + 2 * GUARD)
+        self.nbytes = nbytes
+        self.ptr = self.raw.ptr + GUARD
+        pat = np.full(GUARD, GUARD_BYTE, np.uint8)
+        self.raw.upload(pat, 0)
+        self.raw.upload(pat, GUARD + nbytes)
+
+    def upload(self, a):
+        self.raw.upload(a, GUARD)
+
+    def download(self, dtype, count):
+        return self.raw.download(dtype, count, GUARD)
+
+    def guards_damaged(self):
+        out = []
+        for name, off in (("head", 0), ("tail", GUARD + self.nbytes)):
+            g = self.raw.download(np.uint8, GUARD, off)
+            bad = np.nonzero(g != GUARD_BYTE)[0]
+            if bad.size:
+                out.append(f"{name} guard: {bad.size} bytes in [{bad[0]}, {bad[-1]}]")
+        return "; ".join(out)
+
+    def free(self):
+        self.raw.free()
+
+
 def main():
     name, mode, max_short = sys.argv[1], sys.argv[2], int(sys.argv[3])
     n, ppn, socket, radix, factor, thresh = map(int, sys.argv[4].split(":"))
@@ -111,18 +146,26 @@ def main():
         print("no device", flush=True)
         sys.exit(2)
 
-    def buf(a):
-        """the op's buffer: the array itself, or a device copy of it"""
+    def buf(a, what="buf"):
+        """the op's buffer: the array itself, or a device copy of it between
+        guard zones, read back right after the upload"""
         if dctx is None:
             return a
-        b = dctx.alloc(max(a.nbytes, 1))
+        b = Guarded(dctx, a.nbytes)
         b.upload(a)
+        chk = b.download(a.dtype, a.size)
+        if not (O.bits(chk) == O.bits(a)).all():
+            fail(f"UPLOAD LOST before any engine call: {what} at 0x{b.ptr:x}; "
+                 f"{identify(chk, a, {'zeros': np.zeros_like(a)})}")
         return b
 
     def back(b, like):
         if isinstance(b, int):             # registered group memory
             return read_reg(b, like)
         return b if dctx is None else b.download(like.dtype, like.size)
+
+    def ptr(b):
+        return b.ptr if isinstance(b, Guarded) else b
 
     # TOPO_REGISTERED=1: send buffers from the group's registered memory
     # (ucg_builtin_lgroup_mem_alloc), exposed in place by remote-key steps
@@ -146,10 +189,13 @@ def main():
             ctypes.memmove(p, a.ctypes.data, a.nbytes)
         return p
 
-    def free_buf(b):
+    def free_buf(b, what):
         if isinstance(b, int):
             group.mem_free(b)
         elif dctx is not None and b is not None:
+            bad = b.guards_damaged()
+            if bad:
+                fail(f"guard zone of {what} at 0x{b.ptr:x} written: {bad}")
             b.free()
 
     iface = ops.ShmIface(name, n, rank, max_short=max_short, ring_cells=16)
@@ -184,8 +230,13 @@ def main():
                 seen.update({f"c{ci} {kind}{root} want{m}": w for m, w in enumerate(want)
                              if w is not None})
             sbuf = send_buf(inputs[rank].copy())
-            rbuf = buf(np.zeros_like(inputs[rank])) if (kind == "allreduce" or
-                                                         rank == root) else None
+            rbuf = buf(np.zeros_like(inputs[rank]), "recv buffer") if (
+                kind == "allreduce" or rank == root) else None
+            if dctx is not None:
+                # every user buffer's address, so that a corrupted range can be
+                # matched against the engine's launches (XUCG_RMA_TRACE)
+                print(f"case c{ci} {kind}{root} {dt} {op}: sbuf 0x{ptr(sbuf):x} rbuf "
+                      f"{'-' if rbuf is None else hex(ptr(rbuf))}", flush=True)
             coll = (group.allreduce(sbuf, rbuf, count, DTYPES[dt], OPS[op]) if kind == "allreduce"
                     else group.reduce(sbuf, rbuf, count, DTYPES[dt], OPS[op], root))
             if oplan is None:
@@ -210,6 +261,12 @@ def main():
                     fail(f"{kind} root={root}: buffers not described\n{text}")
             # persistent: a second start reuses the keys of the first
             for rep in range(2 if mode in ("rma", "shm") and ci < 2 else 1):
+                if dctx is not None and not isinstance(sbuf, int):
+                    pre = back(sbuf, inputs[rank])
+                    if not (O.bits(pre) == O.bits(inputs[rank])).all():
+                        fail(f"{kind} {dt} {op}: send buffer changed before start {rep} "
+                             f"(no engine call has touched it): "
+                             f"{identify(pre, inputs[rank], {'zeros': np.zeros_like(pre)})}")
                 st = coll.run()
                 got = back(rbuf, inputs[rank]) if rbuf is not None else None
                 if st != 0:
@@ -219,16 +276,16 @@ def main():
                     fail(f"{kind} {dt} {op} n={count} root={root} start {rep}: "
                          f"{bad.size} elements differ, first {bad[:6].tolist()}: got "
                          f"{got[bad[:3]].tolist()} want {want[rank][bad[:3]].tolist()}; "
-                         f"{identify(got, want[rank], seen)}")
+                         f"{identify(got, want[rank], dict(seen, zeros=np.zeros_like(got)))}")
             sgot = back(sbuf, inputs[rank])
             if not (O.bits(sgot) == O.bits(inputs[rank])).all():
                 fail(f"{kind} {dt} {op}: send buffer modified; "
-                     f"{identify(sgot, inputs[rank], seen)}")
+                     f"{identify(sgot, inputs[rank], dict(seen, zeros=np.zeros_like(sgot)))}")
             if registered and ci == 0 and "Send buffer: registered" not in coll.describe():
                 fail(f"{kind} root={root}: registered send buffer not exposed in place")
             coll.close()
-            for b in (sbuf, rbuf):
-                free_buf(b)
+            free_buf(sbuf, "send buffer")
+            free_buf(rbuf, "recv buffer")
 
     # rounded fp32: tolerance against the fp64 sum, digests for identity
     for ci, count in enumerate((4096, 1000)):

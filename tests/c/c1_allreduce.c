@@ -82,10 +82,13 @@ int main(int argc, char **argv)
     ucg_builtin_dev_ctx_t *dev = NULL;
     void *dsend = NULL, *drecv = NULL, *inputs_reg = NULL;
 
+    /* the configuration read the way UCX reads it (UCX_BUILTIN_DEV_*) */
+    ucg_builtin_combine_config_read(&cfg);
+    if (!getenv("C1_DEVICE_STAGING") && !getenv("C1_DEVICE_BUFFERS")) {
+        cfg.dev_enable = 0;       /* host buffers: every combine on reduce_cb_f */
+    }
     if (getenv("C1_DEVICE_STAGING")) {
-        /* every step staged on the GPU: the configuration read the way UCX
-         * reads it (UCX_BUILTIN_DEV_*), then forced on for any size */
-        ucg_builtin_combine_config_read(&cfg);
+        /* every step staged on the GPU, forced on for any size */
         cfg.dev_enable    = 2;
         cfg.dev_min_bytes = 0;
     }

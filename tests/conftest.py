@@ -23,29 +23,3 @@ def dev_ctx():
     ctx = xucg_amd.DevContext(device=0)
     yield ctx
     ctx.close()
-
-
-def _launches_workers(item):
-    import inspect
-    fn = getattr(item, "function", None)
-    try:
-        src = inspect.getsource(fn) if fn else ""
-    except (OSError, TypeError):
-        return False
-    return any(k in src for k in ("launch(", "launch_exe(", "subprocess"))
-
-
-def pytest_collection_modifyitems(session, config, items):
-    """GPU tests that run their ranks as worker processes (or a C harness or
-    bench.py in a subprocess) go first, before any
-    test initialises the GPU inside the pytest process itself. On the one-GPU
-    box, 5-member device groups launched after the in-process device tests
-    stalled for 10-46 s per device call (profiles/r02/r02s6: 2.98 s for the
-    5-member placement test from a fresh pytest, 154 s and a timeout after the
-    in-process tests); each worker group stays bounded by its own deadline."""
-    if os.environ.get("XUCG_TEST_ORDER") == "as-given":    # scripts/stall_probe.sh
-        return
-    first = [it for it in items if it.get_closest_marker("gpu") and _launches_workers(it)]
-    if first:
-        keep = set(map(id, first))
-        items[:] = first + [it for it in items if id(it) not in keep]

@@ -296,6 +296,9 @@ def test_engine_placements_device_buffers(spec, oneshot, monkeypatch):
     every way."""
     n, factor = int(spec.split(":")[0]), int(spec.split(":")[4])
     monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "90")   # a lost message fails inside the deadline
+    # every device write of the engine, pool buffer and import on stderr, so a
+    # mismatch in the output below names the writer (DESIGN.md 7)
+    monkeypatch.setenv("XUCG_RMA_TRACE", "1")
     _oneshot_env(monkeypatch, oneshot)
     codes, outs = launch("_worker_topo.py", n, args=(shm_name(), "rma", 256, spec),
                          timeout=150)

@@ -47,6 +47,8 @@ struct rma_msg {
 };
 
 
+static int rma_trace_on(void);
+
 struct rma_pool {
     void    *ptr;
     size_t   bytes;
@@ -228,6 +230,9 @@ static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
     if (st != UCS_OK) {
         return st;
     }
+    if (rma_trace_on()) {
+        fprintf(stderr, "[rma %u] import of member %u's buffer -> %p\n", g->my, peer, *ptr);
+    }
     m = &g->imp[g->nimp++];
     m->peer = peer;
     m->kind = kind;
@@ -304,6 +309,35 @@ static ucs_status_t slow_note(const ucg_builtin_lcoll_t *c, const char *what, do
     return st;
 }
 
+/* XUCG_RMA_TRACE=1: every device write of the remote-key steps (its dst
+ * range and its sources), every pool buffer and every imported peer buffer,
+ * one line each on stderr - so that a corrupted range in a test can be matched
+ * against what the engine wrote */
+static int rma_trace_on(void)
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("XUCG_RMA_TRACE");
+        on = e && (e[0] == '1' || e[0] == 'y');
+    }
+    return on;
+}
+
+static void rma_trace(const ucg_builtin_lcoll_t *c, const char *what, const void *dst,
+                      size_t bytes, const void *const *srcs, unsigned n)
+{
+    unsigned i;
+    if (!rma_trace_on()) {
+        return;
+    }
+    fprintf(stderr, "[rma %u c%u] %s dst %p..%p", c->g->my, c->coll_id, what, dst,
+            (const void*)((const char*)dst + bytes));
+    for (i = 0; i < n; i++) {
+        fprintf(stderr, "%s%p", i ? " " : " src ", srcs[i]);
+    }
+    fputc('\n', stderr);
+}
+
 /* the receive's combine: dst = srcs[n-1] (op) (... (srcs[1] (op) srcs[0])) */
 static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *const *srcs,
                              unsigned n)
@@ -312,6 +346,7 @@ static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *cons
     ucs_status_t st = UCS_OK;
     if (c->rma == RMA_DEV) {
         const double t0 = now_s();
+        rma_trace(c, "fold", dst, c->length, srcs, n);
         return slow_note(c, "fold", t0,
                          ucg_builtin_combine_dev_fold(c->g->cmb, c->op, c->dtype, dst,
                                                       srcs, n, (size_t)c->count));
@@ -336,6 +371,7 @@ static ucs_status_t rma_copy(ucg_builtin_lcoll_t *c, void *dst, const void *src)
 {
     if (c->rma == RMA_DEV) {
         const double t0 = now_s();
+        rma_trace(c, "copy", dst, c->length, &src, 1);
         return slow_note(c, "copy", t0,
                          ucg_builtin_combine_dev_copy(c->g->cmb, dst, src, c->length));
     }
@@ -542,6 +578,7 @@ static ucs_status_t rma_butterfly(ucg_builtin_lcoll_t *c, void *dst, const void 
     ucs_status_t st = UCS_OK;
     if (c->rma == RMA_DEV) {
         const double t0 = now_s();
+        rma_trace(c, "butterfly", dst, bytes, srcs, N);
         return slow_note(c, "butterfly", t0,
                          ucg_builtin_combine_dev_butterfly(c->g->cmb, c->op, c->dtype, dst,
                                                            srcs, N, self, n));
@@ -582,6 +619,9 @@ static ucs_status_t rma_copy_n(ucg_builtin_lcoll_t *c, void *const *dsts,
     unsigned i;
     if (c->rma == RMA_DEV) {
         const double t0 = now_s();
+        for (i = 0; i < k; i++) {
+            rma_trace(c, "copy_n", dsts[i], bytes, &srcs[i], 1);
+        }
         return slow_note(c, "copy_n", t0,
                          ucg_builtin_combine_dev_copy_n(c->g->cmb, dsts, srcs, k, bytes));
     }
@@ -879,6 +919,11 @@ UCG_INTERNAL ucs_status_t rma_setup(ucg_builtin_lcoll_t *c, void *rbuf_user)
         }
         c->pool_idx[i] = k;
         c->dbuf[i]     = c->g->pool[k].ptr;
+        if (rma_trace_on()) {
+            fprintf(stderr, "[rma %u] op buffer %u: pool %d %p..%p\n", c->g->my, i, k,
+                    c->g->pool[k].ptr,
+                    (void*)((char*)c->g->pool[k].ptr + c->g->pool[k].bytes));
+        }
         memcpy(c->key[i], c->g->pool[k].key, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
     }
     /* a send buffer the caller took from the group's registered memory is

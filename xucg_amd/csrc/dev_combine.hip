@@ -470,7 +470,15 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
     }
     /* stream_d2h is created on first use (d2h_stream): only the pipeline of
      * a host-resident dst needs it, and every stream can take a hardware
-     * queue of the GPU that other processes share (stalls) */
+     * queue of the GPU that other processes share (stalls).
+     * UCX_BUILTIN_DEV_D2H_STREAM=eager creates it here, as round 1 did (an
+     * A/B knob for the small-op latency) */
+    {
+        const char *k = getenv("UCX_BUILTIN_DEV_D2H_STREAM");
+        if (e == hipSuccess && k && k[0] == 'e') {
+            e = hipStreamCreateWithFlags(&ctx->stream_d2h, hipStreamNonBlocking);
+        }
+    }
     if (e != hipSuccess) {
         st = hip_status(e, "ctx_create");
         ucg_builtin_dev_ctx_destroy(ctx);
