@@ -144,6 +144,17 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
 void         ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *group);
 /* Progress the transport and any pending resends of this group's ops. */
 unsigned     ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *group);
+/* The resend timer of the group's async context (RESEND_TIMER_TICK,
+ * builtin/builtin.c:55-56, 284-294, 408-413): every interval_s a thread of its
+ * own retries the sends of every op that stopped at UCS_ERR_NO_RESOURCE, as
+ * progress does; a step whose sends then complete drains what is stashed for
+ * it, so the combine may run on that thread ("Thread
+ * boundary"). Every entry point of the group takes the group's lock, as the
+ * reference's UCS_ASYNC_BLOCK. Stopped by lgroup_destroy. */
+ucs_status_t ucg_builtin_lgroup_set_async_timer(ucg_builtin_lgroup_t *group,
+                                                double interval_s);
+/* [0] resends made by the timer thread, [1] fragments it combined */
+void         ucg_builtin_lgroup_async_stats(ucg_builtin_lgroup_t *group, uint64_t out[2]);
 
 /* MPI_Allreduce (modifiers AGGREGATE|BROADCAST, api/ucg_mpi.h:53-54), the
  * plan ucg_builtin_choose_topology picks (builtin/builtin.c:112-121):
@@ -198,6 +209,11 @@ void        *ucg_builtin_lgroup_mem_alloc(ucg_builtin_lgroup_t *group, size_t by
 void         ucg_builtin_lgroup_mem_free(ucg_builtin_lgroup_t *group, void *ptr);
 /* ucg_collective_start: UCS_OK if complete, UCS_INPROGRESS, or an error */
 ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *coll);
+/* The same under the collective id base/ hands out (ucg_collective_trigger,
+ * base/ucg_group.c:485-500; ucg_builtin_op_trigger, builtin_control.c:
+ * 1309-1352): every member must start the op under the same id.
+ * UCS_ERR_BUSY when the id's slot (coll_id % 16) still runs an op. */
+ucs_status_t ucg_builtin_lcoll_start_as(ucg_builtin_lcoll_t *coll, uint8_t coll_id);
 /* 1 when the last start completed; its status in *status */
 int          ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *coll,
                                     ucs_status_t *status);

@@ -30,7 +30,8 @@ def test_dev_library_exports_every_declared_symbol():
 
 
 def test_host_library_exports_every_declared_symbol():
-    names = sorted(set(declared("ucg_builtin_combine.h")) | set(declared("ucg_builtin_ops.h")))
+    names = sorted(set(declared("ucg_builtin_combine.h")) | set(declared("ucg_builtin_ops.h")) |
+                   set(declared("ucg_builtin_component.h")))
     assert len(names) >= 10
     lib = ctypes.CDLL(_lib.HOST_LIB)
     missing = [n for n in names if not hasattr(lib, n)]
@@ -61,3 +62,16 @@ def test_version_and_errors_without_gpu():
     assert L.ucg_builtin_dev_reduce(None, 0, 10, None, None, 4) == _lib.UCS_ERR_INVALID_PARAM
     assert L.ucg_builtin_dev_sync(None) == _lib.UCS_ERR_INVALID_PARAM
     assert L.ucg_builtin_dev_stage_end(None) == _lib.UCS_ERR_INVALID_PARAM
+
+
+def test_host_library_exports_the_plan_component():
+    """The drop-in boundary: the global ucg_builtin_component of type
+    ucg_plan_component_t (api/ucg_plan_component.h:141-188, defined as
+    builtin/builtin.c:1007-1016 defines it), already registered in
+    ucg_plan_components_list by its load-time constructor."""
+    lib = ctypes.CDLL(_lib.HOST_LIB)
+    comp = ctypes.c_char.in_dll(lib, "ucg_builtin_component")
+    name = ctypes.string_at(ctypes.addressof(comp), 16).split(b"\0")[0]
+    assert name == b"builtin"
+    head = (ctypes.c_void_p * 2).in_dll(lib, "ucg_plan_components_list")
+    assert head[1] != ctypes.addressof(head), "component not in ucg_plan_components_list"

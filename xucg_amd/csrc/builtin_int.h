@@ -12,6 +12,7 @@
 
 #include "ucg_builtin_ops.h"
 
+#include <pthread.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -199,6 +200,17 @@ struct ucg_builtin_lgroup {
     unsigned                 npool;
     struct rma_imp          *imp;
     unsigned                 nimp;
+    /* the worker's async context (UCS_ASYNC_BLOCK, builtin.c:263-267, 331-335):
+     * every entry point holds this recursive lock, and so does the resend
+     * timer (builtin.c:284-294, 408-413) when it runs on its own thread */
+    pthread_mutex_t          async_lock;
+    pthread_cond_t           timer_cv;
+    pthread_t                timer;
+    int                      timer_on;
+    int                      timer_stop;
+    double                   timer_tick;
+    _Atomic uint64_t         async_resends;
+    _Atomic uint64_t         async_combines;   /* host combines on the timer thread */
 };
 
 struct ucg_builtin_lcoll {

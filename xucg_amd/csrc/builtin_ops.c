@@ -31,6 +31,21 @@ static int  recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
                     size_t length);
 static void step_execute(ucg_builtin_lcoll_t *c);
 
+/* set on the resend timer's thread: what it combines is counted */
+static __thread int on_timer_thread;
+
+/* UCS_ASYNC_BLOCK / UNBLOCK of the group (recursive: completion callbacks and
+ * the stash drain re-enter the engine on the same thread) */
+static inline void group_block(ucg_builtin_lgroup_t *g)
+{
+    pthread_mutex_lock(&g->async_lock);
+}
+
+static inline void group_unblock(ucg_builtin_lgroup_t *g)
+{
+    pthread_mutex_unlock(&g->async_lock);
+}
+
 static stash_t *stash_new(uint64_t header, const void *payload, size_t length)
 {
     stash_t *m = malloc(sizeof(*m) + length);
@@ -413,6 +428,9 @@ static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
     if (offset + length > c->length) {
         st = UCS_ERR_IO_ERROR;          /* a message outside recv.buffer */
     } else if (s->aggregation == AGG_REDUCE) {
+        if (on_timer_thread) {
+            c->g->async_combines++;
+        }
         st = c->step_open ?
              ucg_builtin_combine_fragment(c->g->cmb, offset, data, length) :
              /* ucg_builtin_mpi_reduce_fragment, builtin_comp_step.inl:112-120 */
@@ -544,6 +562,14 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
     if (g == NULL) {
         return UCS_ERR_NO_MEMORY;
     }
+    {
+        pthread_mutexattr_t a;
+        pthread_mutexattr_init(&a);
+        pthread_mutexattr_settype(&a, PTHREAD_MUTEX_RECURSIVE);
+        pthread_mutex_init(&g->async_lock, &a);
+        pthread_mutexattr_destroy(&a);
+        pthread_cond_init(&g->timer_cv, NULL);
+    }
     g->iface    = iface;
     g->group_id = group_id;
     g->size     = member_count;
@@ -603,6 +629,15 @@ void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
     if (g == NULL) {
         return;
     }
+    if (g->timer_on) {
+        /* ucg_context_unset_async_timer, builtin.c:485 */
+        group_block(g);
+        g->timer_stop = 1;
+        pthread_cond_signal(&g->timer_cv);
+        group_unblock(g);
+        pthread_join(g->timer, NULL);
+        g->timer_on = 0;
+    }
     for (i = 0; i < UCG_BUILTIN_OPS_MAX_CONCURRENT; i++) {
         stash_t *m;
         while ((m = g->slots[i].msgs) != NULL) {
@@ -612,13 +647,18 @@ void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
     }
     g->iface->groups[g->group_id % UNEXP_GROUPS] = NULL;
     rma_group_free(g);
+    pthread_cond_destroy(&g->timer_cv);
+    pthread_mutex_destroy(&g->async_lock);
     free(g);
 }
 
-unsigned ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *g)
+/* the resend queue (ucg_builtin_async_resend, builtin.c:270-282): every op
+ * whose sends stopped at UCS_ERR_NO_RESOURCE goes on from where it stopped; a
+ * step whose sends complete drains what is stashed for it, so this may
+ * combine. Called with the group blocked. */
+static unsigned group_resend(ucg_builtin_lgroup_t *g)
 {
-    unsigned n = ucg_builtin_shm_progress(g->iface, am_handler, g->iface), i;
-    /* resend queue (builtin.c:260-294, 329-337) */
+    unsigned i, n = 0;
     for (i = 0; i < UCG_BUILTIN_OPS_MAX_CONCURRENT; i++) {
         ucg_builtin_lcoll_t *c = g->slots[i].req;
         if (c && c->send_pending) {
@@ -632,6 +672,67 @@ unsigned ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *g)
         }
     }
     return n;
+}
+
+/* ucg_builtin_op_progress, builtin.c:318-340: the transport first, then the
+ * resend queue */
+unsigned ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *g)
+{
+    unsigned n;
+    group_block(g);
+    n  = ucg_builtin_shm_progress(g->iface, am_handler, g->iface);
+    n += group_resend(g);
+    group_unblock(g);
+    return n;
+}
+
+/* ucg_builtin_async_check, builtin.c:284-294, on a timer of its own thread
+ * (the UCS async context's timer, set in ucg_builtin_create, :408-413) */
+static void *async_timer(void *arg)
+{
+    ucg_builtin_lgroup_t *g = arg;
+    on_timer_thread = 1;
+    group_block(g);
+    while (!g->timer_stop) {
+        struct timespec ts;
+        double t = now_s() + g->timer_tick;
+        clock_gettime(CLOCK_MONOTONIC, &ts);
+        ts.tv_sec  = (time_t)t;
+        ts.tv_nsec = (long)((t - (double)(time_t)t) * 1e9);
+        pthread_cond_timedwait(&g->timer_cv, &g->async_lock, &ts);
+        if (!g->timer_stop) {
+            g->async_resends += group_resend(g);
+        }
+    }
+    group_unblock(g);
+    return NULL;
+}
+
+ucs_status_t ucg_builtin_lgroup_set_async_timer(ucg_builtin_lgroup_t *g, double interval_s)
+{
+    pthread_condattr_t a;
+    if (g == NULL || interval_s <= 0.0 || g->timer_on) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    /* the timed wait runs on the monotonic clock, like now_s() */
+    pthread_cond_destroy(&g->timer_cv);
+    pthread_condattr_init(&a);
+    pthread_condattr_setclock(&a, CLOCK_MONOTONIC);
+    pthread_cond_init(&g->timer_cv, &a);
+    pthread_condattr_destroy(&a);
+    g->timer_tick = interval_s;
+    g->timer_stop = 0;
+    if (pthread_create(&g->timer, NULL, async_timer, g) != 0) {
+        return UCS_ERR_NO_RESOURCE;
+    }
+    g->timer_on = 1;
+    return UCS_OK;
+}
+
+void ucg_builtin_lgroup_async_stats(ucg_builtin_lgroup_t *g, uint64_t out[2])
+{
+    out[0] = g ? g->async_resends : 0;
+    out[1] = g ? g->async_combines : 0;
 }
 
 void ucg_builtin_lgroup_stats(ucg_builtin_lgroup_t *g, uint64_t out[4])
@@ -711,9 +812,9 @@ static int allreduce_use_tree(unsigned size)
     return (size & (size - 1)) != 0;   /* builtin.c:112-121 */
 }
 
-ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sbuf,
-                                         void *rbuf, int count, void *dtype,
-                                         void *op, ucg_builtin_lcoll_t **coll_p)
+static ucs_status_t lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                    void *rbuf, int count, void *dtype,
+                                    void *op, ucg_builtin_lcoll_t **coll_p)
 {
     ucg_builtin_lcoll_t *c;
     plan_ctx_t pc;
@@ -754,10 +855,10 @@ ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sb
     return UCS_OK;
 }
 
-ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
-                                      void *rbuf, int count, void *dtype,
-                                      void *op, unsigned root,
-                                      ucg_builtin_lcoll_t **coll_p)
+static ucs_status_t lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                 void *rbuf, int count, void *dtype,
+                                 void *op, unsigned root,
+                                 ucg_builtin_lcoll_t **coll_p)
 {
     ucg_builtin_lcoll_t *c;
     plan_ctx_t pc;
@@ -809,24 +910,77 @@ ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
     return UCS_OK;
 }
 
+ucs_status_t ucg_builtin_lcoll_allreduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                         void *rbuf, int count, void *dtype,
+                                         void *op, ucg_builtin_lcoll_t **coll_p)
+{
+    ucs_status_t st;
+    if (g == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    group_block(g);
+    st = lcoll_allreduce(g, sbuf, rbuf, count, dtype, op, coll_p);
+    group_unblock(g);
+    return st;
+}
+
+ucs_status_t ucg_builtin_lcoll_reduce(ucg_builtin_lgroup_t *g, const void *sbuf,
+                                      void *rbuf, int count, void *dtype,
+                                      void *op, unsigned root,
+                                      ucg_builtin_lcoll_t **coll_p)
+{
+    ucs_status_t st;
+    if (g == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    group_block(g);
+    st = lcoll_reduce(g, sbuf, rbuf, count, dtype, op, root, coll_p);
+    group_unblock(g);
+    return st;
+}
+
+static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id);
+
 ucs_status_t ucg_builtin_lcoll_start(ucg_builtin_lcoll_t *c)
 {
-    ucg_builtin_lgroup_t *g;
-    op_slot_t *slot;
-
+    ucs_status_t st;
     if (c == NULL) {
         return UCS_ERR_INVALID_PARAM;
     }
+    group_block(c->g);
+    st = lcoll_start_at(c, c->g->next_coll_id);
+    group_unblock(c->g);
+    return st;
+}
+
+ucs_status_t ucg_builtin_lcoll_start_as(ucg_builtin_lcoll_t *c, uint8_t coll_id)
+{
+    ucs_status_t st;
+    if (c == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    group_block(c->g);
+    st = lcoll_start_at(c, coll_id);
+    group_unblock(c->g);
+    return st;
+}
+
+/* ucg_builtin_op_trigger, builtin_control.c:1309-1352, for the coll_id that
+ * ucg_collective_trigger hands out (base/ucg_group.c:485-500) */
+static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id)
+{
+    ucg_builtin_lgroup_t *g = c->g;
+    op_slot_t *slot;
+
     if (c->active) {
         return UCS_ERR_BUSY;
     }
-    g = c->g;
-    c->coll_id = g->next_coll_id;
-    slot = &g->slots[c->coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
+    slot = &g->slots[coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
     if (slot->req != NULL) {
         return UCS_ERR_BUSY;    /* more than 16 ops outstanding */
     }
-    g->next_coll_id++;          /* ucg_collective_trigger, base/ucg_group.c:485 */
+    c->coll_id      = coll_id;
+    g->next_coll_id = (uint8_t)(coll_id + 1);
     if (c->rma) {
         return rma_start(c, slot);
     }
@@ -917,8 +1071,12 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
             continue;
         }
         if (now_s() - t0 > lim) {
-            timeout_dump(c);
-            finish(c, UCS_ERR_TIMED_OUT);
+            group_block(c->g);
+            if (!c->done) {
+                timeout_dump(c);
+                finish(c, UCS_ERR_TIMED_OUT);
+            }
+            group_unblock(c->g);
             break;
         }
         sched_yield();
@@ -943,10 +1101,17 @@ ucs_status_t ucg_builtin_lcoll_set_completion(ucg_builtin_lcoll_t *c,
 
 void ucg_builtin_lcoll_destroy(ucg_builtin_lcoll_t *c)
 {
-    if (c && c->active) {
+    ucg_builtin_lgroup_t *g;
+    if (c == NULL) {
+        return;
+    }
+    g = c->g;
+    group_block(g);
+    if (c->active) {
         finish(c, UCS_ERR_CANCELED);
     }
     lcoll_free(c);
+    group_unblock(g);
 }
 
 size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)

@@ -96,9 +96,14 @@ HOST_API = {
     "ucg_builtin_lcoll_reduce": (_int, [_vp, _vp, _vp, _int, _vp, _vp, _u,
                                         ctypes.POINTER(_vp)]),
     "ucg_builtin_lcoll_start": (_int, [_vp]),
+    "ucg_builtin_lcoll_start_as": (_int, [_vp, ctypes.c_uint8]),
+    "ucg_builtin_lgroup_set_async_timer": (_int, [_vp, ctypes.c_double]),
+    "ucg_builtin_lgroup_async_stats": (None, [_vp, ctypes.POINTER(_u64)]),
     "ucg_builtin_lcoll_test": (_int, [_vp, ctypes.POINTER(_int)]),
     "ucg_builtin_lcoll_wait": (_int, [_vp]),
     "ucg_builtin_lcoll_destroy": (None, [_vp]),
     "ucg_builtin_lcoll_describe": (_sz, [_vp, ctypes.c_char_p, _sz]),
     "ucg_builtin_lcoll_set_completion": (_int, [_vp, _vp, _vp, _sz, _sz]),
+    # include/ucg_builtin_component.h
+    "ucg_builtin_component_set_classifier": (None, [OP_FN, DT_FN]),
 }
