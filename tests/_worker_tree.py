@@ -145,8 +145,7 @@ def main():
                 f"send send.buffer to {up[0]},")
         if want not in text:
             fail(f"plan differs from the oracle's tree: expected '{want}'")
-    if rank == 0:
-        print(f"stats {group.stats()} combine {cmb.stats()}", flush=True)
+    print(f"stats {group.stats()} combine {cmb.stats()}", flush=True)
     if ring_cells <= 2 and group.stats()["resends"] == 0 and rank == 0:
         fail(f"expected UCS_ERR_NO_RESOURCE resends at the root with {ring_cells} cells")
     group.close()

@@ -13,6 +13,9 @@ from _launch import launch, launch_exe
 from mock_mpi import MockMPI, OPS, DTYPES
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
 def shm_name():
     return f"ucg_test_{os.getpid()}_{uuid.uuid4().hex[:8]}"
 
@@ -122,6 +125,20 @@ def test_c1_harness_host_sanitizers(monkeypatch, world, max_short, plan, incast,
         assert "Sanitizer" not in out and "runtime error" not in out, out
     line = json.loads(outs[0].strip().splitlines()[-1])
     assert line["bit_exact"] and line["ranks"] == world
+
+
+def test_async_resend_timer_combines_on_its_thread():
+    """the resend timer of the group's async context
+    (builtin.c:260-294, 408-413) sends what stopped at UCS_ERR_NO_RESOURCE
+    while the owner makes no call, then drains the stash - the combine runs on
+    the timer's thread (tests/c/async_resend.c); results bit-exact."""
+    exe = os.path.join(ROOT, "tests", "c", "_build", "async_resend")
+    codes, outs = launch_exe(exe, 2, (shm_name(),), timeout=60)
+    assert codes == [0, 0], "\n".join(outs)
+    import json
+    stats = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][0])
+    assert stats["sent_before_sleep"] < 133 and stats["sent_after_sleep"] == 133
+    assert stats["timer_resends"] > 0 and stats["timer_combines"] > 0
 
 
 @pytest.mark.parametrize("world", [3, 4])
@@ -259,6 +276,28 @@ def test_tree_incast_packers(world, max_short, cells, monkeypatch):
     assert "incast (reducing packer)" in outs[1] and "incast (atomic packer)" in outs[1]
     root_plan = [ln for ln in outs[0].splitlines() if "REDUCE_TERMINAL" in ln][0]
     assert "incast" in root_plan
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,max_short,cells", [(5, 8192, 4), (3, 256, 64)])
+def test_tree_incast_packers_device(world, max_short, cells, monkeypatch):
+    """The SM-root packers on the GPU box (SURVEY 8a row a13, 8f row f4;
+    builtin_pack.c:50-72, 100-148): with every combine forced onto the device,
+    a child's reducing packer combines its data into the root's incast cell
+    through the device path (H2D -> kernel -> D2H on the cell), the atomic
+    packer adds unsigned SUMs into the zeroed cell; results bit-exact against
+    the oracle's tree."""
+    monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", "y")
+    codes, outs = launch("_worker_tree.py", world, args=(shm_name(), "dev", max_short, cells),
+                         timeout=300)
+    assert codes == [0] * world, "\n".join(outs)
+    d = _digests(outs)
+    assert all(x == d[0] for x in d) and d[0], d
+    assert "incast (reducing packer)" in outs[1] and "incast (atomic packer)" in outs[1]
+    # a child's packers combined on the device
+    stats = [ln for ln in outs[world - 1].splitlines() if ln.startswith("stats ")][0]
+    dev_calls = int(stats.split("'dev_calls': ")[1].split(",")[0])
+    assert dev_calls > 0, stats
 
 
 @pytest.mark.gpu
