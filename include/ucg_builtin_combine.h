@@ -67,6 +67,15 @@ typedef struct ucg_builtin_combine_config {
                                 0, n, never: UCG_BUILTIN_DEV_ZCOPY_NEVER)      */
     int      completion;     /* UCX_BUILTIN_DEV_COMPLETION   signal|sync (default
                                 signal: UCG_BUILTIN_DEV_COMPLETION_*)          */
+    void    *stream;         /* the caller's HIP stream (hipStream_t), or NULL:
+                                the device work of this combine - kernels over
+                                the caller's device buffers included - is then
+                                queued behind the caller's own work on it, so
+                                buffers produced asynchronously there are read
+                                only once written. NULL = a private stream
+                                (the caller must then complete its work on the
+                                buffers before starting an op). Not read from
+                                the environment. */
 } ucg_builtin_combine_config_t;
 
 typedef struct ucg_builtin_combine ucg_builtin_combine_t;

@@ -557,10 +557,16 @@ static uint64_t gen_bits(int dt, int dist, uint64_t h)
 
 void ucg_oracle_fill(int dt, int dist, uint64_t seed, void *dst, size_t count)
 {
+    ucg_oracle_fill_range(dt, dist, seed, 0, dst, count);
+}
+
+void ucg_oracle_fill_range(int dt, int dist, uint64_t seed, size_t start, void *dst,
+                           size_t count)
+{
     uint64_t key = ucg_oracle_splitmix64(seed);
     size_t sz = ucg_oracle_dtype_size(dt), i;
     for (i = 0; i < count; i++) {
-        uint64_t b = gen_bits(dt, dist, ucg_oracle_splitmix64(key ^ (uint64_t)i));
+        uint64_t b = gen_bits(dt, dist, ucg_oracle_splitmix64(key ^ (uint64_t)(start + i)));
         switch (sz) {
         case 1: ((uint8_t*)dst)[i]  = (uint8_t)b;  break;
         case 2: ((uint16_t*)dst)[i] = (uint16_t)b; break;

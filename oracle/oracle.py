@@ -66,6 +66,8 @@ def lib():
         L.ucg_oracle_tree_intra.restype = i
         L.ucg_oracle_fill.argtypes = [i, i, u64, vp, sz]
         L.ucg_oracle_fill.restype = None
+        L.ucg_oracle_fill_range.argtypes = [i, i, u64, sz, vp, sz]
+        L.ucg_oracle_fill_range.restype = None
         L.ucg_oracle_is_supported.argtypes = [i, i]
         L.ucg_oracle_is_supported.restype = i
         L.ucg_oracle_dtype_size.argtypes = [i]
@@ -118,6 +120,14 @@ def fill(dt, dist, seed, count):
     out = np.empty(count, dtype=storage(dt))
     d = DISTS.index(dist) if isinstance(dist, str) else int(dist)
     lib().ucg_oracle_fill(dt_index(dt), d, seed, out.ctypes.data, count)
+    return out
+
+
+def fill_range(dt, dist, seed, start, count):
+    """Elements [start, start + count) of fill(dt, dist, seed, ...)."""
+    out = np.empty(count, dtype=storage(dt))
+    d = DISTS.index(dist) if isinstance(dist, str) else int(dist)
+    lib().ucg_oracle_fill_range(dt_index(dt), d, seed, start, out.ctypes.data, count)
     return out
 
 

@@ -126,6 +126,8 @@ static int run(char **argv)
     ucg_builtin_lgroup_destroy(g);
     ucg_builtin_shm_iface_close(iface);
     ucg_builtin_combine_destroy(cmb);
+    free(in);
+    free(out);
     printf("rank %u: %s\n", rank, ok ? "ok" : "FAILED");
     return ok ? 0 : 1;
 }

@@ -67,7 +67,7 @@ int main(int argc, char **argv)
     unsigned world   = (unsigned)atoi(getenv("WORLD_SIZE") ? getenv("WORLD_SIZE") : "1");
     ucg_builtin_reduce_params_t rp = {mini_reduce, is_sum, no, yes, convert,
                                       is_int, is_fp};
-    ucg_builtin_combine_config_t cfg = {0, 1u << 20, 8u << 20, 4, -1, 0, 0};
+    ucg_builtin_combine_config_t cfg = {0, 1u << 20, 8u << 20, 4, -1, 0, 0, NULL};
     ucg_builtin_combine_t *cmb;
     ucg_builtin_shm_iface_t *iface;
     ucg_builtin_lgroup_t *g;

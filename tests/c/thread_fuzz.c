@@ -168,7 +168,7 @@ int main(int argc, char **argv)
     ucg_builtin_reduce_params_t rp = {reduce_cb, is_sum, no, yes, convert, is_int, is_fp};
     /* force: host buffers of any size staged on the GPU; small slots and a
      * shallow ring so steps and whole-buffer calls share and reuse slots */
-    ucg_builtin_combine_config_t cfg = {2, 0, 4096, 3, -1, 0, 0};
+    ucg_builtin_combine_config_t cfg = {2, 0, 4096, 3, -1, 0, 0, NULL};
     pthread_t th[4];
     uint64_t st[6];
     int i;

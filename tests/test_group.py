@@ -208,3 +208,29 @@ def test_oneshot_allreduce_schedule(variant, world, dt, op, count):
             pushes = [c for c in calls[r] if c[0] == "copy_multi"]
             assert sum(n for _, n, _ in pushes) == 2 * (world - 1)
             assert len(pushes) <= 3
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_collective_contract_over_gloo(world):
+    """bench.py --gpus N > 1 fails loudly: a phase that raises on one rank is
+    an error on every rank, every error and every False parity flag lands in
+    collective_failures (collective_ok false, non-zero exit), and the C5
+    phases' sampled parity check (host evaluation of the plan's association)
+    agrees with the oracle and catches one changed element."""
+    codes, outs = launch("_worker_bench_contract.py", world, timeout=120)
+    assert codes == [0] * world, "\n".join(outs)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["oneshot", "steps"])
+def test_c5_engine_512mib_fp64_sampled_oracle(mode):
+    """BASELINE config 5 at full size per member (512 MiB fp64), 8 members on
+    the one GPU: the engine's allreduce on device buffers - one-shot RS + AG
+    (default) or the plan's recursive-doubling steps - bit-exact against the
+    oracle's association on 18 sampled 64 KiB windows of regenerated inputs."""
+    import uuid
+    codes, outs = launch("_worker_c5.py", 8,
+                         args=(f"ucg_c5_{uuid.uuid4().hex[:8]}", 1 << 26, mode), timeout=240)
+    assert codes == [0] * 8, "\n".join(outs)
+    executed = "one-shot" in outs[0]
+    assert executed == (mode == "oneshot"), outs[0]

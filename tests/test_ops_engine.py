@@ -141,6 +141,27 @@ def test_async_resend_timer_combines_on_its_thread():
     assert stats["timer_resends"] > 0 and stats["timer_combines"] > 0
 
 
+@pytest.mark.parametrize("exe,world,args", [("component_test", 4, ("host",)),
+                                             ("component_test", 3, ("host",)),
+                                             ("async_resend", 2, None)])
+def test_component_and_timer_host_sanitizers(monkeypatch, exe, world, args):
+    """The plan component driven through its vtable, and the resend timer
+    thread, with the engine rebuilt under ASan + UBSan."""
+    import fcntl
+    import subprocess
+    cdir = os.path.join(os.path.dirname(__file__), "c")
+    with open(os.path.join(cdir, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", cdir, "asan"], check=True)
+    monkeypatch.setenv("ASAN_OPTIONS", "detect_leaks=1:abort_on_error=0")
+    monkeypatch.setenv("UBSAN_OPTIONS", "print_stacktrace=1")
+    codes, outs = launch_exe(os.path.join(cdir, "_build", "asan", exe), world,
+                             args if args else (shm_name(),), timeout=120)
+    assert codes == [0] * world, "\n".join(outs)
+    for out in outs:
+        assert "Sanitizer" not in out and "runtime error" not in out, out
+
+
 @pytest.mark.parametrize("world", [3, 4])
 def test_completion_callback_and_flags(world):
     """ucg_params_t.completion (api/ucg.h:162-171) as

@@ -115,6 +115,7 @@ void ucg_builtin_combine_config_read(ucg_builtin_combine_config_t *cfg)
         cfg->completion = (c && !strcasecmp(c, "sync")) ? UCG_BUILTIN_DEV_COMPLETION_SYNC :
                                                           UCG_BUILTIN_DEV_COMPLETION_SIGNAL;
     }
+    cfg->stream = NULL;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -143,7 +144,7 @@ ucs_status_t ucg_builtin_combine_create(const ucg_builtin_reduce_params_t *param
     if (cmb->cfg.dev_enable && ucg_builtin_dev_device_count() > 0) {
         ucg_builtin_dev_ctx_params_t dp = {
             .device      = cmb->cfg.device,
-            .stream      = NULL,
+            .stream      = cmb->cfg.stream,
             .stage_bytes = cmb->cfg.stage_bytes,
             .stage_slots = cmb->cfg.stage_slots,
             .zcopy_bytes = cmb->cfg.zcopy_bytes,

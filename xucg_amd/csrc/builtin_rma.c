@@ -7,8 +7,11 @@
 #define _GNU_SOURCE
 #include "builtin_int.h"
 
+#include <dirent.h>
+#include <errno.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -80,12 +83,36 @@ typedef struct {
 _Static_assert(sizeof(shm_key_t) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES, "shm key size");
 #define SHM_KEY_MAGIC 0x4d485358u
 
+/* segments of processes that died before their group was destroyed (a
+ * killed worker): removed once per process, before its first segment */
+static void shm_seg_sweep(void)
+{
+    static _Atomic int done;
+    DIR *d;
+    struct dirent *e;
+    if (atomic_exchange(&done, 1) || (d = opendir("/dev/shm")) == NULL) {
+        return;
+    }
+    while ((e = readdir(d)) != NULL) {
+        char path[300];
+        int pid;
+        unsigned q;
+        if (sscanf(e->d_name, "xucg_rma_%d_%u", &pid, &q) == 2 && pid > 0 &&
+            kill(pid, 0) != 0 && errno == ESRCH) {
+            snprintf(path, sizeof(path), "/%s", e->d_name);
+            shm_unlink(path);
+        }
+    }
+    closedir(d);
+}
+
 static void *shm_seg_alloc(size_t bytes, void *key)
 {
     static _Atomic unsigned seq;
     shm_key_t k;
     void *p;
     int fd;
+    shm_seg_sweep();
     memset(&k, 0, sizeof(k));
     k.magic = SHM_KEY_MAGIC;
     k.bytes = bytes;
@@ -1023,12 +1050,15 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     return c->done ? c->status : UCS_INPROGRESS;
 }
 
-/* the op's buffers go back to the group's pool; peers' mappings stay */
+/* the op's buffers go back to the group's pool; peers' mappings stay. A
+ * buffer that peers may still be reading - the op ended before every DONE
+ * came back (destroyed while running, a timeout, an error) - stays taken
+ * until the group is destroyed, so that no later op writes it under them */
 UCG_INTERNAL void rma_free(ucg_builtin_lcoll_t *c)
 {
     unsigned i;
     for (i = 0; i < 2; i++) {
-        if (c->pool_idx[i] >= 0) {
+        if (c->pool_idx[i] >= 0 && c->readers[i] == 0) {
             c->g->pool[c->pool_idx[i]].busy = 0;
         }
     }

@@ -563,6 +563,9 @@ ucs_status_t ucg_builtin_dev_complete(ucg_builtin_dev_ctx_t *ctx)
     if (ctx == nullptr) {
         return set_error(UCS_ERR_INVALID_PARAM, "complete", "ctx is NULL");
     }
+    /* the sequence number, the queued flag and the lazily allocated word are
+     * shared with the staged steps (stage_begin/end, combine, combine_host) */
+    std::lock_guard<std::mutex> g(ctx->lock);
     ctx->queued = true;          /* whatever was launched since the last wait */
     return stream_complete(ctx, true);
 }

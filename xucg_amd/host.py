@@ -38,12 +38,16 @@ def read_config():
 
 
 def make_config(dev_enable=1, dev_min_bytes=1 << 20, stage_bytes=8 << 20,
-                stage_slots=4, device=-1, zcopy_bytes=0, completion="signal"):
+                stage_slots=4, device=-1, zcopy_bytes=0, completion="signal",
+                stream=None):
     """zcopy_bytes: 0 = the device library's default (64 KiB), None = never;
-    completion: "signal" (pinned completion word) or "sync" (stage_end)"""
+    completion: "signal" (pinned completion word) or "sync" (stage_end);
+    stream: the caller's HIP stream (an int, e.g. torch's
+    current_stream().cuda_stream) the device work is queued on, None = a
+    private one"""
     zc = _lib.ZCOPY_NEVER if zcopy_bytes is None else zcopy_bytes
     return CombineConfig(dev_enable, dev_min_bytes, stage_bytes, stage_slots, device, zc,
-                         _lib.COMPLETION[completion])
+                         _lib.COMPLETION[completion], stream)
 
 
 class BuiltinCombine:
@@ -54,6 +58,7 @@ class BuiltinCombine:
 
     def __init__(self, callbacks, config=None, op_classifier=None,
                  dt_classifier=None):
+        self.stream = getattr(config, "stream", None) if config is not None else None
         cb = callbacks
         # keep every ctypes thunk alive for the lifetime of the object
         self._thunks = []

@@ -33,7 +33,7 @@ class CombineConfig(ctypes.Structure):
     _fields_ = [("dev_enable", ctypes.c_int), ("dev_min_bytes", _sz),
                 ("stage_bytes", _sz), ("stage_slots", ctypes.c_uint),
                 ("device", ctypes.c_int), ("zcopy_bytes", _sz),
-                ("completion", ctypes.c_int)]
+                ("completion", ctypes.c_int), ("stream", _vp)]
 
 
 HOST_API = {

@@ -117,11 +117,33 @@ def _addr(x):
     return x.ptr
 
 
+def _torch_cuda(*bufs):
+    return any(getattr(b, "is_cuda", False) for b in bufs)
+
+
 class _Collective:
     """A persistent collective of the builtin planner (status != 0: the
-    create call failed and `handle` is None)."""
+    create call failed and `handle` is None).
+
+    Torch CUDA tensors as buffers: the engine's device work runs on the
+    combine's stream (host.make_config(stream=...)), so work torch queued on
+    another stream that produces the send buffer must be complete first:
+    start() synchronizes torch's current stream unless it is the combine's."""
+
+    _torch_sync = False
+    _stream = None
+
+    def _note_buffers(self, group, *bufs):
+        if _torch_cuda(*bufs):
+            self._torch_sync = True
+            self._stream = getattr(group.combine, "stream", None)
 
     def start(self):
+        if self._torch_sync:
+            import torch
+            cur = torch.cuda.current_stream()
+            if not self._stream or cur.cuda_stream != self._stream:
+                cur.synchronize()
         return _lib.host().ucg_builtin_lcoll_start(self.handle)
 
     def wait(self):
@@ -163,6 +185,7 @@ class Allreduce(_Collective):
         self.status = _lib.host().ucg_builtin_lcoll_allreduce(
             group.handle, _addr(sbuf), _addr(rbuf), count, dtype, op, ctypes.byref(h))
         self.handle = h.value if self.status == 0 else None
+        self._note_buffers(group, sbuf, rbuf)
 
 
 class Reduce(_Collective):
@@ -175,3 +198,4 @@ class Reduce(_Collective):
             group.handle, _addr(sbuf), 0 if rbuf is None else _addr(rbuf), count,
             dtype, op, root, ctypes.byref(h))
         self.handle = h.value if self.status == 0 else None
+        self._note_buffers(group, sbuf, rbuf)
