@@ -305,6 +305,15 @@ void        *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
 void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 void        *ucg_builtin_dev_host_alloc(size_t bytes);      /* pinned */
 void         ucg_builtin_dev_host_free(void *ptr);
+/* Page-lock a caller's host buffer for DMA (hipHostRegister): the memory
+ * registration of the reference's zero-copy optimisation (uct_md_mem_reg after
+ * MEM_REG_OPT_CNT uses of an op, builtin_control.c:276-286, 345-373). A
+ * staged step's H2D / D2H of a registered recv buffer then moves by DMA with
+ * no staging copy in the runtime. The buffer must stay allocated until
+ * unregistered. */
+ucs_status_t ucg_builtin_dev_host_register(ucg_builtin_dev_ctx_t *ctx, void *ptr,
+                                           size_t bytes);
+ucs_status_t ucg_builtin_dev_host_unregister(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                     const void *src, size_t bytes); /* sync */
 

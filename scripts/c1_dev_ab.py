@@ -5,9 +5,10 @@ same command as bench.py's extra.c1_loopback_allreduce_4kib_fp32
 
     python scripts/c1_dev_ab.py OUT.json [reps]
 
-Settings: the default library, and UCX_BUILTIN_DEV_D2H_STREAM=eager (the
-context's second stream created at create time, as before commit b153abf),
-and the completion by hipStreamSynchronize (UCX_BUILTIN_DEV_COMPLETION=sync).
+Settings: the default library (the context's second stream created with it),
+UCX_BUILTIN_DEV_D2H_STREAM=lazy (created on first use, round 2's default),
+the same with GPU_MAX_HW_QUEUES=2, the default with GPU_MAX_HW_QUEUES=1, and
+the completion by hipStreamSynchronize (UCX_BUILTIN_DEV_COMPLETION=sync).
 The parent never touches the GPU: ranks are child processes."""
 import json
 import os
@@ -40,7 +41,9 @@ def run(world, count, iters, env_extra):
 
 def main():
     out, reps = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    settings = {"default": {}, "d2h_eager": {"UCX_BUILTIN_DEV_D2H_STREAM": "eager"},
+    settings = {"default": {}, "d2h_lazy": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy"},
+                "d2h_lazy_hwq2": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy", "GPU_MAX_HW_QUEUES": "2"},
+                "hwq1": {"GPU_MAX_HW_QUEUES": "1"},
                 "sync": {"UCX_BUILTIN_DEV_COMPLETION": "sync"}}
     res = {k: {"4kib_us": [], "64mib_us": []} for k in settings}
     for rep in range(reps):

@@ -15,8 +15,8 @@ for S in "$@"; do
   case $S in
   suite)
     step suite
-    timeout -k 10 900 python -u -m pytest tests -v -m gpu --timeout 250 \
-        --timeout-method thread -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+    timeout -k 10 1000 python -u -m pytest tests -v -m gpu --timeout 250 \
+        --timeout-method thread -p no:cacheprovider --durations=40 > $OUT/pytest_gpu.log 2>&1
     rc=$?; tail -3 $OUT/pytest_gpu.log; grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -20
     [ $rc -eq 0 ] || exit $rc ;;
   c1ab)
@@ -34,7 +34,7 @@ for S in "$@"; do
         > $OUT/c1prof_rank$r.log 2>&1 &
     done
     RANK=0 WORLD_SIZE=4 C1_DEVICE_BUFFERS=1 C1_REGISTERED=1 UCX_BUILTIN_WAIT_TIMEOUT=60 \
-      timeout -k 5 150 taskset -c ${CPUS[0]} rocprofv3 --kernel-trace --stats -d $OUT/c1prof \
+      timeout -k 5 150 taskset -c ${CPUS[0]} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/c1prof \
       -o c1 -- tests/c/_build/c1_allreduce $NAME 2000 256 1024 > $OUT/c1prof_rank0.log 2>&1
     rc=$?; wait; tail -2 $OUT/c1prof_rank0.log; [ $rc -eq 0 ] || exit $rc ;;
   bench)
@@ -47,6 +47,10 @@ print(d['value'], r['frac'], r['kernel_avg_us'], json.dumps({k: v.get('latency_u
   benchfull)
     step benchfull
     timeout -k 10 500 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; } ;;
+  stage)
+    step stage
+    timeout -k 10 300 tests/c/_build/stage_bench $((64<<20)) 8184 5 > $OUT/stage_bench.json 2> $OUT/stage_bench.err || { tail -5 $OUT/stage_bench.err; exit 1; }
+    cut -c1-400 $OUT/stage_bench.json ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }

@@ -143,6 +143,49 @@ int main(int argc, char **argv)
         ucg_oracle_reduce_fragmented(ORA_SUM, ORA_F32, src, want, n, frag);
         t_cpu[i] = now_s() - t0;
     }
+    /* the same step with the recv buffer registered (hipHostRegister, as a
+     * persistent op registers it after MEM_REG_OPT_CNT starts): its H2D and
+     * D2H move by DMA. Beside it, the floors of the staged step on this host:
+     * copying every borrowed fragment into pinned memory (the ring copy), and
+     * the recv buffer's H2D and D2H from registered memory. */
+    double t_reg[MAXREPS], t_memcpy[MAXREPS], t_h2d[MAXREPS], t_d2h[MAXREPS];
+    {
+        char *pin = ucg_builtin_dev_host_alloc(total);
+        void *dbuf = ucg_builtin_dev_malloc(ctx[ZC], total);
+        size_t off;
+        if (pin == NULL || dbuf == NULL ||
+            ucg_builtin_dev_host_register(ctx[ZC], dst, total) != UCS_OK) {
+            fprintf(stderr, "register: %s\n", ucg_builtin_dev_last_error());
+            return 1;
+        }
+        memcpy(dst, ref, total);
+        memcpy(want, ref, total);
+        ucg_oracle_reduce_fragmented(ORA_SUM, ORA_F32, src, want, n, frag);
+        if (staged_step(ctx[ZC], dst, src, total, frag) != 0) {
+            return 1;
+        }
+        ok &= memcmp(dst, want, total) == 0;
+        for (i = 0; i < reps; i++) {
+            t0 = now_s();
+            staged_step(ctx[ZC], dst, src, total, frag);
+            t_reg[i] = now_s() - t0;
+            t0 = now_s();
+            for (off = 0; off < total; off += frag) {
+                size_t m = total - off < frag ? total - off : frag;
+                memcpy(pin + off, (const char*)src + off, m);
+            }
+            t_memcpy[i] = now_s() - t0;
+            t0 = now_s();
+            ucg_builtin_dev_memcpy(ctx[ZC], dbuf, dst, total);
+            t_h2d[i] = now_s() - t0;
+            t0 = now_s();
+            ucg_builtin_dev_memcpy(ctx[ZC], dst, dbuf, total);
+            t_d2h[i] = now_s() - t0;
+        }
+        ucg_builtin_dev_host_unregister(ctx[ZC], dst);
+        ucg_builtin_dev_free(ctx[ZC], dbuf);
+        ucg_builtin_dev_host_free(pin);
+    }
     /* cost of the memory-kind query the dispatcher makes per step (and per
      * whole-buffer combine): pageable host memory and device memory */
     double mk_host_ns, mk_dev_ns;
@@ -263,7 +306,11 @@ int main(int argc, char **argv)
             md[c] = median(t_step[c], reps);
         }
         cpu_md = median(t_cpu, reps);
-        printf("{\"config\": \"f1 staged REDUCE step, fp32 SUM, pageable host buffers\", "
+        printf("{\"device_staged_ms_registered_recv\": %.3f, \"fragment_memcpy_ms\": %.3f, "
+               "\"h2d_registered_ms\": %.3f, \"d2h_registered_ms\": %.3f, ",
+               median(t_reg, reps) * 1e3, median(t_memcpy, reps) * 1e3,
+               median(t_h2d, reps) * 1e3, median(t_d2h, reps) * 1e3);
+        printf("\"config\": \"f1 staged REDUCE step, fp32 SUM, pageable host buffers\", "
                "\"bytes\": %zu, \"fragment_bytes\": %zu, \"fragments\": %zu, \"reps\": %d, "
                "\"device_staged_ms\": %.3f, \"device_staged_gibs_n\": %.2f, "
                "\"device_staged_ms_range\": [%.3f, %.3f], "

@@ -23,3 +23,24 @@ def dev_ctx():
     ctx = xucg_amd.DevContext(device=0)
     yield ctx
     ctx.close()
+
+
+@pytest.fixture
+def in_child(request):
+    """For GPU tests that initialise torch's device context: in the pytest
+    process, run this test in a child pytest and return True (the caller then
+    returns at once); in that child return False (run the body). torch's
+    context held by the pytest process for the rest of the session slowed the
+    multi-process device tests that follow it (stalls)."""
+    import subprocess
+
+    def run():
+        if os.environ.get("XUCG_IN_CHILD") == request.node.nodeid:
+            return False
+        env = dict(os.environ, XUCG_IN_CHILD=request.node.nodeid)
+        p = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider",
+                            "-m", "gpu", request.node.nodeid], cwd=ROOT, env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0 and " passed" in p.stdout, p.stdout[-3000:] + p.stderr[-2000:]
+        return True
+    return run

@@ -299,12 +299,15 @@ def test_thread_fuzz_c_harness_bit_exact():
 
 
 @pytest.mark.gpu
-def test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu():
+def test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu(in_child):
     """UCX_BUILTIN_DEV_COMBINE=y (default): a host recv buffer is combined by
     reduce_cb_f (staging would cross PCIe); a device-resident one
     (GPU-aware MPI) on the GPU in place, whatever its size, with a host or a
     device src; an op the device cannot classify is refused for device
-    memory (the host callback cannot dereference it)."""
+    memory (the host callback cannot dereference it). Torch tensors: runs in
+    a child process."""
+    if in_child():
+        return
     import torch
     from xucg_amd import _lib
     mpi = MockMPI()
@@ -339,9 +342,12 @@ def test_default_policy_host_buffers_stay_on_host_device_buffers_on_gpu():
 
 
 @pytest.mark.gpu
-def test_staged_step_into_device_resident_recv_buffer():
+def test_staged_step_into_device_resident_recv_buffer(in_child):
     """A fragmented step whose recv buffer is device memory accumulates into
-    it in place (no mirror copies), bit-exact with the host callback."""
+    it in place (no mirror copies), bit-exact with the host callback. Torch
+    tensors: runs in a child process."""
+    if in_child():
+        return
     import torch
     n = (1 << 20) + 3
     frag = host.fragment_length(8192, 4)

@@ -89,6 +89,8 @@ DEV_API = {
     "ucg_builtin_dev_free": (None, [_vp, _vp]),
     "ucg_builtin_dev_host_alloc": (_vp, [_sz]),
     "ucg_builtin_dev_host_free": (None, [_vp]),
+    "ucg_builtin_dev_host_register": (_int, [_vp, _vp, _sz]),
+    "ucg_builtin_dev_host_unregister": (_int, [_vp, _vp]),
     "ucg_builtin_dev_memcpy": (_st, [_vp, _vp, _vp, _sz]),
     "ucg_builtin_dev_fill": (_st, [_vp, _int, _int, _u64, _vp, _sz]),
     "ucg_builtin_dev_profile_reduce": (_st, [_vp, _int, _int, _vp, _vp, _sz, _u,

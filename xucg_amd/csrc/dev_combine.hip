@@ -468,14 +468,14 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
             e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
         }
     }
-    /* stream_d2h is created on first use (d2h_stream): only the pipeline of
-     * a host-resident dst needs it, and every stream can take a hardware
-     * queue of the GPU that other processes share (stalls).
-     * UCX_BUILTIN_DEV_D2H_STREAM=eager creates it here, as round 1 did (an
-     * A/B knob for the small-op latency) */
+    /* The D2H stream of the host pipeline is created here, with the compute
+     * stream. Created on first use instead (UCX_BUILTIN_DEV_D2H_STREAM=lazy,
+     * round 2's default), every small device op of the remote-key steps took
+     * 55-61 us instead of 11-12 us: the completion kernel behind a 5-us fold
+     * ran for 50 us (rocprofv3 trace, profiles/r03/r03a). */
     {
         const char *k = getenv("UCX_BUILTIN_DEV_D2H_STREAM");
-        if (e == hipSuccess && k && k[0] == 'e') {
+        if (e == hipSuccess && !(k && k[0] == 'l')) {
             e = hipStreamCreateWithFlags(&ctx->stream_d2h, hipStreamNonBlocking);
         }
     }
@@ -1388,6 +1388,34 @@ void ucg_builtin_dev_host_free(void *ptr)
     if (ptr) {
         (void)hipHostFree(ptr);
     }
+}
+
+ucs_status_t ucg_builtin_dev_host_register(ucg_builtin_dev_ctx_t *ctx, void *ptr,
+                                           size_t bytes)
+{
+    if (ctx == nullptr || ptr == nullptr || bytes == 0) {
+        return set_error(UCS_ERR_INVALID_PARAM, "host_register", "bad arguments");
+    }
+    ucs_status_t st = set_device(ctx);
+    if (st != UCS_OK) {
+        return st;
+    }
+    HIP_TRY(hipHostRegister(ptr, bytes, hipHostRegisterDefault));
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_host_unregister(ucg_builtin_dev_ctx_t *ctx, void *ptr)
+{
+    if (ctx == nullptr || ptr == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "host_unregister", "bad arguments");
+    }
+    /* no copy of this context may still read or write it */
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (ctx->stream_d2h) {
+        HIP_TRY(hipStreamSynchronize(ctx->stream_d2h));
+    }
+    HIP_TRY(hipHostUnregister(ptr));
+    return UCS_OK;
 }
 
 ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
