@@ -85,6 +85,17 @@ ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *iface,
                                        unsigned expected, size_t length,
                                        ucg_builtin_pack_cb_f pack, void *arg,
                                        int concurrent);
+/* The batched incast (UCX_BUILTIN_SM_INCAST=batched when the iface is
+ * opened): the `expected` children of `root` each copy their message into a
+ * slot of one cell of the root, and the root's progress delivers the cell as
+ * ONE message of `expected` records - the reference's BATCHED_DATA receive
+ * (builtin_comp_step.inl:242-273), where the root reduces every chunk itself:
+ * [payload 0][header 1][payload 1]...[header n-1][payload n-1] after the
+ * first header, records in arrival order. */
+ucs_status_t ucg_builtin_shm_am_incast_batched(ucg_builtin_shm_iface_t *iface,
+                                               unsigned root, uint64_t header,
+                                               unsigned expected, const void *payload,
+                                               size_t length);
 /* Blocking barrier of all members (set-up / tear-down only). */
 void         ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *iface);
 

@@ -51,6 +51,10 @@ print(d['value'], r['frac'], r['kernel_avg_us'], json.dumps({k: v.get('latency_u
     step stage
     timeout -k 10 300 tests/c/_build/stage_bench $((64<<20)) 8184 5 > $OUT/stage_bench.json 2> $OUT/stage_bench.err || { tail -5 $OUT/stage_bench.err; exit 1; }
     cut -c1-400 $OUT/stage_bench.json ;;
+  multi)
+    step multi
+    bash scripts/multi_pmc.sh $OUT/multi > $OUT/multi.log 2>&1 || { tail -5 $OUT/multi.log; exit 1; }
+    grep -E "%|MiB" $OUT/multi/tune_multi_24.txt ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }

@@ -299,26 +299,53 @@ def test_tree_incast_packers(world, max_short, cells, monkeypatch):
     assert "incast" in root_plan
 
 
+@pytest.mark.parametrize("world,max_short,cells", [(3, 256, 64), (5, 64, 64), (7, 256, 2),
+                                                 (6, 8192, 4)])
+def test_tree_incast_batched(world, max_short, cells, monkeypatch):
+    """The BATCHED_DATA receive (builtin_comp_step.inl:242-273, SURVEY 8a row
+    a4): every child copies its fragment into its own slot of one cell at the
+    root, which receives the cell as one message and reduces the children's
+    chunks in arrival order; integer and exact-fp results bit-exact against
+    the oracle's tree, rounded fp within tolerance and identical on every
+    member."""
+    monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", "batched")
+    codes, outs = launch("_worker_tree.py", world, args=(shm_name(), "host", max_short, cells),
+                         timeout=240)
+    assert codes == [0] * world, "\n".join(outs)
+    d = _digests(outs)
+    assert all(x == d[0] for x in d) and d[0], d
+    assert "incast (batched packer)" in outs[1]
+    root_plan = [ln for ln in outs[0].splitlines() if "REDUCE_TERMINAL" in ln][0]
+    assert "incast (batched)" in root_plan
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,max_short,cells", [(5, 8192, 4), (3, 256, 64)])
-def test_tree_incast_packers_device(world, max_short, cells, monkeypatch):
+@pytest.mark.parametrize("world,max_short,cells,incast", [(5, 8192, 4, "y"), (3, 256, 64, "y"),
+                                                        (5, 8192, 4, "batched")])
+def test_tree_incast_packers_device(world, max_short, cells, incast, monkeypatch):
     """The SM-root packers on the GPU box (SURVEY 8a row a13, 8f row f4;
     builtin_pack.c:50-72, 100-148): with every combine forced onto the device,
     a child's reducing packer combines its data into the root's incast cell
     through the device path (H2D -> kernel -> D2H on the cell), the atomic
     packer adds unsigned SUMs into the zeroed cell; results bit-exact against
     the oracle's tree."""
-    monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", "y")
+    monkeypatch.setenv("UCX_BUILTIN_SM_INCAST", incast)
     codes, outs = launch("_worker_tree.py", world, args=(shm_name(), "dev", max_short, cells),
                          timeout=300)
     assert codes == [0] * world, "\n".join(outs)
     d = _digests(outs)
     assert all(x == d[0] for x in d) and d[0], d
-    assert "incast (reducing packer)" in outs[1] and "incast (atomic packer)" in outs[1]
-    # a child's packers combined on the device
-    stats = [ln for ln in outs[world - 1].splitlines() if ln.startswith("stats ")][0]
+    if incast == "y":
+        assert "incast (reducing packer)" in outs[1] and "incast (atomic packer)" in outs[1]
+        # a child's packers combined on the device
+        stats = [ln for ln in outs[world - 1].splitlines() if ln.startswith("stats ")][0]
+    else:
+        # batched: the root combines every child's chunk, staged on the device
+        assert "incast (batched packer)" in outs[1]
+        stats = [ln for ln in outs[0].splitlines() if ln.startswith("stats ")][0]
     dev_calls = int(stats.split("'dev_calls': ")[1].split(",")[0])
-    assert dev_calls > 0, stats
+    dev_steps = int(stats.split("'dev_steps': ")[1].split(",")[0])
+    assert dev_calls + dev_steps > 0, stats
 
 
 @pytest.mark.gpu

@@ -75,6 +75,7 @@ struct ucg_builtin_shm_iface {
     unsigned  cells;
     size_t    ring_bytes;
     size_t    incast_cell_size;
+    int       incast_batched;  /* cells hold every child's message side by side */
     size_t    incast_bytes;    /* one member's incast area */
     size_t    incast_base;     /* offset of member 0's incast area */
     size_t    seg_bytes;
@@ -141,7 +142,7 @@ typedef enum { AGG_NOP, AGG_REDUCE, AGG_WRITE } op_aggregation_t;
 
 /* bcopy packers of an SM-root child (builtin_pack.c): plain copy, reducing
  * (:50-72) or unsigned-SUM atomic (:100-148) */
-typedef enum { PACK_COPY, PACK_REDUCING, PACK_ATOMIC } op_packer_t;
+typedef enum { PACK_COPY, PACK_REDUCING, PACK_ATOMIC, PACK_BATCHED } op_packer_t;
 
 
 typedef struct {
@@ -161,7 +162,10 @@ typedef struct {
                                      on once all its contributions are in
                                      (PIPELINED / BY_FRAGMENT_OFFSET,
                                      builtin_control.c:831-834, 978-980) */
-    int         incast;           /* sends / receives go through the incast */
+    int         incast;           /* sends / receives go through the incast:
+                                     1 one reduced message per fragment, 2 (a
+                                     root) batched: every child's fragment in
+                                     one message, reduced here in order */
     uint8_t     packer;           /* op_packer_t of an incast send */
     unsigned    incast_expected;  /* children packing each incast message */
     size_t      frag_len;         /* 0: single message */
@@ -184,7 +188,7 @@ struct ucg_builtin_lgroup {
     ucg_builtin_combine_t   *cmb;
     op_slot_t                slots[UCG_BUILTIN_OPS_MAX_CONCURRENT];
     uint8_t                  next_coll_id;
-    int                      incast;   /* UCX_BUILTIN_SM_INCAST */
+    int                      incast;   /* UCX_BUILTIN_SM_INCAST: 0 n, 1 y, 2 batched */
     uint64_t                 stats[4];
     /* placement and planner knobs (ucg_builtin_lgroup_params_t) */
     uint8_t                  distance[UCG_BUILTIN_OPS_MAX_MEMBERS];

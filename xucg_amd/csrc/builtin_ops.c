@@ -21,7 +21,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-static const char *const packer_name[] = {"copy", "reducing", "atomic"};
+static const char *const packer_name[] = {"copy", "reducing", "atomic", "batched"};
 static const char *const method_name[] = {
     "REDUCE_RECURSIVE", "REDUCE_TERMINAL", "SEND_TO_SM_ROOT", "SEND_TERMINAL",
     "RECV_TERMINAL", "REDUCE_WAYPOINT", "BCAST_WAYPOINT"
@@ -227,6 +227,10 @@ static ucs_status_t send_one(ucg_builtin_lcoll_t *c, const op_step_t *s,
     if (!s->incast) {
         return ucg_builtin_shm_am_short(c->g->iface, peer, header, buf, n);
     }
+    if (s->packer == PACK_BATCHED) {
+        return ucg_builtin_shm_am_incast_batched(c->g->iface, peer, header,
+                                                 s->incast_expected, buf, n);
+    }
     a.c = c;
     a.src = buf;
     a.length = n;
@@ -425,7 +429,31 @@ static int recv_cb(ucg_builtin_lcoll_t *c, uint64_t offset, const void *data,
     op_step_t *s = &c->steps[c->cur];
     ucs_status_t st = UCS_OK;
 
-    if (offset + length > c->length) {
+    if (s->incast == 2 && s->aggregation == AGG_REDUCE) {
+        /* BATCHED_DATA (builtin_comp_step.inl:242-273): one message carries
+         * every child's chunk for this offset, each behind its own header;
+         * they are reduced into the same range in record order. The
+         * reference computes dest_buffer before it scales the offset (:320
+         * against :261-263), so its chunks land at the unscaled offset; here
+         * remote_offset is in bytes and every chunk lands where it belongs. */
+        const size_t rec = (length + 8) / s->incast_expected;
+        const size_t n   = rec - 8;
+        unsigned k;
+        if (rec * s->incast_expected != length + 8 || rec <= 8 || offset + n > c->length) {
+            st = UCS_ERR_IO_ERROR;
+        }
+        for (k = 0; k < s->incast_expected && st == UCS_OK; k++) {
+            const char *chunk = (const char*)data + k * rec;
+            if (on_timer_thread) {
+                c->g->async_combines++;
+            }
+            st = c->step_open ?
+                 ucg_builtin_combine_fragment(c->g->cmb, offset, chunk, n) :
+                 ucg_builtin_combine_reduce(c->g->cmb, c->op, (void*)chunk,
+                                            c->rbuf + offset, (int)(n / c->dt_len),
+                                            c->dtype);
+        }
+    } else if (offset + length > c->length) {
         st = UCS_ERR_IO_ERROR;          /* a message outside recv.buffer */
     } else if (s->aggregation == AGG_REDUCE) {
         if (on_timer_thread) {
@@ -577,7 +605,11 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
     g->cmb      = combine;
     {
         const char *e = getenv("UCX_BUILTIN_SM_INCAST");
-        g->incast = e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1');
+        g->incast = (e && (e[0] == 'b' || e[0] == 'B')) ? 2 :
+                    (e && (e[0] == 'y' || e[0] == 'Y' || e[0] == '1'));
+        if (g->incast == 2 && !iface->incast_batched) {
+            g->incast = 1;     /* the iface was opened without batched cells */
+        }
     }
     for (m = 0; m < UCG_BUILTIN_OPS_MAX_CONCURRENT; m++) {
         g->slots[m].msgs_tail = &g->slots[m].msgs;
@@ -1178,7 +1210,8 @@ size_t ucg_builtin_lcoll_describe(ucg_builtin_lcoll_t *c, char *buf, size_t max)
             }
         }
         if (s->incast) {
-            PUT(s->send_cnt ? ", incast (%s packer)" : ", incast", packer_name[s->packer]);
+            PUT(s->send_cnt ? ", incast (%s packer)" : s->incast == 2 ? ", incast (batched)" :
+                ", incast", packer_name[s->packer]);
         }
         PUT(", fragment length %zu, fragments per endpoint %llu, "
             "fragments total %llu, aggregation %s\n",

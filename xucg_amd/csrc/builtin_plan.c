@@ -443,12 +443,14 @@ UCG_INTERNAL ucs_status_t plan_finish(ucg_builtin_lcoll_t *c, unsigned ppn)
         }
         if (g->incast && s->step_idx == 1 && ppn > 2 && ppn < g->sock_thresh) {
             if (s->method == M_REDUCE_TERMINAL) {
-                s->incast          = 1;
+                s->incast          = g->incast == 2 ? 2 : 1;
+                s->incast_expected = ppn - 1;
                 s->fragments_total = s->frags;
             } else if (s->method == M_SEND_TO_SM_ROOT) {
                 s->incast          = 1;
                 s->incast_expected = ppn - 1;
-                s->packer = ucg_builtin_combine_atomic_sum_length(g->cmb, c->op, c->dtype)
+                s->packer = g->incast == 2 ? PACK_BATCHED :
+                            ucg_builtin_combine_atomic_sum_length(g->cmb, c->op, c->dtype)
                             ? PACK_ATOMIC : PACK_REDUCING;
             }
         }

@@ -64,7 +64,16 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
     it->cells      = ring_cells;
     it->cell_size  = (sizeof(cell_t) + (max_short - 8) + 63) & ~(size_t)63;
     it->ring_bytes = sizeof(ring_ctl_t) + (size_t)ring_cells * it->cell_size;
-    it->incast_cell_size = (sizeof(incast_cell_t) + (max_short - 8) + 63) & ~(size_t)63;
+    {
+        /* UCX_BUILTIN_SM_INCAST=batched: a cell carries every child's message
+         * side by side (the strided incast behind BATCHED_DATA receives,
+         * builtin_comp_step.inl:242-273) */
+        const char *e = getenv("UCX_BUILTIN_SM_INCAST");
+        it->incast_batched = e && (e[0] == 'b' || e[0] == 'B');
+    }
+    it->incast_cell_size = (sizeof(incast_cell_t) +
+                            (it->incast_batched ? members * max_short : max_short - 8) + 63) &
+                           ~(size_t)63;
     it->incast_bytes     = sizeof(incast_ctl_t) + (size_t)ring_cells * it->incast_cell_size;
     it->incast_base      = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
     it->seg_bytes        = it->incast_base + (size_t)members * it->incast_bytes;
@@ -249,6 +258,53 @@ ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *it, unsigned roo
     return UCS_OK;
 }
 
+/* The batched form: every child copies its message (header and payload)
+ * into its own slot of the root's cell - slot k for the k-th to arrive - and
+ * the root receives the cell as one message of `expected` (header, payload)
+ * records, the first header being the cell's: [chunk 0][hdr 1][chunk 1]...
+ * No child combines anything; the root reduces the chunks in slot order. */
+ucs_status_t ucg_builtin_shm_am_incast_batched(ucg_builtin_shm_iface_t *it, unsigned root,
+                                               uint64_t header, unsigned expected,
+                                               const void *payload, size_t length)
+{
+    unsigned idx, k;
+    incast_cell_t *c;
+    char *slot;
+
+    if (root >= it->members || root == it->my || expected == 0 || !it->incast_batched ||
+        expected >= it->members || length + 8 > it->max_short) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    idx = (unsigned)((((header & 0xffffffffull) * 0x9E3779B97F4A7C15ull) >> 40) +
+                     (header >> 32) / (it->max_short - 8)) % it->cells;
+    c   = incast_cell(it, root, idx);
+    spin_lock(&c->lock);
+    if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FREE) {
+        atomic_store_explicit(&c->state, INCAST_FILLING, memory_order_relaxed);
+        atomic_store_explicit(&c->count, 0, memory_order_relaxed);
+        c->header   = header;
+        c->expected = expected;
+        c->length   = (uint32_t)length;
+        c->reserved = 0;                     /* slots handed out */
+    } else if (!(atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FILLING &&
+                 c->header == header)) {
+        spin_unlock(&c->lock);
+        return UCS_ERR_NO_RESOURCE;          /* cell busy with another message */
+    }
+    k = c->reserved++;
+    spin_unlock(&c->lock);
+    slot = (char*)(c + 1) + (size_t)k * (length + 8);
+    if (k) {
+        memcpy(slot - 8, &header, 8);
+    }
+    memcpy(slot, payload, length);
+    if (atomic_fetch_add_explicit(&c->count, 1, memory_order_acq_rel) + 1 == expected) {
+        atomic_store_explicit(&c->state, INCAST_READY, memory_order_release);
+        atomic_fetch_add_explicit(&incast_ctl(it, root)->ready, 1, memory_order_release);
+    }
+    return UCS_OK;
+}
+
 static unsigned incast_progress(ucg_builtin_shm_iface_t *it, ucg_builtin_am_cb_f cb,
                                 void *arg)
 {
@@ -262,7 +318,9 @@ static unsigned incast_progress(ucg_builtin_shm_iface_t *it, ucg_builtin_am_cb_f
         if (atomic_load_explicit(&c->state, memory_order_acquire) != INCAST_READY) {
             continue;
         }
-        (void)cb(arg, &c->header, 8 + (size_t)c->length);
+        (void)cb(arg, &c->header, it->incast_batched ?
+                                  (size_t)c->expected * (8 + (size_t)c->length) :
+                                  8 + (size_t)c->length);
         atomic_fetch_sub_explicit(&ctl->ready, 1, memory_order_relaxed);
         atomic_store_explicit(&c->state, INCAST_FREE, memory_order_release);
         n++;

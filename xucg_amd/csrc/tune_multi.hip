@@ -76,6 +76,49 @@ k_multi_loop(float *dst, SrcList srcs, unsigned self, size_t nvec, unsigned loop
     }
 }
 
+/* load-order A/B: waves of odd workgroups issue their N loads last operand
+ * first, so that at any instant the waves in flight spread over all N
+ * buffers instead of all starting on operand 0 (same tree, same bits) */
+__global__ void __launch_bounds__(64)
+k_multi_alt_order(float *dst, SrcList srcs, unsigned self, size_t nvec)
+{
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= nvec) {
+        return;
+    }
+    u32x4 val[N];
+    if (blockIdx.x & 1) {
+#pragma unroll
+        for (int m = N - 1; m >= 0; m--) {
+            val[m] = ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ m]) + i);
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            val[m] = ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ m]) + i);
+        }
+    }
+    st16<1>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val, fv));
+}
+
+/* the N loads and one store with no combine (an XOR fold; not checked): how
+ * much of the loss is the store itself */
+__global__ void __launch_bounds__(64)
+k_multi_xor_store(float *dst, SrcList srcs, unsigned self, size_t nvec)
+{
+    const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= nvec) {
+        return;
+    }
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        acc ^= ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ m]) + i);
+    }
+    st16<1>(reinterpret_cast<u32x4*>(dst) + i, acc);
+}
+
 /* ceiling probe: the same N loads, no combine and a store only where the
  * (never true) data test passes, so the loads cannot be dropped */
 template <int BS>
@@ -182,7 +225,31 @@ int main(int argc, char **argv)
                                d, ss, 0u, (size_t)0, nv, (size_t)0);
         }, {}});
     }
+    vs.push_back({"product with the XCD-aware tile map (XM=1)",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
+        hipLaunchKernelGGL((k_reduce_multi<float, 0, N, 1>), dim3(g), dim3(kReduceBlock), 0, q,
+                           d, s, 0u, (size_t)0, nv, (size_t)0);
+    }, {}});
+    vs.push_back({"odd waves load the operands in reverse order",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL(k_multi_alt_order, dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, q,
+                           d, s, 0u, nv);
+    }, {}});
     const size_t nvariants_checked = vs.size();
+    vs.push_back({"N loads + 1 store, XOR fold (unchecked)",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL(k_multi_xor_store, dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, q,
+                           d, s, 0u, nv);
+    }, {}});
+    /* the 2-operand combine on operands 0 and 1 (3 streams), same process */
+    vs.push_back({"2-operand k_reduce on two of the buffers (3*S bytes)",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
+        hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(g), dim3(kReduceBlock),
+                           0, q, d, static_cast<const float*>(s.p[1]), (size_t)0, nv,
+                           (size_t)0);
+    }, {}});
     vs.push_back({"ceiling: read the N operands, no store (N*S bytes)",
                   [=](float *d, SrcList s, size_t nv, hipStream_t q) {
         unsigned g = (unsigned)((nv + 63) / 64);
@@ -227,7 +294,8 @@ int main(int argc, char **argv)
     for (auto &v : vs) {
         std::sort(v.ms.begin(), v.ms.end());
         float med = v.ms[v.ms.size() / 2];
-        const double b = v.name.rfind("ceiling", 0) == 0 ? bytes * N / (N + 1) : bytes;
+        const double b = v.name.rfind("ceiling", 0) == 0 ? bytes * N / (N + 1) :
+                         v.name.rfind("2-operand", 0) == 0 ? 3.0 * n * 4 : bytes;
         printf("%-56s median %8.2f us  %7.1f GB/s  %5.1f%% of 8 TB/s\n", v.name.c_str(),
                med * 1e3, b / (med * 1e-3) / 1e9, 100.0 * b / (med * 1e-3) / 8e12);
     }
