@@ -187,6 +187,15 @@ ucs_status_t ucg_builtin_combine_dev_butterfly(ucg_builtin_combine_t *cmb, void 
                                                const void *const *srcs, unsigned nsrc,
                                                unsigned self, size_t count);
 
+/* The memory registration of a persistent op's host recv buffer (the
+ * reference registers an op's buffers after MEM_REG_OPT_CNT starts,
+ * builtin_control.c:276-286, 345-373; dropped in discard, :1289-1292): a
+ * staged step's H2D / D2H of a registered buffer moves by DMA, with no staging
+ * copy in the runtime. UCS_ERR_UNSUPPORTED without a device. */
+ucs_status_t ucg_builtin_combine_mem_reg(ucg_builtin_combine_t *cmb, void *ptr,
+                                         size_t bytes);
+void         ucg_builtin_combine_mem_dereg(ucg_builtin_combine_t *cmb, void *ptr);
+
 /* [0] host calls, [1] host bytes, [2] device calls, [3] device bytes,
  * [4] steps staged on the device, [5] callback errors seen */
 void         ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb,

@@ -85,11 +85,15 @@ def test_bench_collective_phases_world1():
     assert c4["push_allreduce_bit_exact_vs_rccl_rs_ag"] is True, c4
     assert c4["rs_1gib"]["oneshot_bit_exact_vs_rccl_on_exact_inputs"] is True, c4
     c5 = coll["c5_recursive_allreduce_512mib_fp64"]
-    assert c5["doubling"]["bit_exact_vs_oneshot_tree"] is True, c5
-    assert c5["halving"]["bit_exact_vs_oneshot_tree"] is True, c5
-    assert c5["oneshot_xgmi"]["bit_exact_vs_oneshot_tree"] is True, c5
-    assert c5["oneshot_xgmi_push"]["bit_exact_vs_oneshot_tree"] is True, c5
+    assert c5["doubling"]["bit_exact_vs_host_plan_sampled"] is True, c5
+    assert c5["halving"]["bit_exact_vs_host_plan_sampled"] is True, c5
+    assert c5["oneshot_xgmi"]["bit_exact_vs_host_plan_sampled"] is True, c5
+    assert c5["oneshot_xgmi_push"]["bit_exact_vs_host_plan_sampled"] is True, c5
     assert c5["rccl_allreduce_within_8c_tolerance_of_plan"] is True, c5
+    eng = coll["c5_builtin_engine_device_buffers_512mib_fp64"]
+    assert eng["bit_exact_vs_host_plan_sampled"] is True, eng
+    # the line's verdict over every check above
+    assert line["collective_ok"] is True and "collective_failures" not in line, line
 
 
 @pytest.mark.parametrize("mode,bad", [("ok", 0), ("export", 1), ("import", 2), ("import", 0)])

@@ -652,6 +652,28 @@ ucs_status_t ucg_builtin_combine_dev_butterfly(ucg_builtin_combine_t *cmb, void 
     return st;
 }
 
+ucs_status_t ucg_builtin_combine_mem_reg(ucg_builtin_combine_t *cmb, void *ptr, size_t bytes)
+{
+    ucs_status_t st;
+    if (cmb == NULL || cmb->dev == NULL) {
+        return UCS_ERR_UNSUPPORTED;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    st = ucg_builtin_dev_host_register(cmb->dev, ptr, bytes);
+    pthread_mutex_unlock(&cmb->lock);
+    return st;
+}
+
+void ucg_builtin_combine_mem_dereg(ucg_builtin_combine_t *cmb, void *ptr)
+{
+    if (cmb == NULL || cmb->dev == NULL || ptr == NULL) {
+        return;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    (void)ucg_builtin_dev_host_unregister(cmb->dev, ptr);
+    pthread_mutex_unlock(&cmb->lock);
+}
+
 void ucg_builtin_combine_stats(ucg_builtin_combine_t *cmb, uint64_t out[6])
 {
     int i;

@@ -288,6 +288,11 @@ struct ucg_builtin_lcoll {
                                      small message - one pass of every member
                                      over all the data (2), or a one-host
                                      tree's fold in one pass (3) */
+    /* the memory registration of the recv buffer after MEM_REG_OPT_CNT
+     * starts whose steps staged on the device (builtin_control.c:345-373) */
+    int          staged_dev;      /* a step of this op staged on the device */
+    unsigned     dev_starts;      /* starts since */
+    int          rbuf_reg;        /* rbuf registered (dropped in destroy) */
     /* ucg_params_t.completion (api/ucg.h:162-171) */
     int          comp_set;
     ucg_builtin_coll_comp_cb_f comp_cb;

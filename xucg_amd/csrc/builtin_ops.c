@@ -362,6 +362,7 @@ static void step_execute(ucg_builtin_lcoll_t *c)
                                                 c->length);
             if (st == UCS_OK) {
                 c->step_open = 1;
+                c->staged_dev |= ucg_builtin_combine_step_on_device(g->cmb);
             } else if (st != UCS_ERR_BUSY) {
                 finish(c, st);
                 return;
@@ -556,6 +557,16 @@ static unsigned env_uint(const char *name, unsigned dflt)
 {
     const char *e = getenv(name);
     return (e && *e) ? (unsigned)strtoul(e, NULL, 0) : dflt;
+}
+
+/* BUILTIN_MEM_REG_OPT_CNT (builtin.c:49-50), 0 = never register */
+static unsigned mem_reg_opt_cnt(void)
+{
+    static unsigned v = (unsigned)-1;
+    if (v == (unsigned)-1) {
+        v = env_uint("UCX_BUILTIN_MEM_REG_OPT_CNT", 10);
+    }
+    return v;
 }
 
 ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
@@ -777,6 +788,9 @@ void ucg_builtin_lgroup_stats(ucg_builtin_lgroup_t *g, uint64_t out[4])
 
 static void lcoll_free(ucg_builtin_lcoll_t *c)
 {
+    if (c && c->rbuf_reg) {
+        ucg_builtin_combine_mem_dereg(c->g->cmb, c->rbuf);   /* discard, :1289-1292 */
+    }
     if (c) {
         if (c->rma) {
             rma_free(c);
@@ -1015,6 +1029,17 @@ static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id)
     g->next_coll_id = (uint8_t)(coll_id + 1);
     if (c->rma) {
         return rma_start(c, slot);
+    }
+    /* the op's optimisation countdown (ucg_builtin_comp_last_step_cb,
+     * builtin_comp_step.inl:24-27 -> ucg_builtin_optimize, builtin_control.c:
+     * 345-373): after MEM_REG_OPT_CNT starts that staged a step on the device,
+     * its recv buffer is registered, so that every later step's H2D and D2H
+     * of it move by DMA */
+    if (c->staged_dev && !c->rbuf_reg && c->length &&
+        ++c->dev_starts == mem_reg_opt_cnt() &&
+        ucg_builtin_dev_mem_kind(c->rbuf) == UCG_DEV_MEM_HOST &&
+        ucg_builtin_combine_mem_reg(g->cmb, c->rbuf, c->length) == UCS_OK) {
+        c->rbuf_reg = 1;
     }
     /* ucg_builtin_init_reduce: recv <- send (in place: nothing to copy);
      * tree leaves have no init (builtin_control.c:755-767) */

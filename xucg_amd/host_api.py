@@ -53,6 +53,8 @@ HOST_API = {
     "ucg_builtin_combine_step_end": (_int, [_vp]),
     "ucg_builtin_combine_step_on_device": (_int, [_vp]),
     "ucg_builtin_combine_stats": (None, [_vp, ctypes.POINTER(_u64)]),
+    "ucg_builtin_combine_mem_reg": (_int, [_vp, _vp, _sz]),
+    "ucg_builtin_combine_mem_dereg": (None, [_vp, _vp]),
     "ucg_builtin_step_fragment_length": (_sz, [_sz, _sz]),
     "ucg_builtin_step_fragments_total": (_u64, [_sz, _sz, _u]),
     "ucg_builtin_dev_chunk_bytes": (_sz, [_sz, _sz, _sz]),
@@ -81,6 +83,7 @@ HOST_API = {
     "ucg_builtin_shm_am_short": (_int, [_vp, _u, _u64, _vp, _sz]),
     "ucg_builtin_shm_progress": (_u, [_vp, _vp, _vp]),
     "ucg_builtin_shm_barrier": (None, [_vp]),
+    "ucg_builtin_shm_am_incast_batched": (_int, [_vp, _u, _u64, _u, _vp, _sz]),
     "ucg_builtin_shm_am_incast": (_int, [_vp, _u, _u64, _u, _sz, _vp, _vp, _int]),
     "ucg_builtin_lgroup_create": (_int, [_vp, ctypes.c_uint16, _u, _u, _vp,
                                          ctypes.POINTER(_vp)]),
