@@ -55,6 +55,13 @@ print(d['value'], r['frac'], r['kernel_avg_us'], json.dumps({k: v.get('latency_u
     step multi
     bash scripts/multi_pmc.sh $OUT/multi > $OUT/multi.log 2>&1 || { tail -5 $OUT/multi.log; exit 1; }
     grep -E "%|MiB" $OUT/multi/tune_multi_24.txt ;;
+  profile)
+    step profile
+    bash scripts/profile_round.sh $TAG/prof > $OUT/profile.log 2>&1 || { tail -5 $OUT/profile.log; exit 1; }
+    P=gpurun_out/$TAG/prof
+    python3 scripts/pmc_summary.py $(find $P/pmc_fetch -name "*counter_collection.csv" | head -1) \
+        $(find $P/pmc_write -name "*counter_collection.csv" | head -1) $OUT/pmc_traffic.json > /dev/null 2>&1
+    grep -E "ratio|hbm_bytes" $OUT/pmc_traffic.json; cat $P/trace_summary.json | head -c 600 ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }
