@@ -233,6 +233,10 @@ def agreed_phase(out, name, fn, dist, dev, rank=0, t_start=None):
 
 SAMPLE_ELEMS = 8192          # 64 KiB of fp64 per window
 
+# rehearsal only (XUCG_COLLECTIVE_BACKEND=gloo, see HostStagedDist): the C4/C5
+# buffers divided by this power of two; 1 in every real run
+COLL_SCALE = int(os.environ.get("XUCG_COLLECTIVE_SCALE", "1"))
+
 
 def sample_starts(n, elems=SAMPLE_ELEMS, k=16, seed=0x5EED5):
     """Windows for the sampled parity check: head, tail and k windows at
@@ -275,9 +279,31 @@ def sampled_plan_check(dist, init, rank, world):
     xs = np.stack([a.cpu().numpy() for a in allw])
     want = host_butterfly(xs, rank)
 
+    idx_h = idx.cpu().numpy()
+
     def check(acc):
+        """True when acc holds the plan's bits on every window; on a
+        mismatch, check.last says where (elements, shards of the one-shot
+        layout) and whether the bad values are zeros or another member's
+        association."""
+        from xucg_amd import group as G
         got = acc[idx].cpu().numpy()
-        return bool(np.array_equal(got.view(np.int64), want.view(np.int64)))
+        bad = np.nonzero(got.view(np.int64) != want.view(np.int64))[0]
+        check.last = None
+        if bad.size:
+            bounds = [G.shard_bounds(n, 8, world, r) for r in range(world)]
+            shards = sorted({r for b in bad for r, (lo, hi) in enumerate(bounds)
+                             if lo <= idx_h[b] < hi})
+            others = [m for m in range(world)
+                      if np.array_equal(got[bad].view(np.int64),
+                                        host_butterfly(xs[:, bad], m).view(np.int64))]
+            check.last = {"elements": int(bad.size), "of": int(got.size),
+                          "first": [int(idx_h[b]) for b in bad[:4]],
+                          "got": got[bad[:3]].tolist(), "want": want[bad[:3]].tolist(),
+                          "zeros": int((got[bad] == 0).sum()), "shards": shards,
+                          "equals_association_of_members": others}
+        return not bad.size
+    check.last = None
     return check, idx, want, xs
 
 
@@ -309,7 +335,13 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
 
     t_start = time.perf_counter()
 
+    only = [p for p in os.environ.get("XUCG_COLLECTIVE_PHASES", "").split(",") if p]
+
     def agreed(fn, name):
+        # XUCG_COLLECTIVE_PHASES=name,...: run only those (a debugging aid)
+        if only and name not in only:
+            out[name] = {"skipped": "not in XUCG_COLLECTIVE_PHASES"}
+            return
         agreed_phase(out, name, fn, dist, dev, rank, t_start)
 
     def timed(fn, iters):
@@ -324,7 +356,12 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() / iters
 
-    n4 = 1 << 30                      # 4 GiB fp32 (config 4)
+    # every tensor exported to the peers (PeerBuffers) stays allocated until
+    # the phases end: a HIP IPC key is (pid, address, size), so a tensor freed
+    # and allocated again at the same address would give the peers a key
+    # that can resolve to the old memory (r03h)
+    exported = []
+    n4 = (1 << 30) // COLL_SCALE      # 4 GiB fp32 (config 4)
     shard = n4 // world
     x = torch.empty(n4, dtype=torch.float32, device=dev)
     ctx.fill("float32", "exact", 0x5EED4000 + rank, x, n4)
@@ -351,8 +388,10 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     def oneshot():
         if world & (world - 1) or world > 16:
             return {"skipped": "one-shot needs a power-of-two group <= 16"}
+        exported.append(x)
         peers = G.PeerBuffers(ctx, x.data_ptr(), rank, world, dist)
         mine = torch.empty(shard, dtype=torch.float32, device=dev)
+        exported.append(mine)
         try:
             def rs():
                 G.oneshot_reduce_scatter(ctx, peers, mine.data_ptr(), n4, "float32",
@@ -367,7 +406,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
             # north_star's 8-GPU target is stated on the 1 GiB buffer of the
             # single-GPU target: the first 1 GiB of x, same peers, both ways
-            n1 = 1 << 28
+            n1 = (1 << 28) // COLL_SCALE
             lo1, hi1 = G.shard_bounds(n1, 4, world, rank)
             mine1 = torch.empty(hi1 - lo1, dtype=torch.float32, device=dev)
             rccl1 = torch.empty(n1 // world, dtype=torch.float32, device=dev)
@@ -399,6 +438,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             # place over xGMI (ucg_builtin_dev_gather_multi); parity: bit-exact
             # with RCCL's all-gather of the same shards
             ag_rccl = ag_out.clone()
+            exported.append(ag_out)
             speers = G.PeerBuffers(ctx, mine.data_ptr(), rank, world, dist)
             try:
                 def ag1():
@@ -425,6 +465,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             # shard is written into every peer's recv buffer
             slot = G.stage_slot_bytes(n4, 4, world)
             stage = torch.empty(world * slot // 4, dtype=torch.float32, device=dev)
+            exported.append(stage)
             tpeers = G.PeerBuffers(ctx, stage.data_ptr(), rank, world, dist)
             try:
                 def ar1():
@@ -521,7 +562,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     def recursive_doubling():
         if world & (world - 1):
             return {"skipped": "recursive doubling / halving need a power-of-two group"}
-        n5 = 1 << 26                  # 512 MiB fp64 per rank (config 5)
+        n5 = (1 << 26) // COLL_SCALE  # 512 MiB fp64 per rank (config 5)
         init = torch.empty(n5, dtype=torch.float64, device=dev)
         ctx.fill("float64", "round", 0x5EED5000 + rank, init, n5)
         acc = torch.empty_like(init)
@@ -544,11 +585,13 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                                           n5, 8)
 
         sbar = G.stream_barrier(dist, dev)
+        exported.extend((init, acc))
         ipeers = G.PeerBuffers(ctx, init.data_ptr(), rank, world, dist)
         apeers = G.PeerBuffers(ctx, acc.data_ptr(), rank, world, dist)
 
         slot5 = G.stage_slot_bytes(n5, 8, world)
         stage5 = torch.empty(world * slot5 // 8, dtype=torch.float64, device=dev)
+        exported.append(stage5)
         tpeers = G.PeerBuffers(ctx, stage5.data_ptr(), rank, world, dist)
 
         def once_oneshot():
@@ -564,6 +607,38 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         # parity: the plan's association evaluated on the host over sampled
         # windows of every member's input (head, tail, 16 random 64 KiB)
         check, idx, want_w, xs_w = sampled_plan_check(dist, init, rank, world)
+
+        def head_ok(pb, xs, want):
+            """per member: does its buffer's head window, read through the
+            peer mapping by DMA / by a kernel, hold its input (xs) or the
+            plan's result (want)? "ok/ok", "ok/BAD", ..."""
+            import numpy as np
+            from xucg_amd import _lib
+            torch.cuda.synchronize()
+            out = []
+            loc = torch.empty(SAMPLE_ELEMS, dtype=torch.float64, device=dev)
+            for p, ptr in enumerate(pb.ptrs):
+                ref = (xs[p][:SAMPLE_ELEMS] if xs is not None else want[:SAMPLE_ELEMS]
+                       ).view(np.int64)
+                h = np.empty(SAMPLE_ELEMS, np.float64)       # by DMA
+                _lib.check(_lib.dev().ucg_builtin_dev_memcpy(
+                    ctx.handle, h.ctypes.data, ptr, SAMPLE_ELEMS * 8), "memcpy")
+                _lib.check(ctx.copy_multi([loc.data_ptr()], [ptr], SAMPLE_ELEMS * 8),
+                           "copy_multi")                      # by a kernel
+                torch.cuda.synchronize()
+                k = loc.cpu().numpy()
+                v = ("ok" if np.array_equal(h.view(np.int64), ref) else "BAD") + "/" + \
+                    ("ok" if np.array_equal(k.view(np.int64), ref) else "BAD")
+                if "BAD" in v and xs is not None:
+                    # whose data the mapping shows, and the key it came from
+                    whose = [q for q in range(len(xs)) if np.array_equal(
+                        h.view(np.int64), xs[q][:SAMPLE_ELEMS].view(np.int64))]
+                    b = pb.blobs[p] or b""
+                    v += (f" shows {whose or ('zeros' if not h.any() else '?')}"
+                          f" key {b[:64].hex()} off {int.from_bytes(b[64:72], 'little')}"
+                          f" size {int.from_bytes(b[72:80], 'little')} at 0x{ptr:x}")
+                out.append(v)
+            return out
         res = {"bytes_per_rank": n5 * 8, "steps": G.recursive_steps(world),
                "parity": "host evaluation of the plan's association on 18 sampled "
                          "64 KiB windows of every member's input"}
@@ -584,6 +659,16 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                          "sent_bytes_per_rank": link_bytes,
                          "link_gbs": round(link_bytes / t / 1e9, 1),
                          "bit_exact_vs_host_plan_sampled": same}
+            if not same:
+                res[name]["mismatch"] = mm = dict(check.last)
+                # where it went wrong: the head window of every member's
+                # input and of every member's result, read through the maps
+                # (local reads only, after the form's last collective)
+                try:
+                    mm["inputs_via_map_ok"] = head_ok(ipeers, xs_w, None)
+                    mm["results_via_map_ok"] = head_ok(apeers, None, want_w)
+                except Exception as e:  # noqa: BLE001 - a diagnostic only
+                    mm["diagnostic_error"] = f"{type(e).__name__}: {e}"[:200]
         torch.cuda.synchronize()
         dist.barrier()
         ipeers.close()
@@ -618,7 +703,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         here costs this entry only."""
         if world & (world - 1):
             return {"skipped": "the recursive plan needs a power-of-two group"}
-        n5 = 1 << 26
+        n5 = (1 << 26) // COLL_SCALE
         init = torch.empty(n5, dtype=torch.float64, device=dev)
         ctx.fill("float64", "round", 0x5EED5000 + rank, init, n5)
         acc = torch.zeros_like(init)
@@ -642,7 +727,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                         "executed_as": executed[0] if executed else "the plan's steps",
                         "ms": round(t * 1e3, 3), "algbw_gbs": round(n5 * 8 / t / 1e9, 1),
                         "sent_bytes_per_rank": link, "link_gbs": round(link / t / 1e9, 1),
-                        "bit_exact_vs_host_plan_sampled": same}
+                        "bit_exact_vs_host_plan_sampled": same,
+                        **({} if same else {"mismatch": check.last})}
             finally:
                 torch.cuda.synchronize()
                 dist.barrier()
@@ -662,6 +748,9 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         return res
     agreed(engine_c5, "c5_builtin_engine_device_buffers_512mib_fp64")
     out["wall_s"] = round(time.perf_counter() - t_start, 1)
+    torch.cuda.synchronize()
+    dist.barrier()          # no peer maps any of them any more
+    del exported
     return out
 
 
@@ -802,8 +891,106 @@ def run_collective_children(dist, rank, world, timeout_s=300):
     return res, rc == 0
 
 
+class HostStagedDist:
+    """Rehearsal only (XUCG_COLLECTIVE_BACKEND=gloo): the torch.distributed
+    calls of collective_phases over gloo, with CUDA tensors staged through
+    host memory. RCCL refuses two ranks on one GPU, so this is how the
+    multi-rank glue of the phases (IPC key exchange, peer mappings, the
+    one-shot and push forms, the engine over several processes, phase
+    agreement and every parity check) runs on a 1-GPU box with 2-4 ranks.
+    Each call synchronises the device, so the rehearsal's timings mean
+    nothing; the result carries a "rehearsal" entry saying so."""
+
+    def __init__(self, dist):
+        self._d = dist
+        self.ReduceOp = dist.ReduceOp
+
+    @staticmethod
+    def _sync():
+        import torch
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+    def get_rank(self):
+        return self._d.get_rank()
+
+    def get_world_size(self):
+        return self._d.get_world_size()
+
+    def barrier(self, group=None):
+        self._sync()
+        self._d.barrier(group=group)
+
+    def all_reduce(self, t, op=None, group=None):
+        op = self._d.ReduceOp.SUM if op is None else op
+        c = t.cpu()
+        self._d.all_reduce(c, op=op, group=group)
+        t.copy_(c)
+
+    def all_gather(self, outs, t, group=None):
+        cs = [torch_empty_cpu_like(t) for _ in outs]
+        self._d.all_gather(cs, t.cpu(), group=group)
+        for o, c in zip(outs, cs):
+            o.copy_(c)
+
+    def all_gather_object(self, outs, obj, group=None):
+        self._d.all_gather_object(outs, obj, group=group)
+
+    def broadcast_object_list(self, objs, src=0, group=None):
+        self._d.broadcast_object_list(objs, src=src, group=group)
+
+    def reduce_scatter_tensor(self, out, inp, op=None, group=None):
+        c = inp.cpu()
+        self._d.all_reduce(c, op=self._d.ReduceOp.SUM if op is None else op, group=group)
+        r, w = self._d.get_rank(group), self._d.get_world_size(group)
+        out.copy_(c.view(w, -1)[r])
+
+    def all_gather_into_tensor(self, out, inp, group=None):
+        import torch
+        w = self._d.get_world_size(group)
+        cs = [torch_empty_cpu_like(inp) for _ in range(w)]
+        self._d.all_gather(cs, inp.cpu(), group=group)
+        out.copy_(torch.cat(cs))
+
+    # point to point: group.torch_exchange's P2POp / batch_isend_irecv
+    def isend(self, *a, **k):
+        raise RuntimeError("HostStagedDist: isend only through batch_isend_irecv")
+
+    def irecv(self, *a, **k):
+        raise RuntimeError("HostStagedDist: irecv only through batch_isend_irecv")
+
+    class P2POp:
+        def __init__(self, op, tensor, peer, group=None):
+            self.op, self.tensor, self.peer, self.group = op, tensor, peer, group
+
+    def batch_isend_irecv(self, ops):
+        stage = []
+        for p in ops:
+            send = p.op == self.isend
+            c = p.tensor.cpu() if send else torch_empty_cpu_like(p.tensor)
+            stage.append((p, c, send))
+        works = [(self._d.isend if send else self._d.irecv)(c, p.peer, group=p.group)
+                 for p, c, send in stage]
+        for w in works:
+            w.wait()
+        for p, c, send in stage:
+            if not send:
+                p.tensor.copy_(c)
+
+        class _Done:
+            def wait(self):
+                return True
+        return [_Done() for _ in ops]
+
+
+def torch_empty_cpu_like(t):
+    import torch
+    return torch.empty(t.shape, dtype=t.dtype)
+
+
 def collective_child():
-    """--collective-child: one rank of the collective phases (see above)."""
+    """--collective-child: one rank of the collective phases (see above).
+    XUCG_COLLECTIVE_BACKEND=gloo is the 1-GPU rehearsal (HostStagedDist)."""
     import datetime
     import torch
     import torch.distributed as dist
@@ -814,10 +1001,22 @@ def collective_child():
     torch.cuda.set_device(local_rank)
     # the engine's waits give up after this long instead of outliving the child
     os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "30")
-    dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
-                            device_id=torch.device(f"cuda:{local_rank}"))
+    rehearsal = os.environ.get("XUCG_COLLECTIVE_BACKEND", "nccl") == "gloo"
+    if rehearsal:
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=240))
+        pg = HostStagedDist(dist)
+    else:
+        if COLL_SCALE != 1:
+            raise SystemExit("XUCG_COLLECTIVE_SCALE is for the gloo rehearsal only")
+        dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
+                                device_id=torch.device(f"cuda:{local_rank}"))
+        pg = dist
     ctx = xucg_amd.DevContext.on_torch_stream(local_rank)
-    res = collective_phases(ctx, dist, rank, world, local_rank)
+    res = collective_phases(ctx, pg, rank, world, local_rank)
+    if rehearsal:
+        res["rehearsal"] = {"backend": "gloo, CUDA tensors staged through the host",
+                            "size_divisor": COLL_SCALE,
+                            "note": "checks the multi-rank glue and parity; timings invalid"}
     if rank == 0:
         with open(os.environ["XUCG_COLLECTIVE_OUT"], "w") as f:
             json.dump(res, f)

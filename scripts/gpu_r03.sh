@@ -62,6 +62,11 @@ print(d['value'], r['frac'], r['kernel_avg_us'], json.dumps({k: v.get('latency_u
     python3 scripts/pmc_summary.py $(find $P/pmc_fetch -name "*counter_collection.csv" | head -1) \
         $(find $P/pmc_write -name "*counter_collection.csv" | head -1) $OUT/pmc_traffic.json > /dev/null 2>&1
     grep -E "ratio|hbm_bytes" $OUT/pmc_traffic.json; cat $P/trace_summary.json | head -c 600 ;;
+  place)
+    step place
+    timeout -k 10 200 python -u scripts/place_probe.py $OUT/place_plain.json 6 > $OUT/place_plain.log 2>&1 || { tail -5 $OUT/place_plain.log; exit 1; }
+    timeout -k 10 200 python -u scripts/place_probe.py $OUT/place_torch.json 6 --torch > $OUT/place_torch.log 2>&1 || { tail -5 $OUT/place_torch.log; exit 1; }
+    cat $OUT/place_plain.log $OUT/place_torch.log ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }

@@ -18,12 +18,12 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch(worker, world, args=(), timeout=240):
+def launch(worker, world, args=(), timeout=240, env_extra=None):
     return launch_exe(os.path.join(ROOT, "tests", worker), world, args, timeout,
-                      python=True)
+                      python=True, env_extra=env_extra)
 
 
-def launch_exe(exe, world, args=(), timeout=240, python=False):
+def launch_exe(exe, world, args=(), timeout=240, python=False, env_extra=None):
     port = free_port()
     env = dict(os.environ)
     env["PYTHONPATH"] = ROOT + os.pathsep + env.get("PYTHONPATH", "")
@@ -34,6 +34,7 @@ def launch_exe(exe, world, args=(), timeout=240, python=False):
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
+        e.update(env_extra or {})
         cmd = ([sys.executable] if python else []) + [exe, *map(str, args)]
         procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))

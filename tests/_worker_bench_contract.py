@@ -59,6 +59,41 @@ def main():
     acc[n - 1] = np.nextafter(acc[n - 1].item(), np.inf)       # the tail window
     if check(acc):
         fail("a changed element passed the sampled check")
+
+    # the 1-GPU rehearsal's stand-in for RCCL (bench.HostStagedDist) against
+    # gloo's own results, on CPU tensors
+    from xucg_amd import group as G
+    pg = bench.HostStagedDist(dist)
+    x = torch.arange(world * 6, dtype=torch.float64) * (rank + 1)
+    ref = x.clone()
+    dist.all_reduce(ref)
+    a = x.clone()
+    pg.all_reduce(a)
+    if not torch.equal(a, ref):
+        fail("HostStagedDist.all_reduce")
+    rs = torch.empty(6, dtype=torch.float64)
+    pg.reduce_scatter_tensor(rs, x)
+    if not torch.equal(rs, ref.view(world, 6)[rank]):
+        fail("HostStagedDist.reduce_scatter_tensor")
+    ag = torch.empty(world * 6, dtype=torch.float64)
+    pg.all_gather_into_tensor(ag, rs)
+    parts = [torch.empty(6, dtype=torch.float64) for _ in range(world)]
+    pg.all_gather(parts, rs)
+    if not (torch.equal(ag, ref) and torch.equal(torch.cat(parts), ref)):
+        fail("HostStagedDist.all_gather(_into_tensor)")
+    flag = torch.tensor([float(rank)])
+    pg.all_reduce(flag, op=pg.ReduceOp.MAX)
+    if flag.item() != world - 1:
+        fail("HostStagedDist.all_reduce MAX")
+    send, recv = torch.full((5,), float(rank)), torch.empty(5)
+    G.torch_exchange(pg)(send, recv, rank ^ 1)
+    if not torch.equal(recv, torch.full((5,), float(rank ^ 1))):
+        fail("HostStagedDist point-to-point exchange")
+    objs = [None] * world
+    pg.all_gather_object(objs, rank)
+    if objs != list(range(world)):
+        fail("HostStagedDist.all_gather_object")
+    pg.barrier()
     dist.barrier()
     dist.destroy_process_group()
     print(f"rank {rank}: {'ok' if rc == 0 else 'FAILED'}", flush=True)

@@ -226,6 +226,53 @@ def test_bench_collective_contract_over_gloo(world):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_bench_collective_phases_rehearsal_on_one_gpu(world):
+    """bench.py's N > 1 phases (C4 and C5: RCCL forms, one-shot pull and push
+    forms over IPC-mapped peers, recursive doubling / halving, the engine on
+    device buffers) with `world` ranks on the one GPU of the box. RCCL refuses
+    two ranks per device, so XUCG_COLLECTIVE_BACKEND=gloo stands in for it
+    (bench.HostStagedDist) and the buffers are 1/64 of the real ones. The IPC
+    key exchange, peer mappings, kernels and the engine run for real across
+    processes: no phase may fail and every parity flag must hold."""
+    import importlib
+    import json
+    import tempfile
+    import uuid
+    bench = importlib.import_module("bench")
+    out = os.path.join(tempfile.gettempdir(), f"xucg_rehearsal_{uuid.uuid4().hex}.json")
+    codes, outs = launch("../bench.py", world, args=("--collective-child",), timeout=240,
+                         env_extra={"LOCAL_RANK": "0", "XUCG_COLLECTIVE_BACKEND": "gloo",
+                                    "XUCG_COLLECTIVE_SCALE": "64", "XUCG_COLLECTIVE_OUT": out})
+    assert codes == [0] * world, "\n".join(o[-3000:] for o in outs)
+    with open(out) as f:
+        res = json.load(f)
+    os.unlink(out)
+    assert res["rehearsal"]["size_divisor"] == 64
+    assert bench.collective_failures(res) == [], json.dumps(res)[:3000]
+    phases = ("c4_rccl_rs_ag_4gib_fp32", "c4_oneshot_xgmi_rs_4gib_fp32",
+              "c5_recursive_allreduce_512mib_fp64",
+              "c5_builtin_engine_device_buffers_512mib_fp64")
+    for p in phases:
+        assert p in res and "skipped" not in res[p], (p, res.get(p))
+    c4 = res["c4_oneshot_xgmi_rs_4gib_fp32"]
+    for k in ("bit_exact_vs_rccl_on_exact_inputs", "oneshot_ag_bit_exact_vs_rccl",
+              "oneshot_allreduce_bit_exact_vs_rccl_rs_ag", "push_rs_bit_exact_vs_rccl",
+              "push_allreduce_bit_exact_vs_rccl_rs_ag",
+              "rccl_within_8c_tolerance_on_rounded_inputs"):
+        assert c4[k] is True, (k, c4)
+    assert c4["rs_1gib"]["oneshot_bit_exact_vs_rccl_on_exact_inputs"] is True
+    c5 = res["c5_recursive_allreduce_512mib_fp64"]
+    for form in ("doubling", "halving", "oneshot_xgmi", "oneshot_xgmi_push"):
+        assert c5[form]["bit_exact_vs_host_plan_sampled"] is True, (form, c5)
+    assert c5["rccl_allreduce_within_8c_tolerance_of_plan"] is True
+    eng = res["c5_builtin_engine_device_buffers_512mib_fp64"]
+    assert eng["bit_exact_vs_host_plan_sampled"] is True, eng
+    if world >= 4:
+        assert eng["steps"]["bit_exact_vs_host_plan_sampled"] is True, eng
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["oneshot", "steps"])
 def test_c5_engine_512mib_fp64_sampled_oracle(mode):
     """BASELINE config 5 at full size per member (512 MiB fp64), 8 members on

@@ -16,6 +16,7 @@
 #include <ctime>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <algorithm>
 #include <utility>
 
@@ -1261,6 +1262,27 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
 }
 
 /* ---- peer mapping ------------------------------------------------------- */
+/* ---- exported allocations are never returned to the runtime -------------
+ * A HIP IPC handle is the exporter's pid, the allocation's address and its
+ * size. An allocation freed and made again at the same address and size
+ * carries the old one's key, and a peer can then be handed the old mapping -
+ * stale or since reused memory: the 8-rank rehearsal of bench.py's C4 -> C5
+ * phases read another member's data and zeros through fresh keys, and once
+ * faulted (r03f/r03h). So an allocation of this shim that was
+ * ever exported is parked by ucg_builtin_dev_free instead of freed, and a
+ * later ucg_builtin_dev_malloc of the same device and size takes it back: a
+ * key names the same memory for the life of the process. */
+namespace {
+struct own_alloc {
+    int    device;
+    size_t bytes;
+    bool   exported;
+    bool   parked;
+};
+std::mutex g_alloc_mu;
+std::unordered_map<void*, own_alloc> g_allocs;
+}
+
 struct ipc_blob {
     hipIpcMemHandle_t handle;
     uint64_t          offset;   /* of the exported pointer in its allocation */
@@ -1287,6 +1309,14 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
     ipc_blob b;
     memset(&b, 0, sizeof(b));
     HIP_TRY(hipIpcGetMemHandle(&b.handle, (void*)base));
+    {
+        /* this shim's allocation: never freed from now on (see above) */
+        std::lock_guard<std::mutex> g(g_alloc_mu);
+        auto it = g_allocs.find((void*)base);
+        if (it != g_allocs.end()) {
+            it->second.exported = true;
+        }
+    }
     b.offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
     b.size   = (uint64_t)size;
     b.magic  = kIpcMagic;
@@ -1346,11 +1376,22 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
     if (ctx) {
         (void)hipSetDevice(ctx->device);
     }
+    int device = 0;
+    (void)hipGetDevice(&device);
     /* whole 2 MiB granules: a small hipMalloc may be carved out of a block
      * the runtime shares with other allocations, and such memory cannot be
      * exported through hipIpcGetMemHandle (ucg_builtin_dev_ipc_export) */
     const size_t gran = (size_t)2 << 20;
     bytes = bytes ? (bytes + gran - 1) / gran * gran : gran;
+    {
+        std::lock_guard<std::mutex> g(g_alloc_mu);
+        for (auto &a : g_allocs) {
+            if (a.second.parked && a.second.device == device && a.second.bytes == bytes) {
+                a.second.parked = false;
+                return a.first;
+            }
+        }
+    }
     /* A/B knob: UCX_BUILTIN_DEV_MALLOC=contiguous asks the runtime for
      * physically contiguous memory ("Slow phases") */
     const char *kind = getenv("UCX_BUILTIN_DEV_MALLOC");
@@ -1361,15 +1402,29 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         hip_status(e, contiguous ? "hipExtMallocWithFlags(contiguous)" : "hipMalloc");
         return nullptr;
     }
+    std::lock_guard<std::mutex> g(g_alloc_mu);
+    g_allocs[p] = own_alloc{device, bytes, false, false};
     return p;
 }
 
 void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
 {
     (void)ctx;
-    if (ptr) {
-        (void)hipFree(ptr);
+    if (ptr == nullptr) {
+        return;
     }
+    {
+        std::lock_guard<std::mutex> g(g_alloc_mu);
+        auto it = g_allocs.find(ptr);
+        if (it != g_allocs.end()) {
+            if (it->second.exported) {
+                it->second.parked = true;   /* its key stays this memory's */
+                return;
+            }
+            g_allocs.erase(it);
+        }
+    }
+    (void)hipFree(ptr);
 }
 
 void *ucg_builtin_dev_host_alloc(size_t bytes)

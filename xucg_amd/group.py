@@ -158,7 +158,12 @@ class PeerBuffers:
     ptrs[r] is a device pointer to member r's buffer (the local one for
     r == rank). Collective: every member must construct it together, and
     close it together before any member frees its buffer (HIP leaves a free
-    under a live importer undefined); close() ends with a barrier for that."""
+    under a live importer undefined); close() ends with a barrier for that.
+    A buffer once exported should stay allocated for the life of the process:
+    a HIP IPC key is (pid, address, size), so a buffer freed and allocated
+    again at the same address hands the peers a key that can resolve to the
+    old memory (bench.py keeps its exported tensors; the device shim parks its
+    own exported allocations)."""
 
     def __init__(self, ctx, local_ptr, rank, world, dist, group=None):
         self.ctx = ctx
@@ -176,6 +181,7 @@ class PeerBuffers:
             blob, err = None, e
         blobs = [None] * world
         dist.all_gather_object(blobs, blob, group=group)
+        self.blobs = blobs          # the keys as exchanged (diagnostics)
         if err is None and any(b is None for b in blobs):
             err = RuntimeError("a peer failed to export its buffer")
         if err is None:
