@@ -21,6 +21,7 @@ import torch.distributed as dist
 import xucg_amd
 from oracle import oracle as O
 from xucg_amd import group as G
+from _shards import oracle_shard  # noqa: E402
 
 CASES = [("float32", "sum", "special"), ("float64", "sum", "round"),
          ("int32", "prod", "round"), ("float16", "sum", "special"),
@@ -47,7 +48,7 @@ def main():
         st = O.storage(dt)
         sz = np.dtype(st).itemsize
         inputs = [O.fill(dt, dname, 300 + r, n) for r in range(world)]
-        shards = [G.oracle_shard(op, dt, inputs, r, world, O) for r in range(world)]
+        shards = [oracle_shard(op, dt, inputs, r, world, O) for r in range(world)]
         buf, out, full = ctx.alloc(n * sz), ctx.alloc(n * sz), ctx.alloc(n * sz)
         stage = ctx.alloc(world * G.stage_slot_bytes(n, sz, world))
         buf.upload(inputs[rank])

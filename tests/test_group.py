@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 
 from xucg_amd import group as G
+from _shards import oracle_shard  # noqa: E402
 from _launch import launch
 
 
@@ -195,7 +196,7 @@ def test_oneshot_allreduce_schedule(variant, world, dt, op, count):
     for t in ths:
         t.join()
     assert not errs, errs
-    want = np.concatenate([G.oracle_shard(op, dt, inputs, r, world, O)[2]
+    want = np.concatenate([oracle_shard(op, dt, inputs, r, world, O)[2]
                            for r in range(world)])
     for r in range(world):
         got = mem[recv[r]:recv[r] + nb].view(st)

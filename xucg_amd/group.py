@@ -419,13 +419,3 @@ def stream_barrier(dist, device, group=None):
     def barrier():
         dist.all_reduce(flag, group=group)
     return barrier
-
-
-def oracle_shard(op, dt, inputs, rank, world, oracle):
-    """Expected one-shot shard for tests: the plan's result on the owner."""
-    size = np.dtype(inputs[0].dtype).itemsize
-    lo, hi = shard_bounds(inputs[0].size, size, world, rank)
-    shards = [x[lo:hi] for x in inputs]
-    if is_pow2(len(inputs)):
-        return lo, hi, oracle.reduce_multi(op, dt, shards, rank)
-    return lo, hi, oracle.tree_reduce(op, dt, shards, root=0)
