@@ -287,7 +287,12 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx);
  * offset of the pointer inside that allocation and the allocation's size
  * (import refuses a mapping that does not cover it). Opaque, fixed size.
  * Lifetime (HIP IPC contract): every importer releases its mapping before
- * the exporter frees the memory.
+ * the exporter frees the memory. The key is (pid, address, size), so memory
+ * once exported should stay allocated while the process lives: an allocation
+ * at a freed one's address and size would carry its key, and peers can be
+ * handed the old memory. ucg_builtin_dev_free therefore parks an allocation
+ * of ucg_builtin_dev_malloc that was exported, and the next malloc of that
+ * device and size takes it back, key and all.
  * The memory must come from an allocation of its own (ucg_builtin_dev_malloc,
  * a hipMalloc of >= 2 MiB, a caching-allocator segment): the runtime may carve
  * small hipMalloc blocks out of a shared block, which it refuses to export. */

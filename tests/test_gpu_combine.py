@@ -394,6 +394,31 @@ def test_profile_hook_and_counters(dev_ctx):
 
 
 @pytest.mark.gpu
+def test_exported_allocations_are_parked_and_keep_their_key(dev_ctx):
+    """An allocation of the shim that was exported is never handed back to
+    the runtime: freeing it parks it, the next allocation of that size gets
+    the same memory and the same IPC key (a key is pid + address + size, so a
+    fresh allocation at that address would carry it for other memory). One
+    that was never exported is freed as before."""
+    nbytes = 6 << 20
+    a = dev_ctx.alloc(nbytes)
+    a.upload(np.arange(16, dtype=np.int64))
+    key = dev_ctx.ipc_export(a)
+    pa = a.ptr
+    a.free()
+    b = dev_ctx.alloc(nbytes)
+    try:
+        assert b.ptr == pa
+        assert dev_ctx.ipc_export(b) == key
+        assert (b.download(np.int64, 16) == np.arange(16)).all()   # the same memory
+        c = dev_ctx.alloc(nbytes)          # the parked one is taken: a new one
+        assert c.ptr != pa
+        c.free()
+    finally:
+        b.free()
+
+
+@pytest.mark.gpu
 def test_mem_kind(dev_ctx):
     """ucg_builtin_dev_mem_kind: pageable host 0, pinned host 1, device 2
     (also at an interior offset of a device allocation)."""
