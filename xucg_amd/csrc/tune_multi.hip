@@ -139,6 +139,64 @@ k_multi_readonly(float *dst, SrcList srcs, unsigned self, size_t nvec)
     }
 }
 
+/* operand-major: a wave streams U KiB of one operand at a time (U vectors
+ * per lane, 64 lanes apart, so each load instruction covers 1 KiB) with the
+ * next operand's loads in flight while it combines the current one, and
+ * keeps a stack of log2 N partials: operand m's vectors are folded into the
+ * partials as a binary counter carries, later group first, which is exactly
+ * rd_tree's association (level h: val[m] = f(val[m + h], val[m])). Fewer
+ * registers than holding all N operands, and U times longer contiguous runs
+ * per operand per wave. nvec must be a multiple of 64 U. */
+template <int U>
+__global__ void __launch_bounds__(64)
+k_multi_opmajor(float *dst, SrcList srcs, unsigned self, size_t nvec)
+{
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    constexpr int L = 3;                      /* log2 N */
+    const size_t base = (size_t)blockIdx.x * 64 * U + threadIdx.x;
+    if (base >= nvec) {
+        return;
+    }
+    u32x4 part[L][U], cur[U], nxt[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        cur[u] = ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self]) + base + u * 64);
+    }
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        if (m + 1 < N) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                nxt[u] = ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ (m + 1)]) +
+                                 base + u * 64);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        int lvl = 0;
+#pragma unroll
+        for (int l = 0; l < L; l++) {
+            if (((m >> l) & 1) && lvl == l) {
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    cur[u] = fv(cur[u], part[l][u]);
+                }
+                lvl = l + 1;
+            }
+        }
+        if (m + 1 < N) {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                part[lvl][u] = cur[u];
+                cur[u] = nxt[u];
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + base + u * 64, cur[u]);
+    }
+}
+
 struct Variant {
     std::string name;
     std::function<void(float*, SrcList, size_t, hipStream_t)> run;
@@ -192,6 +250,16 @@ int main(int argc, char **argv)
     VAR(1, 64, 0, 0);
     VAR(4, 64, 1, 0);
 #undef VAR
+#define OPM(U)                                                                        \
+    vs.push_back({"operand-major, " #U " KiB per operand per wave, stack of partials",  \
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {                \
+        hipLaunchKernelGGL((k_multi_opmajor<U>), dim3((unsigned)(nv / (64 * (U)))),    \
+                           dim3(64), 0, q, d, s, 0u, nv);                             \
+    }, {}})
+    OPM(2);
+    OPM(4);
+    OPM(8);
+#undef OPM
     vs.push_back({"temporal stores (U1 BS64)", [=](float *d, SrcList s, size_t nv, hipStream_t q) {
         hipLaunchKernelGGL((k_multi_loop<0>), dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, q,
                            d, s, 0u, nv, 0u);
