@@ -64,9 +64,14 @@ print(d['value'], r['frac'], r['kernel_avg_us'], json.dumps({k: v.get('latency_u
     grep -E "ratio|hbm_bytes" $OUT/pmc_traffic.json; cat $P/trace_summary.json | head -c 600 ;;
   place)
     step place
-    timeout -k 10 200 python -u scripts/place_probe.py $OUT/place_plain.json 6 > $OUT/place_plain.log 2>&1 || { tail -5 $OUT/place_plain.log; exit 1; }
-    timeout -k 10 200 python -u scripts/place_probe.py $OUT/place_torch.json 6 --torch > $OUT/place_torch.log 2>&1 || { tail -5 $OUT/place_torch.log; exit 1; }
-    cat $OUT/place_plain.log $OUT/place_torch.log ;;
+    P=$OUT/place_$(date +%H%M%S)
+    timeout -k 10 200 python -u scripts/place_probe.py ${P}_plain.json 4 > ${P}_plain.log 2>&1 || { tail -5 ${P}_plain.log; exit 1; }
+    timeout -k 10 200 python -u scripts/place_probe.py ${P}_torch.json 4 --torch > ${P}_torch.log 2>&1 || { tail -5 ${P}_torch.log; exit 1; }
+    python3 -c "
+import json, statistics as S
+for k in ('plain', 'torch'):
+    d = json.load(open('${P}_' + k + '.json'))['frac_of_8tbs']
+    print(k, {n: round(S.median(v), 3) for n, v in d.items()})" ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }

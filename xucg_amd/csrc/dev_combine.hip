@@ -16,6 +16,7 @@
 #include <ctime>
 #include <mutex>
 #include <string>
+#include <map>
 #include <unordered_map>
 #include <algorithm>
 #include <utility>
@@ -1280,7 +1281,8 @@ struct own_alloc {
     bool   parked;
 };
 std::mutex g_alloc_mu;
-std::unordered_map<void*, own_alloc> g_allocs;
+std::unordered_map<void*, own_alloc> g_allocs;                  /* live and parked */
+std::multimap<std::pair<int, size_t>, void*> g_parked;          /* (device, bytes) */
 }
 
 struct ipc_blob {
@@ -1385,11 +1387,12 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
     bytes = bytes ? (bytes + gran - 1) / gran * gran : gran;
     {
         std::lock_guard<std::mutex> g(g_alloc_mu);
-        for (auto &a : g_allocs) {
-            if (a.second.parked && a.second.device == device && a.second.bytes == bytes) {
-                a.second.parked = false;
-                return a.first;
-            }
+        auto it = g_parked.find({device, bytes});
+        if (it != g_parked.end()) {
+            p = it->second;
+            g_parked.erase(it);
+            g_allocs[p].parked = false;
+            return p;
         }
     }
     /* A/B knob: UCX_BUILTIN_DEV_MALLOC=contiguous asks the runtime for
@@ -1417,8 +1420,11 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         std::lock_guard<std::mutex> g(g_alloc_mu);
         auto it = g_allocs.find(ptr);
         if (it != g_allocs.end()) {
-            if (it->second.exported) {
-                it->second.parked = true;   /* its key stays this memory's */
+            if (it->second.exported) {      /* its key stays this memory's */
+                if (!it->second.parked) {   /* (a second free is ignored) */
+                    it->second.parked = true;
+                    g_parked.emplace(std::make_pair(it->second.device, it->second.bytes), ptr);
+                }
                 return;
             }
             g_allocs.erase(it);
