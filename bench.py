@@ -126,6 +126,12 @@ def c1_loopback(ranks=4, iters=20000):
                 ("tree_3_ranks_max_short_256", 3, 256, {}),
                 ("device_buffers_4kib", ranks, 256, dev, 1024, 2000),
                 ("device_buffers_64mib", ranks, 256, dev, 1 << 24, 20)]
+    # the same allreduce through the drop-in boundary: ucg_builtin_component's
+    # vtable driven as base/ drives it (tests/c/component_test.c, "latency":
+    # the op prepared once, trigger + progress per start)
+    variants.append(("component_vtable_max_short_256", ranks, 256,
+                     {"UCX_BUILTIN_SHORT_MAX_TX_SIZE": "256"}, 1024, iters, "component"))
+    comp_exe = os.path.join(ROOT, "tests", "c", "_build", "component_test")
     # one core per rank, as an MPI launcher binds them: the lowest-numbered
     # allowed CPUs (neighbours on one CCD on EPYC); unpinned ranks land on
     # random cores and the latency moves by 2x between runs
@@ -133,12 +139,18 @@ def c1_loopback(ranks=4, iters=20000):
     res = {"cpus": allowed[:max(v[1] for v in variants)]}
     for key, world, max_short, extra_env, *size in variants:
         name = f"ucg_bench_c1_{os.getpid()}_{uuid.uuid4().hex[:6]}"
-        count, n_iter = size if size else (1024, iters)
+        count, n_iter = size[:2] if size else (1024, iters)
+        if size[2:] == ["component"]:
+            # the component names its transport after the job uid (MASTER_PORT here)
+            cmd = [comp_exe, "latency", str(n_iter), str(count)]
+            extra_env = dict(extra_env, MASTER_PORT=str(20000 + int(uuid.uuid4().int % 40000)))
+        else:
+            cmd = [exe, name, str(n_iter), str(max_short), str(count)]
         procs = []
         for r in range(world):
             env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), **extra_env)
             cpu = allowed[r % len(allowed)]
-            procs.append(subprocess.Popen([exe, name, str(n_iter), str(max_short), str(count)],
+            procs.append(subprocess.Popen(cmd,
                                           env=env,
                                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                           text=True,

@@ -7,6 +7,7 @@
  * progress through ucg_request_get_progress, destroy). Test infrastructure.
  *
  *   RANK=r WORLD_SIZE=n MASTER_PORT=p component_test [layout|host|device]
+ *   RANK=r WORLD_SIZE=n MASTER_PORT=p component_test latency [iters [count]]
  *
  * Built twice (tests/test_component.py): over this build's declaration of
  * the API (include/ucg_api_abi.h, linked with libucg_builtin.so), and with
@@ -16,8 +17,9 @@
  * exchange: the two builds must print the same. "host" runs allreduce and
  * reduce ops on host buffers (the combine on reduce_cb_f); "device" on GPU
  * buffers (remote-key steps, the combine kernels), with the builtin-private
- * classifier registered. Inputs are exact integers, so every association
- * gives the same bits and the expected result is a plain sum / max.
+ * classifier registered. "latency" times BASELINE config 1 through the
+ * vtable. Inputs are exact integers, so every association gives the same
+ * bits and the expected result is a plain sum / max.
  */
 #define _GNU_SOURCE
 #ifdef XUCG_REFERENCE_API
@@ -185,13 +187,14 @@ static ucs_status_t coll_run(ucg_group_h g, ucg_coll_h coll)
     /* ucg_request_get_progress, base/ucg_group.c:381-384 */
     ucg_collective_progress_t progress = op->plan->planner->component->progress;
     ucs_status_t st = op->trigger_f(op, g->next_coll_id++, &req);
-    double t0 = (double)time(NULL);
+    const time_t t0 = time(NULL);
+    unsigned polls = 0;
     if (st != UCS_OK && st != UCS_INPROGRESS) {
         return st;
     }
     while (!req.done) {
         progress(coll);
-        if ((double)time(NULL) - t0 > 60) {
+        if ((++polls & 4095) == 0 && time(NULL) - t0 > 60) {
             return UCS_ERR_TIMED_OUT;
         }
     }
@@ -309,7 +312,10 @@ static ucg_collective_params_t make_params(uint16_t mods, uint64_t root, const v
 }
 
 /* member m's input element i: an exact integer */
-static double input(unsigned m, int i) { return (double)(((m * 7919 + i * 104729) % 2001) - 1000); }
+static double input(unsigned m, int i)
+{
+    return (double)((int)((m * 7919u + (unsigned)i * 104729u) % 2001u) - 1000);
+}
 
 static void fill(void *buf, const mpi_dt_t *d, unsigned m, int n)
 {
@@ -348,6 +354,67 @@ static void expect(void *buf, const mpi_dt_t *d, const mpi_op_t *o, unsigned n_m
             ((int64_t*)buf)[i] = (int64_t)acc;
         }
     }
+}
+
+static double now_us(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec * 1e6 + ts.tv_nsec * 1e-3;
+}
+
+/* "latency": BASELINE config 1 through the drop-in boundary - an fp32 SUM
+ * allreduce of `count` elements prepared once (the op cache), then `iters`
+ * starts, each trigger + progress until the completion callback, as base/
+ * runs a persistent MPI_Allreduce; one JSON line from member 0 */
+static int latency_run(ucg_group_h grp, unsigned rank, unsigned world, int iters, int count)
+{
+    const size_t bytes = (size_t)count * 4;
+    char *sbuf = malloc(bytes), *rbuf = calloc(1, bytes), *want = malloc(bytes);
+    ucg_collective_params_t p;
+    ucg_coll_h coll = NULL;
+    ucs_status_t st;
+    double t0, t1;
+    int i, warm = iters / 10 + 1, exact;
+    fill(sbuf, &DT_F32, rank, count);
+    expect(want, &DT_F32, &OP_SUM, world, count);
+    p = make_params(UCG_GROUP_COLLECTIVE_MODIFIER_AGGREGATE |
+                    UCG_GROUP_COLLECTIVE_MODIFIER_BROADCAST, 0, sbuf, rbuf, count,
+                    &DT_F32, &OP_SUM);
+    st = ucg_collective_create(grp, &p, &coll);
+    CHECK(st == UCS_OK, "latency: create %d", st);
+    if (st != UCS_OK) {
+        return 1;
+    }
+    for (i = 0; i < warm && st == UCS_OK; i++) {
+        st = coll_run(grp, coll);
+    }
+    t0 = now_us();
+    for (i = 0; i < iters && st == UCS_OK; i++) {
+        st = coll_run(grp, coll);
+    }
+    t1 = now_us();
+    CHECK(st == UCS_OK, "latency: start status %d", st);
+    exact = st == UCS_OK && memcmp(rbuf, want, bytes) == 0;
+    for (i = 0; !exact && i < count; i++) {
+        if (((float*)rbuf)[i] != ((float*)want)[i]) {
+            CHECK(0, "latency: result differs at %d: %g, want %g", i, ((float*)rbuf)[i],
+                  ((float*)want)[i]);
+            break;
+        }
+    }
+    if (rank == 0) {
+        printf("{\"config\": \"C1 through ucg_builtin_component: %u-rank allreduce, %d fp32 "
+               "SUM, op prepared once, trigger + progress per start\", \"ranks\": %u, "
+               "\"bytes\": %zu, \"latency_us\": %.3f, \"iters\": %d, \"bit_exact\": %s}\n",
+               world, count, world, bytes, (t1 - t0) / iters, iters, exact ? "true" : "false");
+        fflush(stdout);
+    }
+    coll_destroy(coll);
+    free(sbuf);
+    free(rbuf);
+    free(want);
+    return st == UCS_OK && exact ? 0 : 1;
 }
 
 int main(int argc, char **argv)
@@ -444,6 +511,17 @@ int main(int argc, char **argv)
     CHECK(st == UCS_OK, "create %d", st);
     if (st != UCS_OK) {
         return 1;
+    }
+
+    if (!strcmp(mode, "latency")) {
+        const int rc = latency_run(&grp, rank, world, argc > 2 ? atoi(argv[2]) : 20000,
+                                   argc > 3 ? atoi(argv[3]) : 1024);
+        comp->destroy(grp.gctx);
+        comp->finalize(grp.pctx);
+        free(grp.gctx);
+        free(grp.pctx);
+        free(config);
+        return rc;
     }
 
     {

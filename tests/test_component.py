@@ -84,6 +84,19 @@ def test_vtable_over_reference_api(ref_exe, world):
     _run(ref_exe, world)
 
 
+@pytest.mark.parametrize("world", [4, 3])
+def test_vtable_latency_mode_bit_exact(world):
+    """BASELINE config 1 through the vtable (bench.py's
+    c1_loopback_allreduce_4kib_fp32.component_vtable_max_short_256): a
+    persistent fp32 SUM allreduce of 1024 elements started repeatedly,
+    bit-exact at the end (exact inputs)."""
+    import json
+    codes, outs = launch_exe(EXE, world, args=("latency", 300, 1024), timeout=120)
+    assert codes == [0] * world, "\n".join(outs)
+    line = json.loads(outs[0].strip().splitlines()[-1])
+    assert line["bit_exact"] is True and line["ranks"] == world and line["latency_us"] > 0
+
+
 def test_component_source_has_no_reference_text():
     """The reference headers are read where they lie, never copied here."""
     for d in ("include", "compat"):
