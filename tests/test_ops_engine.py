@@ -349,6 +349,20 @@ def test_tree_incast_packers_device(world, max_short, cells, incast, monkeypatch
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [4, 8])
+def test_engine_group_churn_device_buffers(world):
+    """Groups on device buffers created and destroyed 12 times per process,
+    buffers of three recurring sizes freed and allocated in between, half of
+    them sent from the group's registered (exported pool) memory: IPC keys
+    are (pid, address, size) and recur, and every allreduce must still equal
+    the oracle's association bit for bit (stale keys)."""
+    import uuid
+    codes, outs = launch("_worker_churn.py", world, args=(f"ucg_churn_{uuid.uuid4().hex[:8]}", 12),
+                         timeout=180)
+    assert codes == [0] * world, "\n".join(outs)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [3, 5])
 def test_tree_multiprocess_device_staging(world):
     """Tree root's fan-in staged on the GPU: children's fragments at the same

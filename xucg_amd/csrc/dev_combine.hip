@@ -1419,8 +1419,14 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
     {
         std::lock_guard<std::mutex> g(g_alloc_mu);
         auto it = g_allocs.find(ptr);
+        /* UCX_BUILTIN_DEV_PARK=n: free exported memory too (an A/B knob for
+         * the stale-key tests, never for production) */
+        static const bool park = [] {
+            const char *e = getenv("UCX_BUILTIN_DEV_PARK");
+            return !(e && (e[0] == 'n' || e[0] == '0'));
+        }();
         if (it != g_allocs.end()) {
-            if (it->second.exported) {      /* its key stays this memory's */
+            if (it->second.exported && park) {   /* its key stays this memory's */
                 if (!it->second.parked) {   /* (a second free is ignored) */
                     it->second.parked = true;
                     g_parked.emplace(std::make_pair(it->second.device, it->second.bytes), ptr);
