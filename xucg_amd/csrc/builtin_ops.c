@@ -738,8 +738,7 @@ static void *async_timer(void *arg)
     group_block(g);
     while (!g->timer_stop) {
         struct timespec ts;
-        double t = now_s() + g->timer_tick;
-        clock_gettime(CLOCK_MONOTONIC, &ts);
+        const double t = now_s() + g->timer_tick;   /* CLOCK_MONOTONIC, as the condvar */
         ts.tv_sec  = (time_t)t;
         ts.tv_nsec = (long)((t - (double)(time_t)t) * 1e9);
         pthread_cond_timedwait(&g->timer_cv, &g->async_lock, &ts);
