@@ -534,6 +534,28 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             ratio = float((err / tol.clamp_min(1e-30)).max())
             ulps = max_ulps(mine, rs_out)
             del abs_rs, tol, err
+            # and against the plan itself: V(rank) evaluated on the host over
+            # sampled windows of this rank's shard of every member's rounded
+            # input (head, tail, 16 random windows of each shard), bit for bit
+            import numpy as np
+            bounds = [G.shard_bounds(n4, 4, world, r) for r in range(world)]
+            pos = []
+            for lo_r, hi_r in bounds:
+                w = min(SAMPLE_ELEMS, hi_r - lo_r)
+                pos.append(torch.cat([torch.arange(lo_r + s0, lo_r + s0 + w, device=dev)
+                                      for s0 in sample_starts(hi_r - lo_r, w)]))
+            mine_pos = torch.cat(pos)
+            part = x[mine_pos].contiguous()
+            allw = [torch.empty_like(part) for _ in range(world)]
+            dist.all_gather(allw, part)
+            first = sum(p.numel() for p in pos[:rank])
+            sl = slice(first, first + pos[rank].numel())
+            xs_shard = np.stack([a.cpu().numpy()[sl] for a in allw])
+            want_shard = host_butterfly(xs_shard, rank)
+            got_shard = mine[pos[rank] - bounds[rank][0]].cpu().numpy()
+            rs_plan_exact = bool(np.array_equal(got_shard.view(np.int32),
+                                                want_shard.view(np.int32)))
+            del allw, part, mine_pos
         finally:
             torch.cuda.synchronize()
             dist.barrier()
@@ -564,6 +586,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "bit_exact_vs_rccl_on_exact_inputs": same,
                 "rs_1gib": rs_1gib,
                 "rccl_within_8c_tolerance_on_rounded_inputs": within,
+                "oneshot_rs_bit_exact_vs_host_plan_sampled_rounded": rs_plan_exact,
                 "max_err_over_tolerance": round(ratio, 4),
                 "max_ulps_vs_rccl_on_rounded_inputs": ulps,
                 "association": "recursive doubling (builtin_recursive.c:158-169)"}

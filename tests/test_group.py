@@ -260,7 +260,8 @@ def test_bench_collective_phases_rehearsal_on_one_gpu(world):
     for k in ("bit_exact_vs_rccl_on_exact_inputs", "oneshot_ag_bit_exact_vs_rccl",
               "oneshot_allreduce_bit_exact_vs_rccl_rs_ag", "push_rs_bit_exact_vs_rccl",
               "push_allreduce_bit_exact_vs_rccl_rs_ag",
-              "rccl_within_8c_tolerance_on_rounded_inputs"):
+              "rccl_within_8c_tolerance_on_rounded_inputs",
+              "oneshot_rs_bit_exact_vs_host_plan_sampled_rounded"):
         assert c4[k] is True, (k, c4)
     assert c4["rs_1gib"]["oneshot_bit_exact_vs_rccl_on_exact_inputs"] is True
     c5 = res["c5_recursive_allreduce_512mib_fp64"]
