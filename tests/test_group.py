@@ -215,6 +215,22 @@ def test_oneshot_allreduce_schedule(variant, world, dt, op, count):
             assert len(pushes) <= 3
 
 
+@pytest.mark.parametrize("dt", ["float32", "float64"])
+@pytest.mark.parametrize("n", [1, 2, 4, 8, 16])
+def test_bench_host_butterfly_is_the_oracle_association(dt, n):
+    """bench.py's host evaluation of the recursive-doubling plan (the C4/C5
+    sampled parity checks) equals the oracle's ucg_oracle_reduce_multi, bit
+    for bit, for every member index, in fp32 and fp64."""
+    import importlib
+    from oracle import oracle as O
+    bench = importlib.import_module("bench")
+    xs = np.stack([O.fill(dt, "round", 0x5EED4100 + m, 4099) for m in range(n)])
+    for r in range(n):
+        got = bench.host_butterfly(xs, r)
+        want = O.reduce_multi("sum", dt, list(xs), r)
+        assert (O.bits(got) == O.bits(want)).all(), (dt, n, r)
+
+
 @pytest.mark.parametrize("world", [2, 4])
 def test_bench_collective_contract_over_gloo(world):
     """bench.py --gpus N > 1 fails loudly: a phase that raises on one rank is
