@@ -197,6 +197,43 @@ k_multi_opmajor(float *dst, SrcList srcs, unsigned self, size_t nvec)
     }
 }
 
+/* L lanes per vector (verdict item 5's suggestion): the N = 8 operands of
+ * one 16-B vector are split over L lanes of a wave (N / L each, lanes 64 / L
+ * apart), each lane folds its operands as the subtree rd_tree builds for them,
+ * and the partials meet over lane exchanges (xor 32, then 16): the same
+ * association, so the same bits. A wave covers 64 / L vectors per operand. */
+template <int L>
+__global__ void __launch_bounds__(64)
+k_multi_lanes(float *dst, SrcList srcs, unsigned self, size_t nvec)
+{
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    constexpr int K = N / L;                 /* operands per lane */
+    constexpr int W = 64 / L;                /* vectors per wave */
+    const unsigned part = threadIdx.x / W;   /* which K operands */
+    const size_t i = (size_t)blockIdx.x * W + (threadIdx.x % W);
+    u32x4 val[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+        val[k] = ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[self ^ (part * K + k)]) + i);
+    }
+    u32x4 acc = rd_tree<K>(val, fv);
+    /* level log2 K + 1 ...: the partial of the higher group is the src */
+#pragma unroll
+    for (int w = 1; w < L; w <<= 1) {
+        u32x4 other;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+            other[c] = __shfl_xor(acc[c], w * W, 64);
+        }
+        if ((part & w) == 0) {
+            acc = fv(other, acc);
+        }
+    }
+    if (part == 0 && i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, acc);
+    }
+}
+
 struct Variant {
     std::string name;
     std::function<void(float*, SrcList, size_t, hipStream_t)> run;
@@ -250,6 +287,16 @@ int main(int argc, char **argv)
     VAR(1, 64, 0, 0);
     VAR(4, 64, 1, 0);
 #undef VAR
+    vs.push_back({"2 lanes per vector (4 operands each, xor-32 exchange)",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_multi_lanes<2>), dim3((unsigned)(nv / 32)), dim3(64), 0, q,
+                           d, s, 0u, nv);
+    }, {}});
+    vs.push_back({"4 lanes per vector (2 operands each, xor-32/16 exchange)",
+                  [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_multi_lanes<4>), dim3((unsigned)(nv / 16)), dim3(64), 0, q,
+                           d, s, 0u, nv);
+    }, {}});
 #define OPM(U)                                                                        \
     vs.push_back({"operand-major, " #U " KiB per operand per wave, stack of partials",  \
                   [=](float *d, SrcList s, size_t nv, hipStream_t q) {                \
