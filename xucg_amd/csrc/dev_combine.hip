@@ -1283,6 +1283,7 @@ struct own_alloc {
 std::mutex g_alloc_mu;
 std::unordered_map<void*, own_alloc> g_allocs;                  /* live and parked */
 std::multimap<std::pair<int, size_t>, void*> g_parked;          /* (device, bytes) */
+std::unordered_multimap<void*, void*> g_imports;   /* imported pointer -> mapping base */
 }
 
 struct ipc_blob {
@@ -1345,17 +1346,22 @@ ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
     void *base = nullptr;
     HIP_TRY(hipIpcOpenMemHandle(&base, b.handle, hipIpcMemLazyEnablePeerAccess));
     /* the mapping must span the exporter's whole allocation: a short or
-     * stale mapping is refused here instead of faulting a kernel later */
+     * stale mapping is refused here instead of faulting a kernel later.
+     * Where the runtime cannot answer the range query for an imported
+     * pointer, the mapping is taken as it is. */
     hipDeviceptr_t mbase = nullptr;
     size_t msize = 0;
     const hipError_t e = hipMemGetAddressRange(&mbase, &msize, (hipDeviceptr_t)base);
-    if (e != hipSuccess || mbase != (hipDeviceptr_t)base || msize < b.size ||
-        b.offset >= b.size) {
+    if (b.offset >= b.size ||
+        (e == hipSuccess && (mbase != (hipDeviceptr_t)base || msize < b.size))) {
         (void)hipIpcCloseMemHandle(base);
         return set_error(UCS_ERR_INVALID_PARAM, "ipc_import",
                          "mapped range does not cover the exported allocation");
     }
+    (void)hipGetLastError();
     *dev_ptr = (char*)base + b.offset;
+    std::lock_guard<std::mutex> g(g_alloc_mu);
+    g_imports.emplace(*dev_ptr, base);
     return UCS_OK;
 }
 
@@ -1364,10 +1370,24 @@ ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx, void *dev_p
     if (ctx == nullptr || dev_ptr == nullptr) {
         return set_error(UCS_ERR_INVALID_PARAM, "ipc_release", "bad arguments");
     }
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr));
-    HIP_TRY(hipIpcCloseMemHandle((void*)base));
+    void *base = nullptr;
+    {
+        /* the mapping's base as import returned it (no range query on an
+         * imported pointer) */
+        std::lock_guard<std::mutex> g(g_alloc_mu);
+        auto it = g_imports.find(dev_ptr);
+        if (it != g_imports.end()) {
+            base = it->second;
+            g_imports.erase(it);
+        }
+    }
+    if (base == nullptr) {
+        hipDeviceptr_t b = nullptr;
+        size_t size = 0;
+        HIP_TRY(hipMemGetAddressRange(&b, &size, (hipDeviceptr_t)dev_ptr));
+        base = (void*)b;
+    }
+    HIP_TRY(hipIpcCloseMemHandle(base));
     return UCS_OK;
 }
 
