@@ -5,7 +5,10 @@ operands of the combine's geometry, ucg_builtin_dev_profile_stream kind 0),
 in several interleaved rounds. A buffer that is slow in every round while its
 neighbours are fast is slow by placement, not by time.
 
-    python scripts/alloc_scan.py OUT.json [count=24] [mib=256] [rounds=3]
+    python scripts/alloc_scan.py OUT.json [count=24] [mib=256] [rounds=3] [window_mib]
+
+With window_mib, every allocation is scanned in windows of that size (is the
+speed a property of the whole allocation or of regions inside it?).
 """
 import json
 import sys
@@ -25,17 +28,21 @@ def main():
     for b in bufs:
         ctx.fill("float32", "round", 5, b, nbytes // 4)
     ctx.sync()
-    half = nbytes // 2
-    rates = [[] for _ in bufs]
+    win = (int(sys.argv[5]) << 20) if len(sys.argv) > 5 else nbytes
+    spans = [(b.ptr + off, win) for b in bufs for off in range(0, nbytes, win)]
+    rates = [[] for _ in spans]
     for _ in range(rounds):
-        for i, b in enumerate(bufs):
-            ctx.profile_stream(0, b.ptr + half, b.ptr, half, 5)
-            us = sorted(ctx.profile_stream(0, b.ptr + half, b.ptr, half, 20) for _ in range(3))[1]
-            rates[i].append(round(nbytes / (us * 1e-6) / 8e12, 4))
+        for i, (p, w) in enumerate(spans):
+            half = w // 2
+            ctx.profile_stream(0, p + half, p, half, 5)
+            us = sorted(ctx.profile_stream(0, p + half, p, half, 20) for _ in range(3))[1]
+            rates[i].append(round(w / (us * 1e-6) / 8e12, 4))
     med = [sorted(r)[len(r) // 2] for r in rates]
-    print(json.dumps({"mib": mib, "read_only_frac_by_allocation_order": med}), flush=True)
+    print(json.dumps({"mib": mib, "window_mib": win >> 20,
+                      "read_only_frac_in_order": med}), flush=True)
     with open(out, "w") as f:
-        json.dump({"mib": mib, "count": count, "rounds": rounds, "frac": rates,
+        json.dump({"mib": mib, "window_mib": win >> 20, "count": count, "rounds": rounds,
+                   "frac": rates,
                    "median": med, "ptrs": [hex(b.ptr) for b in bufs]}, f, indent=1)
     for b in bufs:
         b.free()

@@ -77,7 +77,8 @@ for k in ('plain', 'torch'):
     P=$OUT/scan_$(date +%H%M%S)
     timeout -k 10 200 python -u scripts/alloc_scan.py ${P}_256.json 24 256 3 > ${P}_256.log 2>&1 || { tail -5 ${P}_256.log; exit 1; }
     timeout -k 10 200 python -u scripts/alloc_scan.py ${P}_1024.json 8 1024 3 > ${P}_1024.log 2>&1 || { tail -5 ${P}_1024.log; exit 1; }
-    tail -1 ${P}_256.log; tail -1 ${P}_1024.log ;;
+    timeout -k 10 200 python -u scripts/alloc_scan.py ${P}_arena.json 1 8192 3 512 > ${P}_arena.log 2>&1 || { tail -5 ${P}_arena.log; exit 1; }
+    tail -1 ${P}_256.log; tail -1 ${P}_1024.log; tail -1 ${P}_arena.log ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }
