@@ -5,6 +5,9 @@ placed operand pairs, interleaved over several rounds (HIP events, median of
 
     python scripts/place_probe.py OUT.json [rounds] [--torch]
 
+gib_src+Xk: the 1 GiB pair's first 256 MiB with src moved X KiB against dst
+(aliasing of the two operands in the HBM channel/bank map).
+
 Pairs: `first` (allocated first, as bench.py's), `gib` (a 1 GiB pair, the
 north-star shape), `win0` / `win512` (256 MiB windows of the 1 GiB pair at 0
 and 512 MiB), `joint` (src and dst in one 512 MiB allocation), `later` (a
@@ -48,6 +51,12 @@ def main():
         "joint": (joint.offset(N * 4), joint, N),
         "later": (d_later, s_later, N),
     }
+    # the same 1 GiB pair with src moved against dst by a few bytes to MiB
+    # inside its allocation (16-B aligned: the same kernel): if the slow pairs
+    # are slow because src and dst alias in HBM's channel/bank map, some
+    # offsets recover the rate
+    for off in (4 << 10, 64 << 10, 1 << 20, (2 << 20) + (4 << 10), (16 << 20) + (64 << 10)):
+        pairs[f"gib_src+{off >> 10}k"] = (d_gib, s_gib.offset(off), N)
     for name, (d, s, n) in pairs.items():
         ctx.fill("float32", "round", 11, s, n)
         ctx.fill("float32", "round", 12, d, n)
