@@ -79,6 +79,9 @@ for k in ('plain', 'torch'):
     timeout -k 10 200 python -u scripts/alloc_scan.py ${P}_1024.json 8 1024 3 > ${P}_1024.log 2>&1 || { tail -5 ${P}_1024.log; exit 1; }
     timeout -k 10 200 python -u scripts/alloc_scan.py ${P}_arena.json 1 8192 3 512 > ${P}_arena.log 2>&1 || { tail -5 ${P}_arena.log; exit 1; }
     tail -1 ${P}_256.log; tail -1 ${P}_1024.log; tail -1 ${P}_arena.log ;;
+  alias)
+    step alias
+    timeout -k 10 200 python -u scripts/alias_probe.py $OUT/alias_$(date +%H%M%S).json 6 2 ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }
