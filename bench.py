@@ -1100,8 +1100,13 @@ def main():
     # stream-ordered without host syncs
     ctx = xucg_amd.DevContext.on_torch_stream(local_rank) if dist else \
         xucg_amd.DevContext(device=local_rank)
-    src = ctx.alloc(n * 4)
-    dst = ctx.alloc(n * 4)
+    # src and dst as the two halves of ONE allocation. Two separately
+    # allocated operands can alias in HBM's channel/bank map: on some boxes
+    # such pairs combine at 79-83 % where this layout reads 84.5-85 % on every
+    # box probed (scripts/place_probe.py "joint", scripts/alias_probe.py;
+    # DESIGN.md 5, "Operand aliasing"). A fixed layout, not a measured choice.
+    pair = ctx.alloc(2 * n * 4)
+    src, dst = pair.ptr, pair.ptr + n * 4
     ctx.fill("float32", "round", 0x5EED0000 + 2 * rank, src, n)
     ctx.fill("float32", "round", 0x5EED0001 + 2 * rank, dst, n)
     ctx.sync()
@@ -1153,7 +1158,8 @@ def main():
     if not args.no_extra and rank == 0:
         # north-star: 1 GiB fp32 combine, device-resident
         nb = 1 << 28
-        s1, d1 = ctx.alloc(nb * 4), ctx.alloc(nb * 4)
+        pair1 = ctx.alloc(2 * nb * 4)          # one allocation, as the headline pair
+        s1, d1 = pair1.ptr, pair1.ptr + nb * 4
         ctx.fill("float32", "round", 11, s1, nb)
         ctx.fill("float32", "round", 12, d1, nb)
         # steady state, as for the headline kernel: 20 launches (10 ms) bring
@@ -1170,8 +1176,7 @@ def main():
             "frac_of_8tbs": round(g1 / HBM_PEAK_GBS, 4), "target_frac": 0.80,
             "batch_us": [round(b, 2) for b in batches],
             "timing": "20 warm launches, then median of 5 batches of 20 (HIP events)"}
-        s1.free()
-        d1.free()
+        pair1.free()
         extra["same_box_reference_kernels"] = same_box_reference(n)
         # H2D/D2H-inclusive rate: host-resident (pinned) buffers, pipelined
         hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)
@@ -1192,8 +1197,7 @@ def main():
 
     collective, children_ok, collective_bad = None, True, False
     if (world > 1 and not args.no_collective) or args.collective_force:
-        src.free()
-        dst.free()
+        pair.free()
         ctx.close()
         collective, children_ok = run_collective_children(dist, rank, world)
 
@@ -1221,6 +1225,7 @@ def main():
                 "workload": "BASELINE config 2: device-resident local combine dst += src, "
                             "2 x 256 MiB fp32 per GPU (ucg_builtin_dev_reduce)",
                 "count": n, "op": "sum", "bytes_per_step_per_gpu": bytes_per_step,
+                "layout": "src and dst the two halves of one 512 MiB allocation",
                 "parallelism": f"{world} independent per-rank shards (no data-path collective)",
             },
             "roofline": {
