@@ -854,8 +854,8 @@ def same_box_reference(n, iters=50):
     bytes), timed with events on torch's stream. HBM throughput differs by a
     few per cent from box to box; these put the combine's number in context."""
     import torch
-    a = torch.rand(n, device="cuda")
-    b = torch.rand(n, device="cuda")
+    ab = torch.rand(2 * n, device="cuda")      # one allocation, as the headline pair
+    a, b = ab[:n], ab[n:]
 
     def time_us(fn):
         for _ in range(5):
@@ -869,7 +869,7 @@ def same_box_reference(n, iters=50):
         return e0.elapsed_time(e1) * 1e3 / iters
     add_us = time_us(lambda: b.add_(a))
     copy_us = time_us(lambda: b.copy_(a))
-    del a, b
+    del a, b, ab
     torch.cuda.empty_cache()
     return {"torch_add_inplace_us": round(add_us, 3),
             "torch_add_inplace_gbs": round(3 * n * 4 / (add_us * 1e-6) / 1e9, 1),
