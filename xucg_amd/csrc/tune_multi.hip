@@ -352,6 +352,30 @@ int main(int argc, char **argv)
                            d, s, 0u, nv);
     }, {}});
     const size_t nvariants_checked = vs.size();
+    /* operands AND dst in one allocation (dst after the 8 operands, each
+     * S + pad apart): the product kernel on the one-allocation layout that
+     * avoids operand aliasing for the 2-operand combine;
+     * timing only (the same kernel as the product, other pointers) */
+    for (size_t pad : {(size_t)0, (size_t)4096}) {
+        char *big;
+        CHECK(hipMalloc(&big, (N + 1) * (n * 4 + pad)));
+        stag.push_back(big);
+        SrcList ss;
+        for (int m = 0; m < kMaxMulti; m++) {
+            ss.p[m] = m < N ? big + m * (n * 4 + pad) : nullptr;
+        }
+        for (int m = 0; m < N; m++) {
+            CHECK(hipMemcpy(const_cast<void*>(ss.p[m]), bufs[m], n * 4, hipMemcpyDeviceToDevice));
+        }
+        float *jd = reinterpret_cast<float*>(big + N * (n * 4 + pad));
+        vs.push_back({"product, operands and dst in one allocation, S+" + std::to_string(pad) +
+                      " apart (unchecked)",
+                      [=](float *, SrcList, size_t nv, hipStream_t q) {
+            unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
+            hipLaunchKernelGGL((k_reduce_multi<float, 0, N>), dim3(g), dim3(kReduceBlock), 0, q,
+                               jd, ss, 0u, (size_t)0, nv, (size_t)0);
+        }, {}});
+    }
     vs.push_back({"N loads + 1 store, XOR fold (unchecked)",
                   [=](float *d, SrcList s, size_t nv, hipStream_t q) {
         hipLaunchKernelGGL(k_multi_xor_store, dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, q,
