@@ -82,6 +82,9 @@ for k in ('plain', 'torch'):
   alias)
     step alias
     timeout -k 10 200 python -u scripts/alias_probe.py $OUT/alias_$(date +%H%M%S).json 6 2 ;;
+  aliasj)
+    step aliasj
+    timeout -k 10 200 python -u scripts/alias_probe.py $OUT/aliasj_$(date +%H%M%S).json 4 2 --joint ;;
   smoke)
     step smoke
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; }
