@@ -106,7 +106,11 @@ def main():
             rc = 1
     for c in colls:
         c.close()
-    if ring_cells <= 4 and group.stats()["resends"] == 0:
+    # with every message on the remote-key steps only small control messages
+    # use the ring, and whether 3 cells ever fill depends on the peers' timing:
+    # the resend check holds for the data-carrying ring only
+    zcopy = os.environ.get("UCX_BUILTIN_SHM_ZCOPY_THRESH", "") == "1"
+    if ring_cells <= 4 and not zcopy and group.stats()["resends"] == 0:
         print(f"rank {rank}: expected UCS_ERR_NO_RESOURCE resends with {ring_cells} cells",
               flush=True)
         rc = 1
