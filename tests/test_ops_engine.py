@@ -474,3 +474,51 @@ def test_rma_pool_size_classes(monkeypatch):
     assert len(segs()) == before
     iface.close()
     cmb.close()
+
+
+ASSOC_CASES = [  # (world, kind, keys)
+    (2, "allreduce", ()), (4, "allreduce", ()), (8, "allreduce", ()),
+    (4, "allreduce", ("factor=4",)), (16, "allreduce", ("factor=4",)),
+    (8, "allreduce", ("factor=4",)),                  # not a power of 4: one-host tree
+    (3, "allreduce", ()), (5, "allreduce", ()), (6, "allreduce", ()),
+    (5, "reduce", ("root=0",)), (5, "reduce", ("root=3",)),
+    (8, "allreduce", ("ppn=4",)), (8, "allreduce", ("ppn=2",)),
+    (6, "allreduce", ("ppn=3",)), (12, "allreduce", ("ppn=4",)),
+]
+
+
+@pytest.mark.parametrize("transport", ["am", "remote_key"])
+@pytest.mark.parametrize("world,kind,keys", ASSOC_CASES)
+def test_association_traced_against_reference_text(world, kind, keys, transport):
+    """The engine's actual reduction trees, recorded by a reduce_cb_f that
+    writes "(" src dst ")" into dst, checked against trees derived from the
+    reference's text (tests/_worker_assoc.py). This pins the association the
+    GPU's one-shot kernels reproduce without going through the planner code
+    or oracle/plans.py: recursive doubling and K-ing, the one-host and
+    multi-host fan-in/fan-out trees of groups that are not a power of two,
+    MPI_Reduce to a non-zero root, and host fan-in + recursive doubling over
+    host masters + fan-out. Several fragments per step (max_short 256: 3
+    elements of 64 B per fragment); `remote_key`: every message on the
+    shared-memory remote-key steps."""
+    env = {"UCX_BUILTIN_SHM_ZCOPY_THRESH": "1"} if transport == "remote_key" else None
+    codes, outs = launch("_worker_assoc.py", world,
+                         args=(shm_name(), kind, 256, 10) + keys, timeout=120, env_extra=env)
+    assert codes == [0] * world, "\n".join(outs)
+    rows = {}   # member -> the hashes of its result, one per start
+    for r, out in enumerate(outs):
+        for line in out.splitlines():
+            if " rows " in line:
+                rows.setdefault(r, []).append(line.split(" rows ")[1])
+    kv = dict(k.split("=") for k in keys)
+    if kind == "reduce":
+        assert list(rows) == [int(kv["root"])]
+        return
+    assert sorted(rows) == list(range(world))
+    ppn, factor = int(kv.get("ppn", world)), int(kv.get("factor", 2))
+    one_tree = world & (world - 1) or (ppn == world and factor ** round(
+        np.log(world) / np.log(factor)) != world)
+    for r in range(world):
+        # a fanned-out result is a copy of the root's (the tree) or of the
+        # host master's (recursive over masters), start by start
+        src = 0 if one_tree else (r - r % ppn if ppn < world else r)
+        assert rows[r] == rows[src], (r, src, rows)
