@@ -75,9 +75,10 @@ static ucs_status_t hip_status(hipError_t e, const char *what)
 struct LaunchCfg {
     int max_blocks;  /* grid cap for the streaming kernels */
     int variant;     /* fp32-SUM tuning variant (0 = product default) */
+    int multi_waves; /* waves per CU of the multi-operand kernels: -1 table */
 };
 
-static LaunchCfg g_cfg = {-1, -1};
+static LaunchCfg g_cfg = {-1, -1, -1};
 
 static const LaunchCfg &launch_cfg()
 {
@@ -90,6 +91,10 @@ static const LaunchCfg &launch_cfg()
             g_cfg.max_blocks = 2048;
         }
         g_cfg.variant = v ? atoi(v) : 0; /* 0: the product geometry */
+        /* UCX_BUILTIN_DEV_MULTI_WAVES: "auto" (unset) = the measured table
+         * below, 0 = no cap, W = at most W waves per CU for every count */
+        const char *w = getenv("UCX_BUILTIN_DEV_MULTI_WAVES");
+        g_cfg.multi_waves = (w && strcmp(w, "auto") != 0) ? atoi(w) : -1;
     });
     return g_cfg;
 }
@@ -103,6 +108,38 @@ int launch_max_blocks()
 int launch_variant()
 {
     return launch_cfg().variant;
+}
+
+/* Occupancy of the multi-operand kernels (k_reduce_multi, k_reduce_tree and
+ * their realigning forms). With every CU full of one-wave workgroups, each
+ * holding one 16-B load of every operand, HBM serves (operands + 1) streams
+ * from ~32 waves per CU and loses 5-10 points to it; capping the workgroups
+ * per CU gains them back (tools/tune_occ, profiles/r03/r03s2occ: N = 8 fp32
+ * SUM at 64 MiB per operand 77.6 % of 8 TB/s uncapped, 85.8 % at 8 waves per
+ * CU). The cap is dynamic LDS the kernels never touch: at most W workgroups
+ * fit a CU's 160 KiB. Best cap per number of distinct operands, measured
+ * (DESIGN.md 3); two operands (the 2-operand combine's shape) run uncapped. */
+static int multi_waves_for(unsigned operands)
+{
+    if (operands <= 2)  return 0;
+    if (operands == 3)  return 20;
+    if (operands <= 7)  return 12;
+    if (operands == 8)  return 8;
+    if (operands <= 12) return 10;
+    return 8;
+}
+
+size_t multi_lds_bytes(unsigned operands)
+{
+    int w = launch_cfg().multi_waves;
+    if (w < 0) {
+        w = multi_waves_for(operands);
+    }
+    if (w <= 0) {
+        return 0;
+    }
+    constexpr size_t kLdsPerCu = 160 * 1024;   /* gfx950 */
+    return kLdsPerCu / (size_t)w / 512 * 512;
 }
 }  // namespace ucgdev
 

@@ -406,6 +406,22 @@ int main(int argc, char **argv)
         }
         goto run;
     }
+    if (getenv("TUNE_OCC")) {
+        /* occupancy A/B: the product kernel with dynamic LDS that the kernel
+         * does not use, so that at most W one-wave workgroups fit a CU
+         * (160 KiB of LDS per CU); fewer loads in flight per CU */
+        for (int W : {4, 8, 12, 16, 20, 24, 28}) {
+            const size_t lds = (size_t)163840 / W / 512 * 512;
+            char buf[128];
+            snprintf(buf, sizeof(buf), "product, <= %d waves per CU (LDS %zu B)", W, lds);
+            vs.push_back({buf, [=](float *d, const float *s, size_t nv, hipStream_t q) {
+                unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
+                hipLaunchKernelGGL((k_reduce<float, 0, kReduceU, 1, kReduceBlock>), dim3(g),
+                                   dim3(kReduceBlock), lds, q, d, s, (size_t)0, nv, (size_t)0);
+            }, {}});
+        }
+        goto run;
+    }
     if (getenv("TUNE_XCD_ONLY")) {
         xcd(0);
         xcd(16);

@@ -272,6 +272,23 @@ int main(int argc, char **argv)
         hipLaunchKernelGGL((k_reduce_multi<float, 0, N>), dim3(g), dim3(kReduceBlock), 0, q,
                            d, s, 0u, (size_t)0, nv, (size_t)0);
     }, {}});
+    const bool occ = getenv("TUNE_OCC") != nullptr;
+    if (occ) {
+        /* occupancy A/B: dynamic LDS the kernel does not use caps the
+         * one-wave workgroups per CU at W (160 KiB of LDS per CU): fewer
+         * operand streams in flight at once */
+        for (int W : {4, 6, 8, 12, 16, 20, 24, 28}) {
+            const size_t lds = (size_t)163840 / W / 512 * 512;
+            vs.push_back({"product, <= " + std::to_string(W) + " waves per CU",
+                          [=](float *d, SrcList s, size_t nv, hipStream_t q) {
+                unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
+                hipLaunchKernelGGL((k_reduce_multi<float, 0, N>), dim3(g), dim3(kReduceBlock),
+                                   lds, q, d, s, 0u, (size_t)0, nv, (size_t)0);
+            }, {}});
+        }
+    }
+    std::vector<char*> stag;
+    if (!occ) {
 #define VAR(U, BS, NTL, CONTIG)                                                       \
     vs.push_back({"var U" #U " BS" #BS " NTL" #NTL " CONTIG" #CONTIG,                 \
                   [=](float *d, SrcList s, size_t nv, hipStream_t q) {                \
@@ -320,7 +337,6 @@ int main(int argc, char **argv)
     /* the operands at staggered offsets inside one allocation: operand m at
      * m * (S + pad); tests whether N streams at equal offsets of 2^k-sized
      * buffers collide in the HBM channel/bank map */
-    std::vector<char*> stag;
     for (size_t pad : {(size_t)4096, (size_t)65536, (size_t)(1 << 20) + 4096, (size_t)(2 << 20) + 256 * 1024 + 4096}) {
         char *big;
         CHECK(hipMalloc(&big, N * (n * 4 + pad)));
@@ -351,7 +367,9 @@ int main(int argc, char **argv)
         hipLaunchKernelGGL(k_multi_alt_order, dim3((unsigned)((nv + 63) / 64)), dim3(64), 0, q,
                            d, s, 0u, nv);
     }, {}});
+    }
     const size_t nvariants_checked = vs.size();
+    if (!occ) {
     /* operands AND dst in one allocation (dst after the 8 operands, each
      * S + pad apart): the product kernel on the one-allocation layout that
      * avoids operand aliasing for the 2-operand combine;
@@ -382,6 +400,7 @@ int main(int argc, char **argv)
                            d, s, 0u, nv);
     }, {}});
     /* the 2-operand combine on operands 0 and 1 (3 streams), same process */
+    }
     vs.push_back({"2-operand k_reduce on two of the buffers (3*S bytes)",
                   [=](float *d, SrcList s, size_t nv, hipStream_t q) {
         unsigned g = (unsigned)((nv + kReduceBlock - 1) / kReduceBlock);
