@@ -321,6 +321,13 @@ ucs_status_t ucg_builtin_dev_host_register(ucg_builtin_dev_ctx_t *ctx, void *ptr
 ucs_status_t ucg_builtin_dev_host_unregister(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                     const void *src, size_t bytes); /* sync */
+/* Diagnostics: what the runtime and this shim know about a device address
+ * (range, attributes, live / parked / imported allocation) and the process's
+ * recent memory events near it (malloc, free, park, IPC import and release),
+ * as text into out[max]; returns the full length. For test harnesses that
+ * find a buffer corrupted. */
+size_t       ucg_builtin_dev_debug_ptr(ucg_builtin_dev_ctx_t *ctx, const void *ptr,
+                                       char *out, size_t max);
 
 /* Fill `count` elements with the counter-based synthetic generator
  * (splitmix64; identical to ucg_oracle_fill() in oracle/combine_ref.c). */

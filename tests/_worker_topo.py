@@ -157,6 +157,7 @@ def main():
         if not (O.bits(chk) == O.bits(a)).all():
             fail(f"UPLOAD LOST before any engine call: {what} at 0x{b.ptr:x}; "
                  f"{identify(chk, a, {'zeros': np.zeros_like(a)})}")
+            diag(b, what)
         return b
 
     def back(b, like):
@@ -196,6 +197,7 @@ def main():
             bad = b.guards_damaged()
             if bad:
                 fail(f"guard zone of {what} at 0x{b.ptr:x} written: {bad}")
+                diag(b, what)
             b.free()
 
     iface = ops.ShmIface(name, n, rank, max_short=max_short, ring_cells=16)
@@ -211,6 +213,20 @@ def main():
         nonlocal rc
         print(f"rank {rank}: MISMATCH {msg}", flush=True)
         rc = 1
+
+    def diag(b, what):
+        """after a corrupted buffer: what the runtime and the device shim know
+        about its allocation, the process's memory events near it, and whether
+        it still reads the same 50 ms later (corruption analysis)"""
+        if not isinstance(b, Guarded):
+            return
+        import time
+        g0 = b.raw.download(np.uint8, GUARD, 0)
+        time.sleep(0.05)
+        g1 = b.raw.download(np.uint8, GUARD, 0)
+        print(f"rank {rank}: DIAG {what} allocation 0x{b.raw.ptr:x} (+{b.raw.nbytes} B): head "
+              f"guard zero bytes {int((g0 == 0).sum())} -> {int((g1 == 0).sum())} after 50 ms\n"
+              + dctx.debug_ptr(b.raw.ptr), flush=True)
 
     kinds = [("allreduce", 0)] + [("reduce", r) for r in sorted({0, n - 1, n // 2})]
     seen = {}          # recent arrays, for identify() on a mismatch
@@ -267,6 +283,7 @@ def main():
                         fail(f"{kind} {dt} {op}: send buffer changed before start {rep} "
                              f"(no engine call has touched it): "
                              f"{identify(pre, inputs[rank], {'zeros': np.zeros_like(pre)})}")
+                        diag(sbuf, "send buffer")
                 st = coll.run()
                 got = back(rbuf, inputs[rank]) if rbuf is not None else None
                 if st != 0:

@@ -96,6 +96,22 @@ def test_self_combine(dev_ctx):
     assert (bits(b.download(np.float32, n)) == bits(O.reduce("sum", "float32", x, x))).all()
 
 
+def test_debug_ptr_memory_events(dev_ctx):
+    """ucg_builtin_dev_debug_ptr: the runtime's view of a live allocation, and
+    the malloc / free events of its address in the shim's event log (the
+    diagnostics the device-buffer placement worker prints on a corrupted
+    buffer)."""
+    b = dev_ctx.alloc(3 << 20)
+    p = b.ptr
+    live = dev_ctx.debug_ptr(p + 100)
+    assert "runtime range ok" in live and "own allocation" in live, live
+    assert f" M ptr 0x{p:x}" in live, live
+    b.free()
+    gone = dev_ctx.debug_ptr(p)
+    assert f" F ptr 0x{p:x}" in gone and "rc 0" in gone, gone
+    assert "own allocation" not in gone, gone
+
+
 def test_argument_errors(dev_ctx):
     b = dev_ctx.alloc(4096)
     # partial overlap

@@ -1321,6 +1321,35 @@ std::mutex g_alloc_mu;
 std::unordered_map<void*, own_alloc> g_allocs;                  /* live and parked */
 std::multimap<std::pair<int, size_t>, void*> g_parked;          /* (device, bytes) */
 std::unordered_multimap<void*, void*> g_imports;   /* imported pointer -> mapping base */
+
+/* The last memory events of the process (allocations, frees, parks, IPC
+ * imports and releases), for ucg_builtin_dev_debug_ptr: a buffer found to read
+ * as zeros is matched against what happened to its address range. */
+struct mem_event {
+    char     kind;      /* M malloc, R reuse of a parked one, F free, P park,
+                           I import, C release (close) */
+    void    *ptr;
+    void    *base;
+    size_t   bytes;
+    uint64_t ns;        /* CLOCK_MONOTONIC */
+    int      rc;        /* the runtime's return code */
+};
+constexpr size_t kMemEvents = 1024;
+mem_event g_events[kMemEvents];
+uint64_t  g_nevents;                                 /* under g_alloc_mu */
+
+uint64_t now_ns()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+/* caller holds g_alloc_mu */
+void note_event(char kind, void *ptr, void *base, size_t bytes, int rc)
+{
+    g_events[g_nevents++ % kMemEvents] = mem_event{kind, ptr, base, bytes, now_ns(), rc};
+}
 }
 
 struct ipc_blob {
@@ -1356,6 +1385,7 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
         if (it != g_allocs.end()) {
             it->second.exported = true;
         }
+        note_event('X', (void*)dev_ptr, (void*)base, size, 0);
     }
     b.offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
     b.size   = (uint64_t)size;
@@ -1399,6 +1429,7 @@ ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
     *dev_ptr = (char*)base + b.offset;
     std::lock_guard<std::mutex> g(g_alloc_mu);
     g_imports.emplace(*dev_ptr, base);
+    note_event('I', *dev_ptr, base, (size_t)b.size, 0);
     return UCS_OK;
 }
 
@@ -1424,7 +1455,12 @@ ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx, void *dev_p
         HIP_TRY(hipMemGetAddressRange(&b, &size, (hipDeviceptr_t)dev_ptr));
         base = (void*)b;
     }
-    HIP_TRY(hipIpcCloseMemHandle(base));
+    const hipError_t e = hipIpcCloseMemHandle(base);
+    {
+        std::lock_guard<std::mutex> g(g_alloc_mu);
+        note_event('C', dev_ptr, base, 0, (int)e);
+    }
+    HIP_TRY(e);
     return UCS_OK;
 }
 
@@ -1449,6 +1485,7 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
             p = it->second;
             g_parked.erase(it);
             g_allocs[p].parked = false;
+            note_event('R', p, p, bytes, 0);
             return p;
         }
     }
@@ -1464,6 +1501,7 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
     }
     std::lock_guard<std::mutex> g(g_alloc_mu);
     g_allocs[p] = own_alloc{device, bytes, false, false};
+    note_event('M', p, p, bytes, 0);
     return p;
 }
 
@@ -1488,12 +1526,81 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
                     it->second.parked = true;
                     g_parked.emplace(std::make_pair(it->second.device, it->second.bytes), ptr);
                 }
+                note_event('P', ptr, ptr, it->second.bytes, 0);
                 return;
             }
             g_allocs.erase(it);
         }
     }
-    (void)hipFree(ptr);
+    const hipError_t e = hipFree(ptr);
+    std::lock_guard<std::mutex> g(g_alloc_mu);
+    note_event('F', ptr, ptr, 0, (int)e);
+}
+
+/* Diagnostics for a buffer found corrupted (tests/_worker_topo.py): what the
+ * runtime says about the address now, whether it lies in a live, parked or
+ * imported range of this shim, and the recorded memory events whose range
+ * comes within 4 MiB of it, oldest first. */
+size_t ucg_builtin_dev_debug_ptr(ucg_builtin_dev_ctx_t *ctx, const void *ptr, char *out,
+                                 size_t max)
+{
+    std::string t;
+    char line[256];
+    if (ctx) {
+        (void)hipSetDevice(ctx->device);
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    const hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
+    snprintf(line, sizeof(line), "address %p: runtime range %s base %p size %zu\n", ptr,
+             e == hipSuccess ? "ok" : hipGetErrorString(e), (void*)base, size);
+    t += line;
+    (void)hipGetLastError();
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof(at));
+    const hipError_t ea = hipPointerGetAttributes(&at, ptr);
+    snprintf(line, sizeof(line), "attributes %s: type %d device %d devptr %p\n",
+             ea == hipSuccess ? "ok" : hipGetErrorString(ea), (int)at.type, at.device,
+             at.devicePointer);
+    t += line;
+    (void)hipGetLastError();
+    const uintptr_t a = (uintptr_t)ptr, win = (uintptr_t)4 << 20;
+    std::lock_guard<std::mutex> g(g_alloc_mu);
+    for (const auto &kv : g_allocs) {
+        const uintptr_t p = (uintptr_t)kv.first;
+        if (a >= p && a < p + kv.second.bytes) {
+            snprintf(line, sizeof(line), "own allocation %p + %zu exported %d parked %d\n",
+                     kv.first, kv.second.bytes, (int)kv.second.exported,
+                     (int)kv.second.parked);
+            t += line;
+        }
+    }
+    for (const auto &kv : g_imports) {
+        const uintptr_t p = (uintptr_t)kv.second;
+        if (a >= p && a < p + win) {
+            snprintf(line, sizeof(line), "import mapping base %p (pointer %p)\n", kv.second,
+                     kv.first);
+            t += line;
+        }
+    }
+    const uint64_t first = g_nevents > kMemEvents ? g_nevents - kMemEvents : 0;
+    const uint64_t now = now_ns();
+    for (uint64_t i = first; i < g_nevents; i++) {
+        const mem_event &ev = g_events[i % kMemEvents];
+        const uintptr_t lo = (uintptr_t)(ev.base ? ev.base : ev.ptr);
+        if (lo + win > a && lo < a + win) {
+            snprintf(line, sizeof(line), "event #%llu %c ptr %p base %p bytes %zu rc %d, %.3f ms ago\n",
+                     (unsigned long long)i, ev.kind, ev.ptr, ev.base, ev.bytes, ev.rc,
+                     (double)(now - ev.ns) * 1e-6);
+            t += line;
+        }
+    }
+    if (out && max) {
+        const size_t n = t.size() < max - 1 ? t.size() : max - 1;
+        memcpy(out, t.data(), n);
+        out[n] = '\0';
+    }
+    return t.size();
 }
 
 void *ucg_builtin_dev_host_alloc(size_t bytes)

@@ -178,6 +178,13 @@ class DevContext:
     def alloc(self, nbytes):
         return DevBuffer(self, nbytes)
 
+    def debug_ptr(self, ptr):
+        """what the runtime and the shim know about a device address, and the
+        process's recent memory events near it (diagnostics)"""
+        buf = ctypes.create_string_buffer(1 << 16)
+        _lib.dev().ucg_builtin_dev_debug_ptr(self.handle, _ptr(ptr), buf, len(buf))
+        return buf.value.decode(errors="replace")
+
     def fill(self, dt, dist, seed, buf, count):
         check(_lib.dev().ucg_builtin_dev_fill(self.handle, dt_index(dt), dist_index(dist),
                                               seed, _ptr(buf), count), "ucg_builtin_dev_fill")
