@@ -129,13 +129,16 @@ static int multi_waves_for(unsigned operands)
     return 8;
 }
 
-size_t multi_lds_bytes(unsigned operands)
+size_t multi_lds_bytes(unsigned operands, size_t grid)
 {
     int w = launch_cfg().multi_waves;
     if (w < 0) {
         w = multi_waves_for(operands);
     }
-    if (w <= 0) {
+    /* a grid that fits the chip under the cap runs uncapped: nothing to limit
+     * (the engine's small messages, latency-bound launches) */
+    constexpr size_t kCus = 256;               /* MI355X */
+    if (w <= 0 || grid <= kCus * (size_t)w) {
         return 0;
     }
     constexpr size_t kLdsPerCu = 160 * 1024;   /* gfx950 */

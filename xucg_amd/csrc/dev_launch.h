@@ -22,9 +22,11 @@ namespace ucgdev {
 int launch_max_blocks();
 /* UCX_BUILTIN_DEV_VARIANT: A/B tuning knob (0 = product); defined likewise */
 int launch_variant();
-/* dynamic LDS that caps the waves per CU of a multi-operand launch reading
- * `operands` distinct buffers (UCX_BUILTIN_DEV_MULTI_WAVES); likewise */
-size_t multi_lds_bytes(unsigned operands);
+/* dynamic LDS that caps the waves per CU of a multi-operand launch of `grid`
+ * one-wave workgroups reading `operands` distinct buffers
+ * (UCX_BUILTIN_DEV_MULTI_WAVES); 0 for a grid the cap would not limit;
+ * likewise */
+size_t multi_lds_bytes(unsigned operands, size_t grid);
 
 inline size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
 
@@ -265,7 +267,6 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         xm = xm || straddles_lines(static_cast<const T*>(srcs.p[m]) + head);
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
-    const size_t lds = multi_lds_bytes(N);   /* occupancy cap (dev_combine.hip) */
     size_t done = 0;
     do {
         const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
@@ -280,6 +281,7 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             if (first && div_up(head, kReduceBlock) > grid) {
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
+            const size_t lds = multi_lds_bytes(N, grid);   /* occupancy cap */
             if (xm)
                 hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1>), dim3(grid), dim3(kReduceBlock),
                                    lds, st, d + off, sl, self, first ? head : 0, chunk,
@@ -294,6 +296,7 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
+            const size_t lds = multi_lds_bytes(N, grid);
             hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N>), dim3(grid), dim3(kReduceBlock),
                                lds, st, d + off, sl, self, first ? head : 0, chunk,
                                last ? tail : 0);
@@ -360,7 +363,6 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
                    size_t tail, bool aligned, bool xm, hipStream_t st)
 {
     constexpr size_t V = 16 / sizeof(T);
-    const size_t lds = multi_lds_bytes(n);   /* occupancy cap (dev_combine.hip) */
     size_t done = 0;
     do {
         const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
@@ -375,6 +377,7 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             if (first && div_up(head, kReduceBlock) > grid) {
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
+            const size_t lds = multi_lds_bytes(n, grid);   /* occupancy cap */
             if (xm)
                 hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1>), dim3(grid),
                                    dim3(kReduceBlock), lds, st, d + off, sl, n, first ? head : 0,
@@ -389,6 +392,7 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
+            const size_t lds = multi_lds_bytes(n, grid);
             hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX>), dim3(grid),
                                dim3(kReduceBlock), lds, st, d + off, sl, n, first ? head : 0,
                                chunk, last ? tail : 0);
