@@ -877,6 +877,43 @@ def same_box_reference(n, iters=50):
             "d2d_copy_gbs": round(2 * n * 4 / (copy_us * 1e-6) / 1e9, 1)}
 
 
+def one_shot_shape(ctx, nsrc=8, per_op=64 << 20, iters=20):
+    """The C4/C5 one-shot reduce-scatter's kernel on one GPU: 8 local operands
+    of 64 MiB (ucg_builtin_dev_reduce_multi, the recursive-doubling
+    association, occupancy-capped), operands and output in one
+    allocation. (N + 1) x S algorithmic bytes per launch; wall clock over
+    back-to-back launches after a warm-up, then a sampled exactness check
+    ("exact" inputs: every association gives the same bits)."""
+    import numpy as np
+    n = per_op // 4
+    arena = ctx.alloc((nsrc + 1) * per_op)
+    srcs = [arena.ptr + m * per_op for m in range(nsrc)]
+    dst = arena.ptr + nsrc * per_op
+    for m, p in enumerate(srcs):
+        ctx.fill("float32", "exact", 300 + m, p, n)
+    for _ in range(3):
+        assert ctx.reduce_multi("sum", "float32", dst, srcs, 0, n) == 0
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        ctx.reduce_multi("sum", "float32", dst, srcs, 0, n)
+    ctx.sync()
+    us = (time.perf_counter() - t0) / iters * 1e6
+    w = 1 << 16
+    lo = (n // 2) & ~15
+    want = sum(arena.download(np.float32, w, m * per_op + lo * 4).astype(np.float64)
+               for m in range(nsrc))
+    got = arena.download(np.float32, w, nsrc * per_op + lo * 4)
+    ok = bool(np.array_equal(got.astype(np.float64), want))
+    arena.free()
+    gbs = (nsrc + 1) * per_op / (us * 1e-6) / 1e9
+    return {"operands": nsrc, "bytes_per_operand": per_op, "us": round(us, 2),
+            "achieved_gbs": round(gbs, 1), "frac_of_8tbs": round(gbs / HBM_PEAK_GBS, 4),
+            "sampled_exact": ok,
+            "note": "k_reduce_multi, operands + output in one allocation, wall clock over "
+                    f"{iters} back-to-back launches"}
+
+
 def run_collective_children(dist, rank, world, timeout_s=300):
     """Run collective_phases in one child process per rank (a fresh process
     group on a new port), so that a fault in the multi-GPU phases - the IPC
@@ -1177,6 +1214,7 @@ def main():
             "batch_us": [round(b, 2) for b in batches],
             "timing": "20 warm launches, then median of 5 batches of 20 (HIP events)"}
         pair1.free()
+        extra["one_shot_8_operands_64mib_fp32"] = one_shot_shape(ctx)
         extra["same_box_reference_kernels"] = same_box_reference(n)
         # H2D/D2H-inclusive rate: host-resident (pinned) buffers, pipelined
         hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)
