@@ -110,8 +110,8 @@ int launch_variant()
     return launch_cfg().variant;
 }
 
-/* Occupancy of the multi-operand kernels (k_reduce_multi, k_reduce_tree and
- * their realigning forms). With every CU full of one-wave workgroups, each
+/* Occupancy of the multi-operand kernels (k_reduce_multi, k_reduce_tree; their
+ * realigning forms run uncapped, which measured better). With every CU full of one-wave workgroups, each
  * holding one 16-B load of every operand, HBM serves (operands + 1) streams
  * from ~32 waves per CU and loses 5-10 points to it; capping the workgroups
  * per CU gains them back (tools/tune_occ, profiles/r03/r03s2occ: N = 8 fp32

@@ -296,9 +296,10 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
-            const size_t lds = multi_lds_bytes(N, grid);
+            /* uncapped: the realigning form lost 2-4 points under the cap on
+             * two boxes (profiles/r03/shift2) */
             hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N>), dim3(grid), dim3(kReduceBlock),
-                               lds, st, d + off, sl, self, first ? head : 0, chunk,
+                               0, st, d + off, sl, self, first ? head : 0, chunk,
                                last ? tail : 0);
         }
         done += chunk;
@@ -392,9 +393,9 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
-            const size_t lds = multi_lds_bytes(n, grid);
+            /* uncapped, as k_reduce_multi_shift */
             hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX>), dim3(grid),
-                               dim3(kReduceBlock), lds, st, d + off, sl, n, first ? head : 0,
+                               dim3(kReduceBlock), 0, st, d + off, sl, n, first ? head : 0,
                                chunk, last ? tail : 0);
         }
         done += chunk;
