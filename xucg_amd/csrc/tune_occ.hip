@@ -80,6 +80,23 @@ int main(int argc, char **argv)
     CHECK(hipDeviceSynchronize());
 
     std::vector<Case> cs;
+    /* TUNE_OCC_PMC=1: only N = 8 uncapped and at 8 waves per CU, for the
+     * rocprofv3 counter passes (scripts/occ_pmc.sh) */
+    const bool pmc = getenv("TUNE_OCC_PMC") != nullptr;
+    if (pmc) {
+        for (int w : {0, 8}) {
+            const size_t lds = lds_for(w);
+            cs.push_back({"multi N=8", 8, w, [=](float *d, size_t nv, hipStream_t q) { run_multi<8>(d, all, nv, lds, q); }, {}});
+        }
+        for (int r = 0; r < rounds; r++) {
+            for (auto &c : cs) {
+                c.run(out, nvec, st);
+            }
+        }
+        CHECK(hipStreamSynchronize(st));
+        printf("pmc mode: %d rounds of N=8 uncapped, then capped at 8\n", rounds);
+        return 0;
+    }
     const int caps[] = {0, 4, 6, 8, 10, 12, 14, 16, 20, 24, 28};
     for (int w : caps) {
         const size_t lds = lds_for(w);
