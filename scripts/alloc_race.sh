@@ -6,7 +6,7 @@
 set -u
 OUT=$1; NP=${2:-12}; IT=${3:-400}
 mkdir -p $OUT
-for mode in plain ipc; do
+for mode in ${MODES:-plain ipc}; do
   D=$(mktemp -d /tmp/arp.XXXXXX)
   pids=()
   for r in $(seq 0 $((NP - 1))); do

@@ -13,7 +13,11 @@
  * process also exports a long-lived buffer and imports every peer's, as the
  * engine's pools do, and a kernel reads the imports each iteration.
  *
- *   alloc_race_probe <rank> <nprocs> <iters> <mode: plain|ipc> <shm-dir>
+ *   alloc_race_probe <rank> <nprocs> <iters> <mode: plain|ipc|lds> <shm-dir>
+ *
+ * Mode "lds" (no IPC) adds what the engine did when the zeroed allocations
+ * were most frequent: each iteration also launches small kernels with
+ * 20 KiB of dynamic LDS they never touch on four streams of the process.
  *
  * Prints one line: iterations, buffers whose content changed after the
  * verified upload (and how many of those read as all zeros).
@@ -31,6 +35,16 @@
 
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+/* a few workgroups holding dynamic LDS they never touch (the occupancy cap's
+ * launches on small grids) */
+__global__ void k_small(uint32_t *out, const uint32_t *in, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        out[i] = in[i] ^ 0x5a5a5a5au;
+    }
+}
 
 __global__ void k_touch(uint32_t *out, const uint32_t *in, size_t n, const uint32_t *peer,
                         size_t pn)
@@ -60,6 +74,7 @@ int main(int argc, char **argv)
     }
     const int rank = atoi(argv[1]), nprocs = atoi(argv[2]), iters = atoi(argv[3]);
     const bool ipc = strcmp(argv[4], "ipc") == 0;
+    const bool lds = strcmp(argv[4], "lds") == 0;
     const std::string dir = argv[5];
     const size_t bytes = (size_t)2 << 20;           /* one 2 MiB granule */
     const size_t n = bytes / 4;
@@ -98,6 +113,14 @@ int main(int argc, char **argv)
     size_t changed = 0, zeros = 0, checked = 0, upload_lost = 0;
     hipStream_t st;
     CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    hipStream_t side[4];
+    uint32_t *scratch = nullptr;
+    if (lds) {
+        for (auto &q : side) {
+            CHECK(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+        }
+        CHECK(hipMalloc(&scratch, 4 * 4096 * sizeof(uint32_t)));
+    }
     for (int it = 0; it < iters; it++) {
         uint32_t *a = nullptr, *b = nullptr;
         CHECK(hipMalloc(&a, bytes));
@@ -112,6 +135,15 @@ int main(int argc, char **argv)
                            : static_cast<const uint32_t*>(peers[it % peers.size()]);
         hipLaunchKernelGGL(k_touch, dim3((unsigned)(n / 256)), dim3(256), 0, st, b, a, n,
                            pp, n);
+        if (lds) {
+            for (int k = 0; k < 4; k++) {
+                hipLaunchKernelGGL(k_small, dim3(4), dim3(64), 20480, side[k],
+                                   scratch + k * 4096, a + k * 4096, (size_t)256);
+            }
+            for (auto &q : side) {
+                CHECK(hipStreamSynchronize(q));
+            }
+        }
         CHECK(hipStreamSynchronize(st));
         /* a pause of 0-2 ms, as a test process has between upload and use */
         std::this_thread::sleep_for(std::chrono::microseconds((it * 7919 + rank * 104729) % 2000));
@@ -132,7 +164,10 @@ int main(int argc, char **argv)
         CHECK(hipIpcCloseMemHandle(p));
     }
     printf("rank %d mode %s iters %d checked %zu changed %zu all_zero %zu upload_lost %zu\n",
-           rank, ipc ? "ipc" : "plain", iters, checked, changed, zeros, upload_lost);
+           rank, argv[4], iters, checked, changed, zeros, upload_lost);
+    if (scratch) {
+        CHECK(hipFree(scratch));
+    }
     if (mine) {
         /* peers may still hold the mapping: wait for them before freeing */
         const std::string f = dir + "/done" + std::to_string(rank);
