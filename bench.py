@@ -413,6 +413,16 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             for _ in range(warmup):
                 rs()
             t_rs = timed(rs, steps)
+            # the same reduce-scatter with the multi-operand kernel uncapped
+            # ("Occupancy cap": tuned on local HBM; here 7 of 8
+            # operands come over xGMI), then the table again
+            from xucg_amd import _lib as L
+            L.dev().ucg_builtin_dev_set_multi_waves(0)
+            try:
+                rs()
+                t_rs_uncapped = timed(rs, steps)
+            finally:
+                L.dev().ucg_builtin_dev_set_multi_waves(-1)
             dist.reduce_scatter_tensor(rs_out, x)
             torch.cuda.synchronize()
             same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
@@ -565,6 +575,8 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                 "rs_frac_of_xgmi": round(bus / t_rs / 1e9 / XGMI_GBS, 4),
                 "rs_frac_of_xgmi_per_direction": round(bus / t_rs / 1e9 / XGMI_DIR_GBS, 4),
                 "rs_ag_ms": round((t_rs + t_ag) * 1e3, 3),
+                "oneshot_rs_uncapped_ms": round(t_rs_uncapped * 1e3, 3),
+                "oneshot_rs_uncapped_busbw_gbs": round(bus / t_rs_uncapped / 1e9, 1),
                 "oneshot_ag_ms": round(t_ag1 * 1e3, 3),
                 "oneshot_ag_busbw_gbs": round(bus / t_ag1 / 1e9, 1),
                 "oneshot_rs_ag_ms": round((t_rs + t_ag1) * 1e3, 3),

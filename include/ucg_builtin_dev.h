@@ -321,6 +321,12 @@ ucs_status_t ucg_builtin_dev_host_register(ucg_builtin_dev_ctx_t *ctx, void *ptr
 ucs_status_t ucg_builtin_dev_host_unregister(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                     const void *src, size_t bytes); /* sync */
+/* Waves per CU of the multi-operand kernels on large grids, process-wide:
+ * -1 = the measured table (the default), 0 = uncapped, W = at most W. Overrides
+ * UCX_BUILTIN_DEV_MULTI_WAVES; for A/B runs inside one process (bench.py's
+ * one-shot reduce-scatter over xGMI). */
+void         ucg_builtin_dev_set_multi_waves(int waves);
+
 /* Diagnostics: what the runtime and this shim know about a device address
  * (range, attributes, live / parked / imported allocation) and the process's
  * recent memory events near it (malloc, free, park, IPC import and release),

@@ -93,6 +93,7 @@ DEV_API = {
     "ucg_builtin_dev_host_unregister": (_int, [_vp, _vp]),
     "ucg_builtin_dev_memcpy": (_st, [_vp, _vp, _vp, _sz]),
     "ucg_builtin_dev_debug_ptr": (_sz, [_vp, _vp, ctypes.c_char_p, _sz]),
+    "ucg_builtin_dev_set_multi_waves": (None, [_int]),
     "ucg_builtin_dev_fill": (_st, [_vp, _int, _int, _u64, _vp, _sz]),
     "ucg_builtin_dev_profile_reduce": (_st, [_vp, _int, _int, _vp, _vp, _sz, _u,
                                              ctypes.POINTER(ctypes.c_double)]),

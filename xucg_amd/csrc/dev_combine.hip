@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <climits>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -129,9 +130,14 @@ static int multi_waves_for(unsigned operands)
     return 8;
 }
 
+/* ucg_builtin_dev_set_multi_waves: a process-wide override of the table and
+ * of UCX_BUILTIN_DEV_MULTI_WAVES (INT_MIN = none), for A/B runs in one process */
+static std::atomic<int> g_multi_override{INT_MIN};
+
 size_t multi_lds_bytes(unsigned operands, size_t grid)
 {
-    int w = launch_cfg().multi_waves;
+    const int ov = g_multi_override.load(std::memory_order_relaxed);
+    int w = ov != INT_MIN ? ov : launch_cfg().multi_waves;
     if (w < 0) {
         w = multi_waves_for(operands);
     }
@@ -145,6 +151,11 @@ size_t multi_lds_bytes(unsigned operands, size_t grid)
     return kLdsPerCu / (size_t)w / 512 * 512;
 }
 }  // namespace ucgdev
+
+void ucg_builtin_dev_set_multi_waves(int waves)
+{
+    ucgdev::g_multi_override.store(waves < -1 ? -1 : waves, std::memory_order_relaxed);
+}
 
 /* dispatch tables, assembled from the per-dtype translation units */
 struct Tables {
