@@ -112,14 +112,15 @@ int launch_variant()
 }
 
 /* Occupancy of the multi-operand kernels (k_reduce_multi, k_reduce_tree; their
- * realigning forms run uncapped, which measured better). With every CU full of one-wave workgroups, each
- * holding one 16-B load of every operand, HBM serves (operands + 1) streams
- * from ~32 waves per CU and loses 5-10 points to it; capping the workgroups
- * per CU gains them back (tools/tune_occ, profiles/r03/r03s2occ: N = 8 fp32
- * SUM at 64 MiB per operand 77.6 % of 8 TB/s uncapped, 85.8 % at 8 waves per
- * CU). The cap is dynamic LDS the kernels never touch: at most W workgroups
- * fit a CU's 160 KiB. Best cap per number of distinct operands, measured
- * (DESIGN.md 3); two operands (the 2-operand combine's shape) run uncapped. */
+ * realigning forms run uncapped, which measured better). With every CU full
+ * of one-wave workgroups, each holding one 16-B load of every operand, HBM
+ * serves (operands + 1) streams from ~32 waves per CU and loses 5-10 points
+ * to it; capping the workgroups per CU gains them back (tools/tune_occ,
+ * profiles/r03/r03s2occ: N = 8 fp32 SUM at 64 MiB per operand 77.2-78.8 % of
+ * 8 TB/s uncapped, 84.7-86.2 % at 8 waves per CU on three boxes). The cap is
+ * dynamic LDS the kernels never touch: at most W workgroups fit a CU's
+ * 160 KiB. Best cap per number of distinct operands, measured;
+ * two operands (the 2-operand combine's shape) run uncapped. */
 static int multi_waves_for(unsigned operands)
 {
     if (operands <= 2)  return 0;
