@@ -148,6 +148,9 @@ size_t multi_lds_bytes(unsigned operands, size_t grid)
     if (w <= 0 || grid <= kCus * (size_t)w) {
         return 0;
     }
+    if (w < 4) {
+        w = 4;   /* keeps the request within one workgroup's LDS limit */
+    }
     constexpr size_t kLdsPerCu = 160 * 1024;   /* gfx950 */
     return kLdsPerCu / (size_t)w / 512 * 512;
 }
