@@ -1108,12 +1108,89 @@ def collective_child():
     dist.destroy_process_group()
 
 
+def spawn_ranks(n, timeout_s=None):
+    """`--gpus N` with no launcher (WORLD_SIZE unset): start one child per GPU
+    running this same command line, with RANK / LOCAL_RANK / WORLD_SIZE and a
+    fresh 127.0.0.1 rendezvous, as torch.distributed.run would. Called before
+    anything touches the GPU in this process (children are started with
+    subprocess, never by replacing this process). Rank 0's stdout (the JSON
+    line) passes through. When one rank fails the others are given 60 s and
+    then killed by their exact PIDs. Returns the exit code: the first
+    non-zero child code, else 0."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    base = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [None] * n
+    t_fail = None
+    t0 = time.monotonic()
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        bad = [c for c in codes if c not in (None, 0)]
+        now = time.monotonic()
+        if bad and t_fail is None:
+            t_fail = now
+        late = (t_fail is not None and now - t_fail > 60) or \
+            (timeout_s is not None and now - t0 > timeout_s)
+        if late:
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    p.send_signal(signal.SIGKILL)
+                    codes[r] = p.wait()
+        time.sleep(0.05)
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"bench.py --gpus {n}: rank exit codes {codes}", file=sys.stderr, flush=True)
+        return bad[0] if bad[0] > 0 else 1
+    return 0
+
+
+def plumbing(world, rank):
+    """--plumbing (CPU test of the launch contract, no GPU): the ranks
+    rendezvous over gloo, pass the timed region's barrier and max-over-ranks
+    reduction, and rank 0 prints the world size the process group saw. No
+    combine runs, so the line has no value."""
+    import datetime
+    import torch
+    import torch.distributed as dist
+    if world == 1:                      # no launcher: a private rendezvous
+        import socket
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(sk.getsockname()[1]))
+    dist.init_process_group("gloo", rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
+    dist.barrier()
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"plumbing": True, "n_gpus": dist.get_world_size(),
+                          "world_size_env": world, "max_over_ranks": t.item(),
+                          "value": None}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     if "--collective-child" in sys.argv:
         collective_child()
         return
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU: spawned here when no launcher set WORLD_SIZE")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU test of the launch contract only (gloo, no GPU, no value)")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--count", type=int, default=WORKLOAD_COUNT)
@@ -1125,9 +1202,21 @@ def main():
                     help="run the collective phases even at N = 1 (under torchrun)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus < 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus}: need at least 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: one rank per GPU, spawned before any GPU call here
+        sys.exit(spawn_ranks(args.gpus))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: "
+                         "the launcher and the flag must agree")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plumbing:
+        plumbing(world, rank)
+        return
 
     import torch
     import xucg_amd
@@ -1139,6 +1228,10 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=600),
                                 device_id=torch.device(f"cuda:{local_rank}"))
+        # the ranks RCCL itself saw, not the environment's claim
+        if dist.get_world_size() != world:
+            raise SystemExit(f"bench.py: RCCL group has {dist.get_world_size()} ranks, "
+                             f"WORLD_SIZE={world}")
 
     def barrier():
         if dist is not None:
@@ -1262,7 +1355,7 @@ def main():
             "metric": load_baseline_metric(),
             "value": round(value, 3),
             "unit": "GiB/s",
-            "n_gpus": world,
+            "n_gpus": dist.get_world_size() if dist is not None else 1,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 5),
