@@ -368,11 +368,17 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return t.item() / iters
 
-    # every tensor exported to the peers (PeerBuffers) stays allocated until
-    # the phases end: a HIP IPC key is (pid, address, size), so a tensor freed
-    # and allocated again at the same address would give the peers a key
-    # that can resolve to the old memory (r03h)
+    # With torch's memory from the shim's shareable allocator (the default,
+    # collective_child) a key names the physical allocation, and a tensor may
+    # be freed once its mappings are released. On the hipIpc fallback a key
+    # names (pid, address, size): a tensor freed and allocated again at the
+    # same address could hand the peers the old memory (r03h),
+    # so there every exported tensor stays allocated until the phases end.
     exported = []
+
+    def keep(*ts):
+        if not SHAREABLE_PEER_MEMORY[0]:
+            exported.extend(ts)
     n4 = (1 << 30) // COLL_SCALE      # 4 GiB fp32 (config 4)
     shard = n4 // world
     x = torch.empty(n4, dtype=torch.float32, device=dev)
@@ -400,10 +406,10 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
     def oneshot():
         if world & (world - 1) or world > 16:
             return {"skipped": "one-shot needs a power-of-two group <= 16"}
-        exported.append(x)
+        keep(x)
         peers = G.PeerBuffers(ctx, x.data_ptr(), rank, world, dist)
         mine = torch.empty(shard, dtype=torch.float32, device=dev)
-        exported.append(mine)
+        keep(mine)
         try:
             def rs():
                 G.oneshot_reduce_scatter(ctx, peers, mine.data_ptr(), n4, "float32",
@@ -415,14 +421,14 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             t_rs = timed(rs, steps)
             # the same reduce-scatter with the multi-operand kernel uncapped
             # ("Occupancy cap": tuned on local HBM; here 7 of 8
-            # operands come over xGMI), then the table again
+            # operands come over xGMI), then capped again
             from xucg_amd import _lib as L
-            L.dev().ucg_builtin_dev_set_multi_waves(0)
+            L.dev().ucg_builtin_dev_set_multi_cap(0)
             try:
                 rs()
                 t_rs_uncapped = timed(rs, steps)
             finally:
-                L.dev().ucg_builtin_dev_set_multi_waves(-1)
+                L.dev().ucg_builtin_dev_set_multi_cap(-1)
             dist.reduce_scatter_tensor(rs_out, x)
             torch.cuda.synchronize()
             same = bool(torch.equal(mine.view(torch.int32), rs_out.view(torch.int32)))
@@ -460,7 +466,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             # place over xGMI (ucg_builtin_dev_gather_multi); parity: bit-exact
             # with RCCL's all-gather of the same shards
             ag_rccl = ag_out.clone()
-            exported.append(ag_out)
+            keep(ag_out)
             speers = G.PeerBuffers(ctx, mine.data_ptr(), rank, world, dist)
             try:
                 def ag1():
@@ -487,7 +493,7 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
             # shard is written into every peer's recv buffer
             slot = G.stage_slot_bytes(n4, 4, world)
             stage = torch.empty(world * slot // 4, dtype=torch.float32, device=dev)
-            exported.append(stage)
+            keep(stage)
             tpeers = G.PeerBuffers(ctx, stage.data_ptr(), rank, world, dist)
             try:
                 def ar1():
@@ -632,13 +638,13 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2):
                                           n5, 8)
 
         sbar = G.stream_barrier(dist, dev)
-        exported.extend((init, acc))
+        keep(init, acc)
         ipeers = G.PeerBuffers(ctx, init.data_ptr(), rank, world, dist)
         apeers = G.PeerBuffers(ctx, acc.data_ptr(), rank, world, dist)
 
         slot5 = G.stage_slot_bytes(n5, 8, world)
         stage5 = torch.empty(world * slot5 // 8, dtype=torch.float64, device=dev)
-        exported.append(stage5)
+        keep(stage5)
         tpeers = G.PeerBuffers(ctx, stage5.data_ptr(), rank, world, dist)
 
         def once_oneshot():
@@ -1072,9 +1078,59 @@ def torch_empty_cpu_like(t):
     return torch.empty(t.shape, dtype=t.dtype)
 
 
+# whether torch's device memory comes from the shim's shareable allocator in
+# this process (collective_child); a one-element list so phases can read it
+SHAREABLE_PEER_MEMORY = [False]
+
+
+def shareable_memory_probe(store, rank, world, local_rank):
+    """Before torch allocates anything: can every rank map every other rank's
+    shareable allocation (HIP VMM, fd keys from the exporter's key server)
+    and read what its owner wrote? The keys and verdicts go through `store`
+    (no device tensors). Returns (ok, detail); every rank gets the same ok."""
+    import numpy as np
+    import xucg_amd
+    ctx = xucg_amd.DevContext(device=local_rank)
+    buf, maps, err = None, [], ""
+    try:
+        buf = ctx.alloc(2 << 20, shareable=True)
+        buf.upload(np.full(512, rank + 1, np.int64))
+        store.set(f"vmm_key_{rank}", ctx.ipc_export(buf.ptr))
+        for p in range(world):
+            if p == rank:
+                continue
+            m = ctx.ipc_import(store.get(f"vmm_key_{p}"))
+            maps.append(m)
+            got = np.empty(512, np.int64)
+            from xucg_amd import _lib
+            _lib.check(_lib.dev().ucg_builtin_dev_memcpy(ctx.handle, got.ctypes.data, m,
+                                                         got.nbytes), "memcpy")
+            if not (got == p + 1).all():
+                raise RuntimeError(f"member {p}'s buffer read {got[:2].tolist()}")
+    except Exception as e:  # noqa: BLE001 - agreed on below
+        err = f"{type(e).__name__}: {e}"[:200]
+    store.set(f"vmm_ok_{rank}", err or "ok")
+    verdicts = [store.get(f"vmm_ok_{p}").decode() for p in range(world)]
+    for m in maps:
+        ctx.ipc_release(m)
+    store.add("vmm_done", 1)
+    while store.add("vmm_done", 0) < world:       # nobody frees while mapped
+        time.sleep(0.01)
+    if buf is not None:
+        buf.free()
+    ctx.close()
+    bad = [f"rank {p}: {v}" for p, v in enumerate(verdicts) if v != "ok"]
+    return not bad, ("; ".join(bad) if bad else "every rank mapped every peer's allocation")
+
+
 def collective_child():
     """--collective-child: one rank of the collective phases (see above).
-    XUCG_COLLECTIVE_BACKEND=gloo is the 1-GPU rehearsal (HostStagedDist)."""
+    XUCG_COLLECTIVE_BACKEND=gloo is the 1-GPU rehearsal (HostStagedDist).
+    torch's device memory comes from the shim's shareable allocator when
+    every rank can map every other rank's (shareable_memory_probe), so every
+    exported tensor is keyed by its physical allocation; otherwise the phases
+    run on torch's own allocator with hipIpc keys (XUCG_SHAREABLE_TORCH=n
+    forces that)."""
     import datetime
     import torch
     import torch.distributed as dist
@@ -1082,21 +1138,37 @@ def collective_child():
     world = int(os.environ["WORLD_SIZE"])
     rank = int(os.environ["RANK"])
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    timeout = datetime.timedelta(seconds=240)
+    store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                          int(os.environ["MASTER_PORT"]), world, rank == 0, timeout=timeout)
+    peer_memory = {"kind": "hipIpc (torch's caching allocator)"}
+    if os.environ.get("XUCG_SHAREABLE_TORCH", "y")[:1] not in ("n", "0"):
+        ok, detail = shareable_memory_probe(store, rank, world, local_rank)
+        if ok:
+            xucg_amd.use_shareable_torch_memory()
+            SHAREABLE_PEER_MEMORY[0] = True
+            peer_memory = {"kind": "shareable (HIP VMM, fd keys; torch memory from the shim)",
+                           "probe": detail}
+        else:
+            peer_memory["probe"] = detail
     torch.cuda.set_device(local_rank)
     # the engine's waits give up after this long instead of outliving the child
     os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "30")
     rehearsal = os.environ.get("XUCG_COLLECTIVE_BACKEND", "nccl") == "gloo"
+    pstore = dist.PrefixStore("pg", store)
     if rehearsal:
-        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=240))
+        dist.init_process_group("gloo", store=pstore, rank=rank, world_size=world,
+                                timeout=timeout)
         pg = HostStagedDist(dist)
     else:
         if COLL_SCALE != 1:
             raise SystemExit("XUCG_COLLECTIVE_SCALE is for the gloo rehearsal only")
-        dist.init_process_group("nccl", timeout=datetime.timedelta(seconds=240),
-                                device_id=torch.device(f"cuda:{local_rank}"))
+        dist.init_process_group("nccl", store=pstore, rank=rank, world_size=world,
+                                timeout=timeout, device_id=torch.device(f"cuda:{local_rank}"))
         pg = dist
     ctx = xucg_amd.DevContext.on_torch_stream(local_rank)
     res = collective_phases(ctx, pg, rank, world, local_rank)
+    res["peer_memory"] = peer_memory
     if rehearsal:
         res["rehearsal"] = {"backend": "gloo, CUDA tensors staged through the host",
                             "size_divisor": COLL_SCALE,

@@ -283,31 +283,52 @@ ucs_status_t ucg_builtin_dev_combine(ucg_builtin_dev_ctx_t *ctx,
 ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx);
 
 /* ---- peer mapping (xGMI) for the one-shot multi-operand combine ----------*/
-/* An exported device buffer: the HIP IPC handle of its allocation, the byte
- * offset of the pointer inside that allocation and the allocation's size
- * (import refuses a mapping that does not cover it). Opaque, fixed size.
- * Lifetime (HIP IPC contract): every importer releases its mapping before
- * the exporter frees the memory. The key is (pid, address, size), so memory
- * once exported should stay allocated while the process lives: an allocation
- * at a freed one's address and size would carry its key, and peers can be
- * handed the old memory. ucg_builtin_dev_free therefore parks an allocation
- * of ucg_builtin_dev_malloc that was exported, and the next malloc of that
- * device and size takes it back, key and all.
- * The memory must come from an allocation of its own (ucg_builtin_dev_malloc,
- * a hipMalloc of >= 2 MiB, a caching-allocator segment): the runtime may carve
- * small hipMalloc blocks out of a shared block, which it refuses to export. */
+/* The remote key of a device buffer (the uct_md_mkey_pack of the reference's
+ * zero-copy steps, builtin/ops/builtin_control.c:712-719): opaque, fixed size.
+ * A key names the physical allocation, never an address:
+ *  - memory of ucg_builtin_dev_malloc_shareable is mapped by a peer from the
+ *    allocation's file descriptor (HIP virtual memory, POSIX fd handle),
+ *    which the exporter's key server passes over a Unix socket;
+ *  - any other device memory (ucg_builtin_dev_malloc, a caller's hipMalloc of
+ *    an allocation of its own: not a small block the runtime carved out of a
+ *    shared one) goes by hipIpcGetMemHandle, handed out only while the
+ *    runtime's buffer id of the allocation at that address is the exported
+ *    one.
+ * Freeing an exported allocation retires its keys: a later import of one is
+ * refused with UCS_ERR_NO_RESOURCE ("stale key"). A peer that mapped a
+ * shareable allocation keeps its physical memory until it releases the
+ * mapping, so freeing under a live importer costs no fault and hands nobody
+ * else's data out. Exporting the same allocation again gives the same key.
+ * The exporting process must stay alive while peers import its keys. */
 #define UCG_BUILTIN_DEV_IPC_HANDLE_BYTES 96
 ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
                                         const void *dev_ptr, void *handle);
-/* Map a peer's exported buffer into this process (lazy peer access). */
+/* Map a peer's exported buffer into this process (once per key: a second
+ * import of the same key returns the same mapping, reference counted). */
 ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
                                         const void *handle, void **dev_ptr);
+/* Drop one import; the last one waits for this process's device work and
+ * unmaps. */
 ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx,
                                          void *dev_ptr);
 
 /* ---- memory helpers --------------------------------------------------------*/
+/* hipMalloc of whole 2 MiB granules */
 void        *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
+/* Device memory a peer maps by its physical allocation (HIP virtual memory,
+ * POSIX fd handle, 2 MiB granules at a 2 MiB aligned reservation): the
+ * engine's registered buffers. */
+void        *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
+/* 1 when ptr lies in a live allocation of ucg_builtin_dev_malloc_shareable */
+int          ucg_builtin_dev_is_shareable(const void *ptr);
+/* Frees either kind (waits for the device first, as hipFree does) and
+ * retires the allocation's keys; a pointer of neither is hipFree'd. */
 void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);
+/* torch.cuda.memory.CUDAPluggableAllocator entry points over
+ * ucg_builtin_dev_malloc_shareable / ucg_builtin_dev_free, so that every
+ * tensor of a process can be exported by its physical allocation. */
+void        *ucg_builtin_dev_torch_alloc(size_t bytes, int device, void *stream);
+void         ucg_builtin_dev_torch_free(void *ptr, size_t bytes, int device, void *stream);
 void        *ucg_builtin_dev_host_alloc(size_t bytes);      /* pinned */
 void         ucg_builtin_dev_host_free(void *ptr);
 /* Page-lock a caller's host buffer for DMA (hipHostRegister): the memory
@@ -321,15 +342,16 @@ ucs_status_t ucg_builtin_dev_host_register(ucg_builtin_dev_ctx_t *ctx, void *ptr
 ucs_status_t ucg_builtin_dev_host_unregister(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                     const void *src, size_t bytes); /* sync */
-/* Waves per CU of the multi-operand kernels on large grids, process-wide:
- * -1 = the measured table (the default), 0 = uncapped, W = at most W. Overrides
- * UCX_BUILTIN_DEV_MULTI_WAVES; for A/B runs inside one process (bench.py's
- * one-shot reduce-scatter over xGMI). */
-void         ucg_builtin_dev_set_multi_waves(int waves);
+/* Occupancy cap of the multi-operand kernels (at most 12 waves per CU, by
+ * their register allocation), process-wide: -1 = UCX_BUILTIN_DEV_MULTI_CAP
+ * (default on), 0 = off, 1 = on. Only fp32 and fp64 SUM are built both ways;
+ * every other pair always runs capped. For A/B runs inside one process
+ * (bench.py's one-shot reduce-scatter over xGMI). */
+void         ucg_builtin_dev_set_multi_cap(int capped);
 
 /* Diagnostics: what the runtime and this shim know about a device address
- * (range, attributes, live / parked / imported allocation) and the process's
- * recent memory events near it (malloc, free, park, IPC import and release),
+ * (range, attributes, live or imported allocation) and the process's recent
+ * memory events near it (malloc, free, export, IPC import and release),
  * as text into out[max]; returns the full length. For test harnesses that
  * find a buffer corrupted. */
 size_t       ucg_builtin_dev_debug_ptr(ucg_builtin_dev_ctx_t *ctx, const void *ptr,

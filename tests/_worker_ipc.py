@@ -49,8 +49,12 @@ def main():
         sz = np.dtype(st).itemsize
         inputs = [O.fill(dt, dname, 300 + r, n) for r in range(world)]
         shards = [oracle_shard(op, dt, inputs, r, world, O) for r in range(world)]
-        buf, out, full = ctx.alloc(n * sz), ctx.alloc(n * sz), ctx.alloc(n * sz)
-        stage = ctx.alloc(world * G.stage_slot_bytes(n, sz, world))
+        # XUCG_IPC_SHAREABLE=1: every exported buffer is shareable memory
+        # (mapped by its physical allocation), else hipMalloc (hipIpc keys)
+        sh = os.environ.get("XUCG_IPC_SHAREABLE") == "1"
+        buf, out = ctx.alloc(n * sz, shareable=sh), ctx.alloc(n * sz, shareable=sh)
+        full = ctx.alloc(n * sz, shareable=sh)
+        stage = ctx.alloc(world * G.stage_slot_bytes(n, sz, world), shareable=sh)
         buf.upload(inputs[rank])
         ctx.fill(dt, "special", 999, full, n)      # stale contents must not pass
         ctx.sync()

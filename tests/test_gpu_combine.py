@@ -410,28 +410,58 @@ def test_profile_hook_and_counters(dev_ctx):
 
 
 @pytest.mark.gpu
-def test_exported_allocations_are_parked_and_keep_their_key(dev_ctx):
-    """An allocation of the shim that was exported is never handed back to
-    the runtime: freeing it parks it, the next allocation of that size gets
-    the same memory and the same IPC key (a key is pid + address + size, so a
-    fresh allocation at that address would carry it for other memory). One
-    that was never exported is freed as before."""
+@pytest.mark.parametrize("shareable", [True, False])
+def test_ipc_keys_name_allocations_and_retire_on_free(dev_ctx, shareable):
+    """A key names the allocation, not the address (round 4):
+    exporting one allocation twice gives one key; importing it in the
+    exporting process maps the allocation itself; freeing the allocation
+    retires the key, so importing it afterwards is refused with
+    UCS_ERR_NO_RESOURCE ("stale key") even when a new allocation of the same
+    size sits at the same address - and that one has a key of its own."""
+    from xucg_amd import _lib
     nbytes = 6 << 20
-    a = dev_ctx.alloc(nbytes)
+    a = dev_ctx.alloc(nbytes, shareable=shareable)
+    assert bool(_lib.dev().ucg_builtin_dev_is_shareable(a.ptr)) == shareable
     a.upload(np.arange(16, dtype=np.int64))
-    key = dev_ctx.ipc_export(a)
+    key = dev_ctx.ipc_export(a.ptr + 4096)
+    assert dev_ctx.ipc_export(a.ptr + 4096) == key
+    p = dev_ctx.ipc_import(key)
+    assert p == a.ptr + 4096
+    dev_ctx.ipc_release(p)
     pa = a.ptr
     a.free()
-    b = dev_ctx.alloc(nbytes)
+    with pytest.raises(xucg_amd.UcsError) as e:
+        dev_ctx.ipc_import(key)
+    assert e.value.status == -2 and "stale key" in str(e.value)
+    b = dev_ctx.alloc(nbytes, shareable=shareable)
     try:
-        assert b.ptr == pa
-        assert dev_ctx.ipc_export(b) == key
-        assert (b.download(np.int64, 16) == np.arange(16)).all()   # the same memory
-        c = dev_ctx.alloc(nbytes)          # the parked one is taken: a new one
-        assert c.ptr != pa
-        c.free()
+        key_b = dev_ctx.ipc_export(b.ptr + 4096)
+        assert key_b != key, (hex(pa), hex(b.ptr))
+        with pytest.raises(xucg_amd.UcsError):
+            dev_ctx.ipc_import(key)                   # still stale
+        q = dev_ctx.ipc_import(key_b)
+        assert q == b.ptr + 4096
+        dev_ctx.ipc_release(q)
     finally:
         b.free()
+
+
+@pytest.mark.gpu
+def test_ipc_import_rejects_foreign_and_dead_keys(dev_ctx):
+    """A blob that is no key, and a key whose exporter's key server is gone,
+    fail loudly at import."""
+    with pytest.raises(xucg_amd.UcsError) as e:
+        dev_ctx.ipc_import(bytes(96))
+    assert e.value.status == -5
+    a = dev_ctx.alloc(2 << 20, shareable=True)
+    try:
+        key = bytearray(dev_ctx.ipc_export(a.ptr))
+        key[12:16] = (0x7ffffffe).to_bytes(4, "little")     # another (absent) pid
+        with pytest.raises(xucg_amd.UcsError) as e:
+            dev_ctx.ipc_import(bytes(key))
+        assert "key server is gone" in str(e.value)
+    finally:
+        a.free()
 
 
 @pytest.mark.gpu

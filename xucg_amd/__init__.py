@@ -12,6 +12,7 @@ from ._lib import (DTYPES, OPS, DISTS, UcsError, NativeLibraryMissing,  # noqa: 
                    UCS_OK, UCS_ERR_UNSUPPORTED, UCS_ERR_INVALID_PARAM,
                    UCS_ERR_NO_DEVICE, UCS_ERR_OUT_OF_RANGE)
 from .device import (DevContext, DevBuffer, HostBuffer, dtype_size,  # noqa: F401
-                     is_supported, device_count, NP_STORAGE)
+                     is_supported, device_count, NP_STORAGE,
+                     use_shareable_torch_memory)
 
 __version__ = "0.1.0"

@@ -86,6 +86,10 @@ DEV_API = {
     "ucg_builtin_dev_ipc_import": (_st, [_vp, _vp, ctypes.POINTER(_vp)]),
     "ucg_builtin_dev_ipc_release": (_st, [_vp, _vp]),
     "ucg_builtin_dev_malloc": (_vp, [_vp, _sz]),
+    "ucg_builtin_dev_malloc_shareable": (_vp, [_vp, _sz]),
+    "ucg_builtin_dev_is_shareable": (_int, [_vp]),
+    "ucg_builtin_dev_torch_alloc": (_vp, [_sz, _int, _vp]),
+    "ucg_builtin_dev_torch_free": (None, [_vp, _sz, _int, _vp]),
     "ucg_builtin_dev_free": (None, [_vp, _vp]),
     "ucg_builtin_dev_host_alloc": (_vp, [_sz]),
     "ucg_builtin_dev_host_free": (None, [_vp]),
@@ -93,7 +97,7 @@ DEV_API = {
     "ucg_builtin_dev_host_unregister": (_int, [_vp, _vp]),
     "ucg_builtin_dev_memcpy": (_st, [_vp, _vp, _vp, _sz]),
     "ucg_builtin_dev_debug_ptr": (_sz, [_vp, _vp, ctypes.c_char_p, _sz]),
-    "ucg_builtin_dev_set_multi_waves": (None, [_int]),
+    "ucg_builtin_dev_set_multi_cap": (None, [_int]),
     "ucg_builtin_dev_fill": (_st, [_vp, _int, _int, _u64, _vp, _sz]),
     "ucg_builtin_dev_profile_reduce": (_st, [_vp, _int, _int, _vp, _vp, _sz, _u,
                                              ctypes.POINTER(ctypes.c_double)]),

@@ -489,7 +489,8 @@ void *ucg_builtin_combine_dev_alloc(ucg_builtin_combine_t *cmb, size_t bytes)
         return NULL;
     }
     pthread_mutex_lock(&cmb->lock);
-    p = ucg_builtin_dev_malloc(cmb->dev, bytes);
+    /* exported to the peers: mapped by its physical allocation */
+    p = ucg_builtin_dev_malloc_shareable(cmb->dev, bytes);
     pthread_mutex_unlock(&cmb->lock);
     return p;
 }

@@ -269,10 +269,10 @@ static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
 }
 
 /* Group destroy is collective but not synchronised: a peer may still map this
- * member's pool buffers when they are given back here. HIP leaves a free
- * under a live importer undefined; the device shim parks exported memory
- * instead of freeing it (ucg_builtin_dev_free), so the peer still maps live
- * memory, and a later group of this process reuses it under the same key.
+ * member's pool buffers when they are given back here. Pool buffers are
+ * shareable allocations (ucg_builtin_dev_malloc_shareable): a peer's mapping
+ * holds the physical memory until the peer releases it, and the free retires
+ * the buffers' keys, so a later group can never map them by an old key.
  * Shared-memory segments stay alive for the peers that map them. */
 UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
 {

@@ -24,6 +24,7 @@
 
 #include "ucg_builtin_dev.h"
 #include "dev_launch.h"
+#include "dev_internal.h"
 
 using namespace ucgdev;
 
@@ -32,13 +33,13 @@ using namespace ucgdev;
 /* ------------------------------------------------------------------------ */
 static thread_local std::string g_last_error;
 
-static ucs_status_t set_error(ucs_status_t st, const char *what, const char *why)
+ucs_status_t set_error(ucs_status_t st, const char *what, const char *why)
 {
     g_last_error = std::string(what) + ": " + why;
     return st;
 }
 
-static ucs_status_t hip_status(hipError_t e, const char *what)
+ucs_status_t hip_status(hipError_t e, const char *what)
 {
     if (e == hipSuccess) {
         return UCS_OK;
@@ -62,43 +63,35 @@ static ucs_status_t hip_status(hipError_t e, const char *what)
     return set_error(st, what, hipGetErrorString(e));
 }
 
-#define HIP_TRY(_call)                                                        \
-    do {                                                                      \
-        hipError_t _e = (_call);                                              \
-        if (_e != hipSuccess) {                                               \
-            return hip_status(_e, #_call);                                    \
-        }                                                                     \
-    } while (0)
-
 /* ------------------------------------------------------------------------ */
 /* launch configuration (builtin-private knobs, UCX_BUILTIN_DEV_*)          */
 /* ------------------------------------------------------------------------ */
 struct LaunchCfg {
-    int max_blocks;  /* grid cap for the streaming kernels */
-    int variant;     /* fp32-SUM tuning variant (0 = product default) */
-    int multi_waves; /* waves per CU of the multi-operand kernels: -1 table */
+    int  max_blocks;  /* grid cap of the looping (element-wise) kernels */
+    bool multi_cap;   /* occupancy cap of the multi-operand kernels */
 };
 
-static LaunchCfg g_cfg = {-1, -1, -1};
+static LaunchCfg g_cfg = {2048, true};
 
 static const LaunchCfg &launch_cfg()
 {
     static std::once_flag once;
     std::call_once(once, [] {
         const char *b = getenv("UCX_BUILTIN_DEV_MAX_BLOCKS");
-        const char *v = getenv("UCX_BUILTIN_DEV_VARIANT");
         g_cfg.max_blocks = b ? atoi(b) : 2048;
         if (g_cfg.max_blocks < 1) {
             g_cfg.max_blocks = 2048;
         }
-        g_cfg.variant = v ? atoi(v) : 0; /* 0: the product geometry */
-        /* UCX_BUILTIN_DEV_MULTI_WAVES: "auto" (unset) = the measured table
-         * below, 0 = no cap, W = at most W waves per CU for every count */
-        const char *w = getenv("UCX_BUILTIN_DEV_MULTI_WAVES");
-        g_cfg.multi_waves = (w && strcmp(w, "auto") != 0) ? atoi(w) : -1;
+        /* UCX_BUILTIN_DEV_MULTI_CAP=n: the multi-operand kernels uncapped */
+        const char *c = getenv("UCX_BUILTIN_DEV_MULTI_CAP");
+        g_cfg.multi_cap = !(c && (c[0] == 'n' || c[0] == '0'));
     });
     return g_cfg;
 }
+
+/* ucg_builtin_dev_set_multi_cap: a process-wide override of
+ * UCX_BUILTIN_DEV_MULTI_CAP (-1 = none), for A/B runs in one process */
+static std::atomic<int> g_multi_cap_override{-1};
 
 namespace ucgdev {
 int launch_max_blocks()
@@ -106,59 +99,16 @@ int launch_max_blocks()
     return launch_cfg().max_blocks;
 }
 
-int launch_variant()
+bool multi_capped()
 {
-    return launch_cfg().variant;
-}
-
-/* Occupancy of the multi-operand kernels (k_reduce_multi, k_reduce_tree; their
- * realigning forms run uncapped, which measured better). With every CU full
- * of one-wave workgroups, each holding one 16-B load of every operand, HBM
- * serves (operands + 1) streams from ~32 waves per CU and loses 5-10 points
- * to it; capping the workgroups per CU gains them back (tools/tune_occ,
- * profiles/r03/r03s2occ: N = 8 fp32 SUM at 64 MiB per operand 77.2-78.8 % of
- * 8 TB/s uncapped, 84.7-86.2 % at 8 waves per CU on three boxes). The cap is
- * dynamic LDS the kernels never touch: at most W workgroups fit a CU's
- * 160 KiB. Best cap per number of distinct operands, measured;
- * two operands (the 2-operand combine's shape) run uncapped. */
-static int multi_waves_for(unsigned operands)
-{
-    if (operands <= 2)  return 0;
-    if (operands == 3)  return 20;
-    if (operands <= 7)  return 12;
-    if (operands == 8)  return 8;
-    if (operands <= 12) return 10;
-    return 8;
-}
-
-/* ucg_builtin_dev_set_multi_waves: a process-wide override of the table and
- * of UCX_BUILTIN_DEV_MULTI_WAVES (INT_MIN = none), for A/B runs in one process */
-static std::atomic<int> g_multi_override{INT_MIN};
-
-size_t multi_lds_bytes(unsigned operands, size_t grid)
-{
-    const int ov = g_multi_override.load(std::memory_order_relaxed);
-    int w = ov != INT_MIN ? ov : launch_cfg().multi_waves;
-    if (w < 0) {
-        w = multi_waves_for(operands);
-    }
-    /* a grid that fits the chip under the cap runs uncapped: nothing to limit
-     * (the engine's small messages, latency-bound launches) */
-    constexpr size_t kCus = 256;               /* MI355X */
-    if (w <= 0 || grid <= kCus * (size_t)w) {
-        return 0;
-    }
-    if (w < 4) {
-        w = 4;   /* keeps the request within one workgroup's LDS limit */
-    }
-    constexpr size_t kLdsPerCu = 160 * 1024;   /* gfx950 */
-    return kLdsPerCu / (size_t)w / 512 * 512;
+    const int ov = g_multi_cap_override.load(std::memory_order_relaxed);
+    return ov >= 0 ? ov != 0 : launch_cfg().multi_cap;
 }
 }  // namespace ucgdev
 
-void ucg_builtin_dev_set_multi_waves(int waves)
+void ucg_builtin_dev_set_multi_cap(int capped)
 {
-    ucgdev::g_multi_override.store(waves < -1 ? -1 : waves, std::memory_order_relaxed);
+    g_multi_cap_override.store(capped < 0 ? -1 : (capped != 0), std::memory_order_relaxed);
 }
 
 /* dispatch tables, assembled from the per-dtype translation units */
@@ -255,6 +205,11 @@ static ucs_status_t set_device(ucg_builtin_dev_ctx_t *ctx)
 {
     HIP_TRY(hipSetDevice(ctx->device));
     return UCS_OK;
+}
+
+int dev_ctx_device(const ucg_builtin_dev_ctx_t *ctx)
+{
+    return ctx->device;
 }
 
 static ucs_status_t ring_init(ucg_builtin_dev_ctx_t *ctx)
@@ -658,7 +613,7 @@ static ucs_status_t reduce_on(ucg_builtin_dev_ctx_t *ctx, hipStream_t st,
         return set_error(UCS_ERR_INVALID_PARAM, "reduce",
                          "src and dst partially overlap");
     }
-    HIP_TRY(tables().reduce[dt][op](dst, src, count, st, launch_cfg().variant));
+    HIP_TRY(tables().reduce[dt][op](dst, src, count, st));
     ctx->counters[0]++;
     ctx->counters[1] += 3 * bytes;
     return UCS_OK;
@@ -778,7 +733,7 @@ __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbyt
         u32x4 hi;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
-            hi[k] = from_next_lane<0>(lo[k]);
+            hi[k] = from_next_lane(lo[k]);
         }
         if (last_lane) {
             hi = ex;
@@ -819,24 +774,6 @@ k_gather_multi(char *dst, SrcList srcs, unsigned nsrc, size_t row_stride,
     copy_row(dst + (size_t)r * row_stride, src, nbytes, wg);
 }
 
-/* the byte loop the realigning row copy replaced (A/B variant 4 only):
- * grid-stride, workgroups dealt round-robin over the sources as above */
-static __global__ void __launch_bounds__(kBlock)
-k_gather_multi_bytes(char *dst, SrcList srcs, unsigned nsrc, size_t shard_bytes)
-{
-    const unsigned r   = blockIdx.x % nsrc;
-    const size_t wg    = blockIdx.x / nsrc;
-    const size_t nwg   = gridDim.x / nsrc;
-    const char *src    = static_cast<const char*>(srcs.p[r]);
-    if (src == nullptr) {
-        return;
-    }
-    char *out          = dst + (size_t)r * shard_bytes;
-    for (size_t i = wg * kBlock + threadIdx.x; i < shard_bytes; i += nwg * kBlock) {
-        out[i] = src[i];
-    }
-}
-
 ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
                                           const void *const *srcs, unsigned nsrc,
                                           size_t shard_bytes)
@@ -851,29 +788,17 @@ ucs_status_t ucg_builtin_dev_gather_multi(ucg_builtin_dev_ctx_t *ctx, void *dst,
     }
     SrcList list;
     /* any row layout takes the vector kernel (copy_row: byte heads and
-     * tails, out-of-phase sources realigned in registers); the byte loop is
-     * kept as A/B variant 4 for rows out of phase */
-    bool aligned = true;
+     * tails, out-of-phase sources realigned in registers) */
     unsigned live = 0;
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         list.p[i] = (i < nsrc) ? srcs[i] : nullptr;
-        if (i < nsrc && srcs[i] != nullptr) {
-            live++;
-            aligned = aligned &&
-                      (((uintptr_t)srcs[i] ^ ((uintptr_t)dst + (uintptr_t)i * shard_bytes)) &
-                       15) == 0;
-        }
+        live += (i < nsrc && srcs[i] != nullptr);
     }
-    aligned = aligned || launch_variant() != 4;
     if (live == 0) {
         return set_error(UCS_ERR_INVALID_PARAM, "gather_multi", "every source is NULL");
     }
     char *d = static_cast<char*>(dst);
-    if (!aligned) {
-        const unsigned grid = grid_for(shard_bytes, kBlock, 1024) * nsrc;
-        hipLaunchKernelGGL(k_gather_multi_bytes, dim3(grid), dim3(kBlock), 0,
-                           ctx->stream, d, list, nsrc, shard_bytes);
-    } else {
+    {
         /* a dispatch counts work-items in 32 bits: at most 2^31 in total,
          * i.e. 2^31 / nsrc vectors of every source per dispatch */
         const size_t nvec    = shard_bytes / 16;
@@ -918,19 +843,6 @@ k_copy_multi(PairList pl, unsigned n, size_t nbytes)
              blockIdx.x / n);
 }
 
-static __global__ void __launch_bounds__(kBlock)
-k_copy_multi_bytes(PairList pl, unsigned n, size_t nbytes)
-{
-    const unsigned r = blockIdx.x % n;
-    const size_t wg  = blockIdx.x / n;
-    const size_t nwg = gridDim.x / n;
-    const char *src  = static_cast<const char*>(pl.s[r]);
-    char *out        = static_cast<char*>(pl.d[r]);
-    for (size_t i = wg * kBlock + threadIdx.x; i < nbytes; i += nwg * kBlock) {
-        out[i] = src[i];
-    }
-}
-
 ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
                                         void *const *dsts, const void *const *srcs,
                                         unsigned n, size_t nbytes)
@@ -944,23 +856,14 @@ ucs_status_t ucg_builtin_dev_copy_multi(ucg_builtin_dev_ctx_t *ctx,
         return UCS_OK;
     }
     PairList pl;
-    bool aligned = true;   /* every pair in one 16-B phase */
     for (unsigned i = 0; i < (unsigned)kMaxMulti; i++) {
         pl.d[i] = (i < n) ? dsts[i] : nullptr;
         pl.s[i] = (i < n) ? srcs[i] : nullptr;
-        if (i < n) {
-            if (dsts[i] == nullptr || srcs[i] == nullptr) {
-                return set_error(UCS_ERR_INVALID_PARAM, "copy_multi", "NULL pointer");
-            }
-            aligned = aligned && (((uintptr_t)dsts[i] ^ (uintptr_t)srcs[i]) & 15) == 0;
+        if (i < n && (dsts[i] == nullptr || srcs[i] == nullptr)) {
+            return set_error(UCS_ERR_INVALID_PARAM, "copy_multi", "NULL pointer");
         }
     }
-    aligned = aligned || launch_variant() != 4;   /* byte loop: A/B only */
-    if (!aligned) {
-        const unsigned grid = grid_for(nbytes, kBlock, 1024) * n;
-        hipLaunchKernelGGL(k_copy_multi_bytes, dim3(grid), dim3(kBlock), 0, ctx->stream,
-                           pl, n, nbytes);
-    } else {
+    {
         /* at most 2^31 work-items per dispatch: 2^31 / n vectors of every pair */
         const size_t nvec    = nbytes / 16;
         const size_t per_max = (((size_t)1 << 31) / n) / kReduceBlock * kReduceBlock;
@@ -1315,310 +1218,6 @@ ucs_status_t ucg_builtin_dev_stage_end(ucg_builtin_dev_ctx_t *ctx)
     ctx->acc_in_place = false;
     ctx->host_pinned  = false;
     return UCS_OK;
-}
-
-/* ---- peer mapping ------------------------------------------------------- */
-/* ---- exported allocations are never returned to the runtime -------------
- * A HIP IPC handle is the exporter's pid, the allocation's address and its
- * size. An allocation freed and made again at the same address and size
- * carries the old one's key, and a peer can then be handed the old mapping -
- * stale or since reused memory: the 8-rank rehearsal of bench.py's C4 -> C5
- * phases read another member's data and zeros through fresh keys, and once
- * faulted (r03f/r03h). So an allocation of this shim that was
- * ever exported is parked by ucg_builtin_dev_free instead of freed, and a
- * later ucg_builtin_dev_malloc of the same device and size takes it back: a
- * key names the same memory for the life of the process. */
-namespace {
-struct own_alloc {
-    int    device;
-    size_t bytes;
-    bool   exported;
-    bool   parked;
-};
-std::mutex g_alloc_mu;
-std::unordered_map<void*, own_alloc> g_allocs;                  /* live and parked */
-std::multimap<std::pair<int, size_t>, void*> g_parked;          /* (device, bytes) */
-std::unordered_multimap<void*, void*> g_imports;   /* imported pointer -> mapping base */
-
-/* The last memory events of the process (allocations, frees, parks, IPC
- * imports and releases), for ucg_builtin_dev_debug_ptr: a buffer found to read
- * as zeros is matched against what happened to its address range. */
-struct mem_event {
-    char     kind;      /* M malloc, R reuse of a parked one, F free, P park,
-                           I import, C release (close) */
-    void    *ptr;
-    void    *base;
-    size_t   bytes;
-    uint64_t ns;        /* CLOCK_MONOTONIC */
-    int      rc;        /* the runtime's return code */
-};
-constexpr size_t kMemEvents = 1024;
-mem_event g_events[kMemEvents];
-uint64_t  g_nevents;                                 /* under g_alloc_mu */
-
-uint64_t now_ns()
-{
-    timespec ts;
-    clock_gettime(CLOCK_MONOTONIC, &ts);
-    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
-}
-
-/* caller holds g_alloc_mu */
-void note_event(char kind, void *ptr, void *base, size_t bytes, int rc)
-{
-    g_events[g_nevents++ % kMemEvents] = mem_event{kind, ptr, base, bytes, now_ns(), rc};
-}
-}
-
-struct ipc_blob {
-    hipIpcMemHandle_t handle;
-    uint64_t          offset;   /* of the exported pointer in its allocation */
-    uint64_t          size;     /* of the allocation, checked on import */
-    uint64_t          magic;
-};
-static_assert(sizeof(ipc_blob) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES,
-              "IPC blob does not fit the ABI size");
-static const uint64_t kIpcMagic = 0x5543475f49504331ull; /* "UCG_IPC1" */
-
-ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
-                                        const void *dev_ptr, void *handle)
-{
-    if (ctx == nullptr || dev_ptr == nullptr || handle == nullptr) {
-        return set_error(UCS_ERR_INVALID_PARAM, "ipc_export", "bad arguments");
-    }
-    ucs_status_t st = set_device(ctx);
-    if (st != UCS_OK) {
-        return st;
-    }
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr));
-    ipc_blob b;
-    memset(&b, 0, sizeof(b));
-    HIP_TRY(hipIpcGetMemHandle(&b.handle, (void*)base));
-    {
-        /* this shim's allocation: never freed from now on (see above) */
-        std::lock_guard<std::mutex> g(g_alloc_mu);
-        auto it = g_allocs.find((void*)base);
-        if (it != g_allocs.end()) {
-            it->second.exported = true;
-        }
-        note_event('X', (void*)dev_ptr, (void*)base, size, 0);
-    }
-    b.offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
-    b.size   = (uint64_t)size;
-    b.magic  = kIpcMagic;
-    memset(handle, 0, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
-    memcpy(handle, &b, sizeof(b));
-    return UCS_OK;
-}
-
-ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
-                                        const void *handle, void **dev_ptr)
-{
-    if (ctx == nullptr || handle == nullptr || dev_ptr == nullptr) {
-        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import", "bad arguments");
-    }
-    ipc_blob b;
-    memcpy(&b, handle, sizeof(b));
-    if (b.magic != kIpcMagic) {
-        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import", "not an exported handle");
-    }
-    ucs_status_t st = set_device(ctx);
-    if (st != UCS_OK) {
-        return st;
-    }
-    void *base = nullptr;
-    HIP_TRY(hipIpcOpenMemHandle(&base, b.handle, hipIpcMemLazyEnablePeerAccess));
-    /* the mapping must span the exporter's whole allocation: a short or
-     * stale mapping is refused here instead of faulting a kernel later.
-     * Where the runtime cannot answer the range query for an imported
-     * pointer, the mapping is taken as it is. */
-    hipDeviceptr_t mbase = nullptr;
-    size_t msize = 0;
-    const hipError_t e = hipMemGetAddressRange(&mbase, &msize, (hipDeviceptr_t)base);
-    if (b.offset >= b.size ||
-        (e == hipSuccess && (mbase != (hipDeviceptr_t)base || msize < b.size))) {
-        (void)hipIpcCloseMemHandle(base);
-        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import",
-                         "mapped range does not cover the exported allocation");
-    }
-    (void)hipGetLastError();
-    *dev_ptr = (char*)base + b.offset;
-    std::lock_guard<std::mutex> g(g_alloc_mu);
-    g_imports.emplace(*dev_ptr, base);
-    note_event('I', *dev_ptr, base, (size_t)b.size, 0);
-    return UCS_OK;
-}
-
-ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx, void *dev_ptr)
-{
-    if (ctx == nullptr || dev_ptr == nullptr) {
-        return set_error(UCS_ERR_INVALID_PARAM, "ipc_release", "bad arguments");
-    }
-    void *base = nullptr;
-    {
-        /* the mapping's base as import returned it (no range query on an
-         * imported pointer) */
-        std::lock_guard<std::mutex> g(g_alloc_mu);
-        auto it = g_imports.find(dev_ptr);
-        if (it != g_imports.end()) {
-            base = it->second;
-            g_imports.erase(it);
-        }
-    }
-    if (base == nullptr) {
-        hipDeviceptr_t b = nullptr;
-        size_t size = 0;
-        HIP_TRY(hipMemGetAddressRange(&b, &size, (hipDeviceptr_t)dev_ptr));
-        base = (void*)b;
-    }
-    const hipError_t e = hipIpcCloseMemHandle(base);
-    {
-        std::lock_guard<std::mutex> g(g_alloc_mu);
-        note_event('C', dev_ptr, base, 0, (int)e);
-    }
-    HIP_TRY(e);
-    return UCS_OK;
-}
-
-/* ---- memory helpers ------------------------------------------------------ */
-void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
-{
-    void *p = nullptr;
-    if (ctx) {
-        (void)hipSetDevice(ctx->device);
-    }
-    int device = 0;
-    (void)hipGetDevice(&device);
-    /* whole 2 MiB granules: a small hipMalloc may be carved out of a block
-     * the runtime shares with other allocations, and such memory cannot be
-     * exported through hipIpcGetMemHandle (ucg_builtin_dev_ipc_export) */
-    const size_t gran = (size_t)2 << 20;
-    bytes = bytes ? (bytes + gran - 1) / gran * gran : gran;
-    {
-        std::lock_guard<std::mutex> g(g_alloc_mu);
-        auto it = g_parked.find({device, bytes});
-        if (it != g_parked.end()) {
-            p = it->second;
-            g_parked.erase(it);
-            g_allocs[p].parked = false;
-            note_event('R', p, p, bytes, 0);
-            return p;
-        }
-    }
-    /* A/B knob: UCX_BUILTIN_DEV_MALLOC=contiguous asks the runtime for
-     * physically contiguous memory ("Slow phases") */
-    const char *kind = getenv("UCX_BUILTIN_DEV_MALLOC");
-    const bool contiguous = kind && kind[0] == 'c';
-    hipError_t e = contiguous ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous)
-                              : hipMalloc(&p, bytes);
-    if (e != hipSuccess) {
-        hip_status(e, contiguous ? "hipExtMallocWithFlags(contiguous)" : "hipMalloc");
-        return nullptr;
-    }
-    std::lock_guard<std::mutex> g(g_alloc_mu);
-    g_allocs[p] = own_alloc{device, bytes, false, false};
-    note_event('M', p, p, bytes, 0);
-    return p;
-}
-
-void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
-{
-    (void)ctx;
-    if (ptr == nullptr) {
-        return;
-    }
-    {
-        std::lock_guard<std::mutex> g(g_alloc_mu);
-        auto it = g_allocs.find(ptr);
-        /* UCX_BUILTIN_DEV_PARK=n: free exported memory too (an A/B knob for
-         * the stale-key tests, never for production) */
-        static const bool park = [] {
-            const char *e = getenv("UCX_BUILTIN_DEV_PARK");
-            return !(e && (e[0] == 'n' || e[0] == '0'));
-        }();
-        if (it != g_allocs.end()) {
-            if (it->second.exported && park) {   /* its key stays this memory's */
-                if (!it->second.parked) {   /* (a second free is ignored) */
-                    it->second.parked = true;
-                    g_parked.emplace(std::make_pair(it->second.device, it->second.bytes), ptr);
-                }
-                note_event('P', ptr, ptr, it->second.bytes, 0);
-                return;
-            }
-            g_allocs.erase(it);
-        }
-    }
-    const hipError_t e = hipFree(ptr);
-    std::lock_guard<std::mutex> g(g_alloc_mu);
-    note_event('F', ptr, ptr, 0, (int)e);
-}
-
-/* Diagnostics for a buffer found corrupted (tests/_worker_topo.py): what the
- * runtime says about the address now, whether it lies in a live, parked or
- * imported range of this shim, and the recorded memory events whose range
- * comes within 4 MiB of it, oldest first. */
-size_t ucg_builtin_dev_debug_ptr(ucg_builtin_dev_ctx_t *ctx, const void *ptr, char *out,
-                                 size_t max)
-{
-    std::string t;
-    char line[256];
-    if (ctx) {
-        (void)hipSetDevice(ctx->device);
-    }
-    hipDeviceptr_t base = nullptr;
-    size_t size = 0;
-    const hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
-    snprintf(line, sizeof(line), "address %p: runtime range %s base %p size %zu\n", ptr,
-             e == hipSuccess ? "ok" : hipGetErrorString(e), (void*)base, size);
-    t += line;
-    (void)hipGetLastError();
-    hipPointerAttribute_t at;
-    memset(&at, 0, sizeof(at));
-    const hipError_t ea = hipPointerGetAttributes(&at, ptr);
-    snprintf(line, sizeof(line), "attributes %s: type %d device %d devptr %p\n",
-             ea == hipSuccess ? "ok" : hipGetErrorString(ea), (int)at.type, at.device,
-             at.devicePointer);
-    t += line;
-    (void)hipGetLastError();
-    const uintptr_t a = (uintptr_t)ptr, win = (uintptr_t)4 << 20;
-    std::lock_guard<std::mutex> g(g_alloc_mu);
-    for (const auto &kv : g_allocs) {
-        const uintptr_t p = (uintptr_t)kv.first;
-        if (a >= p && a < p + kv.second.bytes) {
-            snprintf(line, sizeof(line), "own allocation %p + %zu exported %d parked %d\n",
-                     kv.first, kv.second.bytes, (int)kv.second.exported,
-                     (int)kv.second.parked);
-            t += line;
-        }
-    }
-    for (const auto &kv : g_imports) {
-        const uintptr_t p = (uintptr_t)kv.second;
-        if (a >= p && a < p + win) {
-            snprintf(line, sizeof(line), "import mapping base %p (pointer %p)\n", kv.second,
-                     kv.first);
-            t += line;
-        }
-    }
-    const uint64_t first = g_nevents > kMemEvents ? g_nevents - kMemEvents : 0;
-    const uint64_t now = now_ns();
-    for (uint64_t i = first; i < g_nevents; i++) {
-        const mem_event &ev = g_events[i % kMemEvents];
-        const uintptr_t lo = (uintptr_t)(ev.base ? ev.base : ev.ptr);
-        if (lo + win > a && lo < a + win) {
-            snprintf(line, sizeof(line), "event #%llu %c ptr %p base %p bytes %zu rc %d, %.3f ms ago\n",
-                     (unsigned long long)i, ev.kind, ev.ptr, ev.base, ev.bytes, ev.rc,
-                     (double)(now - ev.ns) * 1e-6);
-            t += line;
-        }
-    }
-    if (out && max) {
-        const size_t n = t.size() < max - 1 ? t.size() : max - 1;
-        memcpy(out, t.data(), n);
-        out[n] = '\0';
-    }
-    return t.size();
 }
 
 void *ucg_builtin_dev_host_alloc(size_t bytes)

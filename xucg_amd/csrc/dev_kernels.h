@@ -37,6 +37,17 @@ constexpr int kMultiU      = 1;       /* same for k_reduce_multi */
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+/* Occupancy cap of the multi-operand kernels. With every CU full of one-wave
+ * workgroups, each holding one 16-B load of every operand, HBM serves
+ * (operands + 1) streams from up to 32 waves per CU and loses 3-5 points to
+ * it; at most 12 waves per CU gains them back (tools/tune_cap,
+ * profiles/r04/r04b: fp32 SUM, 64 MiB per operand, N = 4 / 8 / 16 at
+ * 76.8 / 78.7 / 75.2 % of 8 TB/s uncapped, 80.2 / 81.6 / 76.8 % capped). The
+ * cap is the kernel's register allocation: a clobbered v167 makes it hold 168
+ * VGPRs, so floor(512 / 168) = 3 waves fit a SIMD, 12 a CU. No LDS is
+ * allocated (round 3's cap was unused dynamic LDS: ADVICE r03). */
+#define UCG_MULTI_CAP_CLOBBER() asm volatile("" ::: "v167")
+
 template <int NT>
 __device__ __forceinline__ u32x4 ld16(const u32x4 *p)
 {
@@ -163,18 +174,13 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
  * past its ends.
  */
 /* lane L gets lane L+1's value (lane 63: undefined, overwritten by the
- * caller). DPP=1: one v_mov_dpp wave_shl:1 (GFX9 whole-wave DPP, kept on
- * CDNA); DPP=0: ds_bpermute through the LDS crossbar. */
-template <int DPP>
+ * caller), through ds_bpermute (the LDS crossbar; no LDS allocated) */
 __device__ __forceinline__ uint32_t from_next_lane(uint32_t x)
 {
-    if (DPP) {
-        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, false);
-    }
     return __shfl_down(x, 1, 64);
 }
 
-template <typename T, int OP, int Q, int U = 1, int DPP = 0>
+template <typename T, int OP, int Q>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
                unsigned rb)
@@ -197,127 +203,22 @@ k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
     const char *sp  = reinterpret_cast<const char*>(src + head);
     const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
     u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
-    /* the wave's tile: U rows of 64 vectors; lane L holds column L */
-    const size_t base    = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * (BS * U) +
+    /* the wave's tile: 64 vectors; lane L holds column L */
+    const size_t i       = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * BS +
                            threadIdx.x;
     const bool last_lane = threadIdx.x == BS - 1;
-    u32x4 lo[U], b[U], ex;
     /* every load in flight before the first wait; lanes past the end load
      * the last vector again (unmasked loads keep the compiler from
      * serialising them) and store nothing */
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const size_t i = base + (size_t)u * BS;
-        b[u]  = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
-        lo[u] = ld16<1>(a4 + (i < nvec ? i : nvec));
-    }
-    {
-        const size_t i = base + (size_t)(U - 1) * BS + 1;
-        ex = ld16<1>(a4 + (last_lane && i <= nvec ? i : nvec));
-    }
-    __builtin_amdgcn_sched_barrier(0);  /* keep the shuffles behind all loads */
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const size_t i = base + (size_t)u * BS;
-        /* A[i + 1]: the next lane's load; for lane 63 the first lane's load
-         * of the next row, or its own extra load after the last row */
-        u32x4 hi;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            hi[k] = from_next_lane<DPP>(lo[u][k]);
-        }
-        if (last_lane) {
-            if (u + 1 < U) {
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    hi[k] = __builtin_amdgcn_readlane(lo[u + 1 < U ? u + 1 : u][k], 0);
-                }
-            } else {
-                hi = ex;
-            }
-        }
-        if (i < nvec) {
-            const uint32_t w[8] = {lo[u][0], lo[u][1], lo[u][2], lo[u][3],
-                                   hi[0], hi[1], hi[2], hi[3]};
-            u32x4 sv;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
-            }
-            st16<1>(d4 + i, vapply<T, OP>(sv, b[u]));
-        }
-    }
-}
-
-/* A/B variant of k_reduce_shift without the cross-lane step: every lane
- * loads both aligned vectors A[i] and A[i+1] itself (the second load mostly
- * hits lines the first load of the neighbouring lane brought into L2), so a
- * lane's store waits only for its own loads. */
-template <typename T, int OP, int Q>
-__global__ void __launch_bounds__(kReduceBlock)
-k_reduce_shift2(T *dst, const T *src, size_t head, size_t nvec, size_t tail, unsigned rb)
-{
-    constexpr int V   = 16 / sizeof(T);
-    const size_t gtid = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
-    if (gtid < head) {
-        dst[gtid] = Comb<T, OP>::apply(src[gtid], dst[gtid]);
-    }
-    if (gtid < tail) {
-        const size_t j = head + nvec * V + gtid;
-        dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
-    }
-    const size_t i = gtid;
-    if (i < nvec) {
-        const char *sp  = reinterpret_cast<const char*>(src + head);
-        const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
-        u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
-        const u32x4 b  = ld16<1>(d4 + i);
-        const u32x4 lo = ld16<1>(a4 + i);
-        const u32x4 hi = ld16<1>(a4 + i + 1);
-        const uint32_t w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        u32x4 sv;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
-        }
-        st16<1>(d4 + i, vapply<T, OP>(sv, b));
-    }
-}
-
-/* A/B variant of k_reduce_shift (U = 1) with other chunk sizes C of the
- * XCD-aware tile map (see xcd_tile; C = 0: one contiguous eighth per XCD);
- * the product uses kXcdChunk. */
-template <typename T, int OP, int Q, int C>
-__global__ void __launch_bounds__(kReduceBlock)
-k_reduce_shift_xcd(T *dst, const T *src, size_t head, size_t nvec, size_t tail, unsigned rb)
-{
-    constexpr int V   = 16 / sizeof(T);
-    const size_t gtid = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
-    if (gtid < head) {
-        dst[gtid] = Comb<T, OP>::apply(src[gtid], dst[gtid]);
-    }
-    if (gtid < tail) {
-        const size_t j = head + nvec * V + gtid;
-        dst[j] = Comb<T, OP>::apply(src[j], dst[j]);
-    }
-    /* C = 0: one contiguous eighth per XCD (a chunk of all its tiles) */
-    const unsigned tile  = xcd_tile<C ? C : 0x7fffffffu>(blockIdx.x, gridDim.x);
-    const size_t i       = (size_t)tile * kReduceBlock + threadIdx.x;
-    const bool last_lane = threadIdx.x == kReduceBlock - 1;
-    const char *sp  = reinterpret_cast<const char*>(src + head);
-    const u32x4 *a4 = reinterpret_cast<const u32x4*>(sp - (4 * Q + rb));
-    u32x4 *d4       = reinterpret_cast<u32x4*>(dst + head);
-    if (nvec == 0) {
-        return;
-    }
-    const u32x4 b4 = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
+    const u32x4 b  = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
     const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
     const u32x4 ex = ld16<1>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
-    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);  /* keep the shuffles behind all loads */
+    /* A[i + 1]: the next lane's load; lane 63 loaded it itself */
     u32x4 hi;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
-        hi[k] = from_next_lane<0>(lo[k]);
+        hi[k] = from_next_lane(lo[k]);
     }
     if (last_lane) {
         hi = ex;
@@ -329,7 +230,7 @@ k_reduce_shift_xcd(T *dst, const T *src, size_t head, size_t nvec, size_t tail, 
         for (int k = 0; k < 4; k++) {
             sv[k] = __builtin_amdgcn_alignbyte(w[Q + k + 1], w[Q + k], rb);
         }
-        st16<1>(d4 + i, vapply<T, OP>(sv, b4));
+        st16<1>(d4 + i, vapply<T, OP>(sv, b));
     }
 }
 
@@ -378,11 +279,14 @@ __device__ __forceinline__ E rd_tree(E (&val)[N], F f)
     return val[0];
 }
 
-template <typename T, int OP, int N, int XM = 0>
+template <typename T, int OP, int N, int XM = 0, int CAP = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                size_t tail)
 {
+    if constexpr (CAP) {
+        UCG_MULTI_CAP_CLOBBER();
+    }
     constexpr int V    = 16 / sizeof(T);
     const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
     auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };
@@ -512,7 +416,7 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
             u32x4 hi;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                hi[k] = from_next_lane<0>(val[m][k]);
+                hi[k] = from_next_lane(val[m][k]);
             }
             if (last_lane) {
                 hi = ex[m];
@@ -536,10 +440,13 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
  * two, and for MPI_Reduce). Operands past n load srcs[0] again (an L2 hit,
  * no branch between the loads) and are not combined.
  */
-template <typename T, int OP, int NMAX, int XM = 0>
+template <typename T, int OP, int NMAX, int XM = 0, int CAP = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
 {
+    if constexpr (CAP) {
+        UCG_MULTI_CAP_CLOBBER();
+    }
     constexpr int V    = 16 / sizeof(T);
     const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
 
@@ -643,7 +550,7 @@ k_reduce_tree_shift(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, 
             u32x4 hi;
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                hi[k] = from_next_lane<0>(val[m][k]);
+                hi[k] = from_next_lane(val[m][k]);
             }
             if (last_lane) {
                 hi = ex[m];
@@ -660,39 +567,6 @@ k_reduce_tree_shift(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, 
             }
         }
         st16<1>(d4 + i, acc);
-    }
-}
-
-/* the tree fan-in element loop (A/B variant 4 only: what k_reduce_tree_shift
- * replaced) */
-template <typename T, int OP>
-__global__ void __launch_bounds__(kBlock)
-k_reduce_tree_scalar(T *dst, SrcList srcs, unsigned n, size_t count)
-{
-    const size_t nthr = (size_t)gridDim.x * kBlock;
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += nthr) {
-        T acc = static_cast<const T*>(srcs.p[0])[i];
-        for (unsigned m = 1; m < n; m++) {
-            acc = Comb<T, OP>::apply(static_cast<const T*>(srcs.p[m])[i], acc);
-        }
-        dst[i] = acc;
-    }
-}
-
-template <typename T, int OP, int N>
-__global__ void __launch_bounds__(kBlock)
-k_reduce_multi_scalar(T *dst, SrcList srcs, unsigned self, size_t count)
-{
-    const size_t nthr = (size_t)gridDim.x * kBlock;
-    auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };
-    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < count;
-         i += nthr) {
-        T val[N];
-#pragma unroll
-        for (int m = 0; m < N; m++) {
-            val[m] = static_cast<const T*>(srcs.p[self ^ m])[i];
-        }
-        dst[i] = rd_tree<N>(val, fs);
     }
 }
 

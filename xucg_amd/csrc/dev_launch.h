@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <type_traits>
 #include <utility>
 
 #include "ucg_builtin_dev.h"
@@ -17,16 +18,13 @@
 
 namespace ucgdev {
 
-/* UCX_BUILTIN_DEV_MAX_BLOCKS: grid cap of the looping (scalar) kernels;
+/* UCX_BUILTIN_DEV_MAX_BLOCKS: grid cap of the looping (element-wise) kernels;
  * defined in dev_combine.hip */
 int launch_max_blocks();
-/* UCX_BUILTIN_DEV_VARIANT: A/B tuning knob (0 = product); defined likewise */
-int launch_variant();
-/* dynamic LDS that caps the waves per CU of a multi-operand launch of `grid`
- * one-wave workgroups reading `operands` distinct buffers
- * (UCX_BUILTIN_DEV_MULTI_WAVES); 0 for a grid the cap would not limit;
+/* whether the multi-operand kernels run under their occupancy cap
+ * (UCX_BUILTIN_DEV_MULTI_CAP, ucg_builtin_dev_set_multi_cap; default yes);
  * likewise */
-size_t multi_lds_bytes(unsigned operands, size_t grid);
+bool multi_capped();
 
 inline size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
 
@@ -46,7 +44,7 @@ inline unsigned grid_for(size_t work_items, size_t per_block, int cap)
 /* reduce launchers                                                         */
 /* ------------------------------------------------------------------------ */
 typedef hipError_t (*reduce_fn_t)(void *dst, const void *src, size_t count,
-                                  hipStream_t st, int variant);
+                                  hipStream_t st);
 
 /* A dispatch packet counts work-items in 32 bits, so one launch covers at
  * most 2^31 16-B vectors (32 GiB per operand); larger operands (HBM holds
@@ -71,16 +69,14 @@ inline size_t line_head(const void *dst, size_t count)
     return h < count ? h : count;
 }
 
-/* XCD-aware tile map when a source's vectors straddle lines (see k_reduce);
- * A/B variant 14 keeps the identity map */
+/* XCD-aware tile map when a source's vectors straddle lines (see k_reduce) */
 inline bool straddles_lines(const void *p)
 {
-    return ((uintptr_t)p & (kLine - 1)) != 0 && launch_variant() != 14;
+    return ((uintptr_t)p & (kLine - 1)) != 0;
 }
 
-template <typename T, int OP, int U, int NT, int BS, int XM = 0>
-void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
-                       hipStream_t st)
+template <typename T, int OP, int XM>
+void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
     constexpr size_t V = 16 / sizeof(T);
     size_t done = 0;
@@ -90,12 +86,13 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
         const size_t off = first ? 0 : head + done * V;
         /* one tile of U vectors per lane: grid sized to the chunk (no loop),
          * and to the head's lanes */
-        unsigned grid = grid_for(chunk, (size_t)BS * U, 0x7fffffff);
-        if (first && div_up(head, BS) > grid) {
-            grid = (unsigned)div_up(head, BS);
+        unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kReduceU, 0x7fffffff);
+        if (first && div_up(head, kReduceBlock) > grid) {
+            grid = (unsigned)div_up(head, kReduceBlock);
         }
-        hipLaunchKernelGGL((k_reduce<T, OP, U, NT, BS, XM>), dim3(grid), dim3(BS), 0, st,
-                           d + off, s + off, first ? head : 0, chunk, last ? tail : 0);
+        hipLaunchKernelGGL((k_reduce<T, OP, kReduceU, 1, kReduceBlock, XM>), dim3(grid),
+                           dim3(kReduceBlock), 0, st, d + off, s + off, first ? head : 0,
+                           chunk, last ? tail : 0);
         done += chunk;
     } while (done < nvec);
 }
@@ -103,7 +100,7 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail,
 /* k_reduce_shift, chunked like launch_vec. Q = (src - dst) mod 16 B in
  * whole words, rb the remaining bytes; pairs a dtype cannot produce (rb != 0
  * for 4-B elements, anything but Q = 2 for 8-B ones) are not instantiated. */
-template <typename T, int OP, int Q, int U = 1, int DPP = 0>
+template <typename T, int OP, int Q>
 void launch_shift(T *d, const T *s, size_t head, size_t nvec, size_t tail,
                   unsigned rb, hipStream_t st)
 {
@@ -121,8 +118,8 @@ void launch_shift(T *d, const T *s, size_t head, size_t nvec, size_t tail,
             size_t items = chunk;
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
-            const unsigned grid = grid_for(items, (size_t)kReduceBlock * U, 0x7fffffff);
-            hipLaunchKernelGGL((k_reduce_shift<T, OP, Q, U, DPP>), dim3(grid), dim3(kReduceBlock),
+            const unsigned grid = grid_for(items, (size_t)kReduceBlock, 0x7fffffff);
+            hipLaunchKernelGGL((k_reduce_shift<T, OP, Q>), dim3(grid), dim3(kReduceBlock),
                                0, st, d + off, s + off, first ? head : 0, chunk,
                                last ? tail : 0, rb);
             done += chunk;
@@ -131,8 +128,7 @@ void launch_shift(T *d, const T *s, size_t head, size_t nvec, size_t tail,
 }
 
 template <int DT, int OP>
-hipError_t launch_reduce(void *dst, const void *src, size_t count,
-                                hipStream_t st, int variant)
+hipError_t launch_reduce(void *dst, const void *src, size_t count, hipStream_t st)
 {
     typedef typename DtType<DT>::T T;
     constexpr size_t sz = sizeof(T);
@@ -141,8 +137,8 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
     const T *s = static_cast<const T*>(src);
     const uintptr_t md = (uintptr_t)dst & 15, ms = (uintptr_t)src & 15;
 
-    if (md != ms && ((md | ms) % sz != 0 || variant == 4)) {
-        /* not even element-aligned (or the A/B variant 4): element loop */
+    if (md != ms && (md | ms) % sz != 0) {
+        /* not even element-aligned: element loop */
         const unsigned grid = grid_for(count, (size_t)kBlock * 4,
                                        launch_max_blocks());
         hipLaunchKernelGGL((k_reduce_scalar<T, OP>), dim3(grid), dim3(kBlock),
@@ -156,41 +152,6 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
     if (md != ms) {
         /* operands disagree mod 16 B: src realigned in registers */
         const unsigned r = (unsigned)((ms + 16 - md) & 15);
-        if constexpr (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM) {
-            if (variant >= 9 && variant <= 12 && r == 4 && nvec < kMaxVecPerLaunch) {
-                /* A/B: XCD-aware tile maps for the realigning kernel */
-                const unsigned g = grid_for(nvec > head ? nvec : head, kReduceBlock,
-                                            0x7fffffff);
-                if (variant == 9)
-                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 0>), dim3(g),
-                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
-                else if (variant == 10)
-                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 2048>), dim3(g),
-                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
-                else if (variant == 11)
-                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 64>), dim3(g),
-                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
-                else
-                    hipLaunchKernelGGL((k_reduce_shift_xcd<T, OP, 1, 128>), dim3(g),
-                                       dim3(kReduceBlock), 0, st, d, s, head, nvec, tail, 0u);
-                return hipGetLastError();
-            }
-            if (variant >= 5 && variant <= 8 && r == 4) {
-                /* A/B: U = 2 or 4 vectors per lane (one extra load per 64 U),
-                 * the DPP lane shift instead of ds_bpermute, or every lane
-                 * loading both aligned vectors (no cross-lane step) */
-                if (variant == 5)      launch_shift<T, OP, 1, 2>(d, s, head, nvec, tail, 0, st);
-                else if (variant == 6) launch_shift<T, OP, 1, 4>(d, s, head, nvec, tail, 0, st);
-                else if (variant == 7) launch_shift<T, OP, 1, 1, 1>(d, s, head, nvec, tail, 0, st);
-                else if (nvec < kMaxVecPerLaunch) {
-                    const unsigned g = grid_for(nvec > head ? nvec : head, kReduceBlock,
-                                                0x7fffffff);
-                    hipLaunchKernelGGL((k_reduce_shift2<T, OP, 1>), dim3(g), dim3(kReduceBlock),
-                                       0, st, d, s, head, nvec, tail, 0u);
-                }
-                return hipGetLastError();
-            }
-        }
         switch (r >> 2) {
         case 0:  launch_shift<T, OP, 0>(d, s, head, nvec, tail, r & 3, st); break;
         case 1:  launch_shift<T, OP, 1>(d, s, head, nvec, tail, r & 3, st); break;
@@ -199,24 +160,10 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count,
         }
         return hipGetLastError();
     }
-
-    if (DT == UCG_DEV_DT_FLOAT32 && OP == UCG_DEV_OP_SUM && variant >= 0) {
-        /* tuning variants of the headline kernel (UCX_BUILTIN_DEV_VARIANT) */
-        switch (variant) {
-        case 1: launch_vec<T, OP, 4, 1, 256>(d, s, head, nvec, tail, st); break;
-        case 2: launch_vec<T, OP, 1, 1, 256>(d, s, head, nvec, tail, st); break;
-        case 3: launch_vec<T, OP, 1, 0, 64>(d, s, head, nvec, tail, st); break;
-        default:
-            if (straddles_lines(s + head))
-                launch_vec<T, OP, kReduceU, 1, kReduceBlock, 1>(d, s, head, nvec, tail, st);
-            else
-                launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
-            break;
-        }
-    } else if (straddles_lines(s + head)) {
-        launch_vec<T, OP, kReduceU, 1, kReduceBlock, 1>(d, s, head, nvec, tail, st);
+    if (straddles_lines(s + head)) {
+        launch_vec<T, OP, 1>(d, s, head, nvec, tail, st);
     } else {
-        launch_vec<T, OP, kReduceU, 1, kReduceBlock>(d, s, head, nvec, tail, st);
+        launch_vec<T, OP, 0>(d, s, head, nvec, tail, st);
     }
     return hipGetLastError();
 }
@@ -243,6 +190,18 @@ reduce_row(std::integer_sequence<int, OPS...>)
 typedef hipError_t (*multi_fn_t)(void *dst, const SrcList &srcs, unsigned n,
                                  unsigned self, size_t count, hipStream_t st);
 
+/* Occupancy cap of the multi-operand kernels (kMultiCap, dev_kernels.h):
+ * with 4 or more operands the aligned forms run capped. The uncapped forms
+ * are also built for fp32 and fp64 SUM, for A/B runs in one process
+ * (ucg_builtin_dev_set_multi_cap(0): bench.py's one-shot reduce-scatter over
+ * xGMI); every other pair always runs capped. */
+template <typename T, int OP>
+constexpr bool uncapped_ab()
+{
+    return OP == UCG_DEV_OP_SUM && (std::is_same<T, float>::value ||
+                                    std::is_same<T, double>::value);
+}
+
 template <typename T, int OP, int N>
 hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
                                  size_t count, hipStream_t st)
@@ -254,18 +213,14 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
     }
     T *d = static_cast<T*>(dst);
-    if (!aligned && launch_variant() == 4) {
-        /* A/B only: the element loop the realigning kernel replaced */
-        const unsigned grid = grid_for(count, kBlock, launch_max_blocks());
-        hipLaunchKernelGGL((k_reduce_multi_scalar<T, OP, N>), dim3(grid),
-                           dim3(kBlock), 0, st, d, srcs, self, count);
-        return hipGetLastError();
-    }
     const size_t head = line_head<T>(dst, count);
     bool xm = false;
     for (int m = 0; m < N; m++) {
         xm = xm || straddles_lines(static_cast<const T*>(srcs.p[m]) + head);
     }
+    /* capped: always with 4+ operands, unless switched off for an A/B pair */
+    constexpr bool can_cap = N >= 4;
+    const bool cap = can_cap && (!uncapped_ab<T, OP>() || multi_capped());
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
     size_t done = 0;
     do {
@@ -276,31 +231,38 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
         for (int m = 0; m < kMaxMulti; m++) {
             sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
         }
+        const size_t h = first ? head : 0, t = last ? tail : 0;
         if (aligned) {
             unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kMultiU, 0x7fffffff);
             if (first && div_up(head, kReduceBlock) > grid) {
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
-            const size_t lds = multi_lds_bytes(N, grid);   /* occupancy cap */
-            if (xm)
-                hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1>), dim3(grid), dim3(kReduceBlock),
-                                   lds, st, d + off, sl, self, first ? head : 0, chunk,
-                                   last ? tail : 0);
-            else
-                hipLaunchKernelGGL((k_reduce_multi<T, OP, N>), dim3(grid), dim3(kReduceBlock), lds,
-                                   st, d + off, sl, self, first ? head : 0, chunk,
-                                   last ? tail : 0);
+            const dim3 g(grid), b(kReduceBlock);
+            if (cap) {
+                if (xm)
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, can_cap>), g, b, 0, st,
+                                       d + off, sl, self, h, chunk, t);
+                else
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 0, can_cap>), g, b, 0, st,
+                                       d + off, sl, self, h, chunk, t);
+            } else if constexpr (!can_cap || uncapped_ab<T, OP>()) {
+                if (xm)
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 0>), g, b, 0, st,
+                                       d + off, sl, self, h, chunk, t);
+                else
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 0, 0>), g, b, 0, st,
+                                       d + off, sl, self, h, chunk, t);
+            }
         } else {
-            /* some operand out of phase with dst: realigned in registers */
+            /* some operand out of phase with dst: realigned in registers
+             * (uncapped: the realigning form lost 2-4 points under a cap on
+             * two boxes, profiles/r03/shift2) */
             size_t items = chunk;
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
-            /* uncapped: the realigning form lost 2-4 points under the cap on
-             * two boxes (profiles/r03/shift2) */
             hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N>), dim3(grid), dim3(kReduceBlock),
-                               0, st, d + off, sl, self, first ? head : 0, chunk,
-                               last ? tail : 0);
+                               0, st, d + off, sl, self, h, chunk, t);
         }
         done += chunk;
     } while (done < nvec);
@@ -364,6 +326,9 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
                    size_t tail, bool aligned, bool xm, hipStream_t st)
 {
     constexpr size_t V = 16 / sizeof(T);
+    /* capped from 5 operands on (NMAX 8 and 16), as launch_multi_n */
+    constexpr bool can_cap = NMAX >= 8;
+    const bool cap = can_cap && (!uncapped_ab<T, OP>() || multi_capped());
     size_t done = 0;
     do {
         const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
@@ -373,20 +338,28 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
         for (int m = 0; m < kMaxMulti; m++) {
             sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
         }
+        const size_t h = first ? head : 0, t = last ? tail : 0;
         if (aligned) {
             unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
             if (first && div_up(head, kReduceBlock) > grid) {
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
-            const size_t lds = multi_lds_bytes(n, grid);   /* occupancy cap */
-            if (xm)
-                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1>), dim3(grid),
-                                   dim3(kReduceBlock), lds, st, d + off, sl, n, first ? head : 0,
-                                   chunk, last ? tail : 0);
-            else
-                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX>), dim3(grid), dim3(kReduceBlock),
-                                   lds, st, d + off, sl, n, first ? head : 0, chunk,
-                                   last ? tail : 0);
+            const dim3 g(grid), b(kReduceBlock);
+            if (cap) {
+                if (xm)
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, can_cap>), g, b, 0, st,
+                                       d + off, sl, n, h, chunk, t);
+                else
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 0, can_cap>), g, b, 0, st,
+                                       d + off, sl, n, h, chunk, t);
+            } else if constexpr (!can_cap || uncapped_ab<T, OP>()) {
+                if (xm)
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 0>), g, b, 0, st,
+                                       d + off, sl, n, h, chunk, t);
+                else
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 0, 0>), g, b, 0, st,
+                                       d + off, sl, n, h, chunk, t);
+            }
         } else {
             /* some operand out of phase with dst: realigned in registers */
             size_t items = chunk;
@@ -395,8 +368,7 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
             /* uncapped, as k_reduce_multi_shift */
             hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX>), dim3(grid),
-                               dim3(kReduceBlock), 0, st, d + off, sl, n, first ? head : 0,
-                               chunk, last ? tail : 0);
+                               dim3(kReduceBlock), 0, st, d + off, sl, n, h, chunk, t);
         }
         done += chunk;
     } while (done < nvec);
@@ -414,13 +386,6 @@ hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
         aligned = aligned && (((uintptr_t)srcs.p[m] & 15) == md);
     }
     T *d = static_cast<T*>(dst);
-    if (!aligned && launch_variant() == 4) {
-        /* A/B only: the element loop the realigning kernel replaced */
-        const unsigned grid = grid_for(count, kBlock, launch_max_blocks());
-        hipLaunchKernelGGL((k_reduce_tree_scalar<T, OP>), dim3(grid), dim3(kBlock), 0, st,
-                           d, srcs, n, count);
-        return hipGetLastError();
-    }
     const size_t head = line_head<T>(dst, count);
     bool xm = false;
     for (unsigned m = 0; m < n; m++) {

@@ -1,0 +1,867 @@
+/*
+ * dev_mem.hip - device memory and peer mapping of the C-ABI shim
+ * (include/ucg_builtin_dev.h, "peer mapping" and "memory helpers").
+ *
+ * It stands in for the memory registration and remote keys the reference gets
+ * from UCT (uct_md_mem_reg / uct_md_mkey_pack for the zero-copy steps,
+ * builtin/ops/builtin_control.c:276-286, 712-719, 1284-1304): a key names a
+ * buffer so that a peer process can read it in place, over xGMI.
+ *
+ * A key names a physical allocation, never an address (round 4):
+ *  - Shareable allocations (ucg_builtin_dev_malloc_shareable) are HIP virtual
+ *    memory: hipMemCreate with a POSIX file descriptor handle type, mapped at
+ *    a reservation of this process. A peer maps one from its file
+ *    descriptor, which it gets from the exporter's key server over a Unix
+ *    socket (SCM_RIGHTS): the fd holds the physical memory itself, so a key
+ *    can never resolve to another allocation, and a peer's mapping keeps the
+ *    memory alive after the exporter frees it (no fault, and nobody else's
+ *    data).
+ *  - Other device memory (ucg_builtin_dev_malloc, a caller's hipMalloc) is
+ *    exported with hipIpcGetMemHandle, whose handle names (pid, address,
+ *    size). The key server hands that handle out only while the runtime's
+ *    buffer id of the allocation at that address is the one recorded at
+ *    export: a buffer freed and allocated again at the same address is a new
+ *    allocation, and its old keys are refused.
+ * Every key carries a per-process id that is never reused; freeing an
+ * exported allocation retires its id, so a stale key fails loudly at import
+ * (UCS_ERR_NO_RESOURCE, "stale key") instead of mapping
+ * whatever now lives there. This replaces round 3's rule that exported
+ * memory is never freed (stale IPC keys).
+ */
+#include <hip/hip_runtime.h>
+
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <fcntl.h>
+#include <pthread.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <tuple>
+#include <unordered_map>
+
+#include "dev_internal.h"
+
+namespace {
+
+constexpr size_t kGran = (size_t)2 << 20;     /* allocation and mapping granule */
+
+size_t round_gran(size_t bytes)
+{
+    return bytes ? (bytes + kGran - 1) / kGran * kGran : kGran;
+}
+
+/* ---- the process's allocations and memory events ------------------------- */
+enum { KIND_PLAIN = 1, KIND_VMM = 2 };
+
+struct own_alloc {
+    int      kind;
+    int      device;
+    size_t   bytes;
+    hipMemGenericAllocationHandle_t handle;   /* KIND_VMM */
+    uint64_t key_id;                          /* 0: never exported */
+};
+
+std::mutex g_mu;                                      /* guards everything here */
+std::unordered_map<void*, own_alloc> g_allocs;        /* base -> allocation */
+
+/* The last memory events of the process, for ucg_builtin_dev_debug_ptr: a
+ * buffer found to read as zeros is matched against what happened to its
+ * address range. */
+struct mem_event {
+    char     kind;      /* M malloc, V shareable malloc, F free, X export,
+                           I import, C release (close), S stale key refused */
+    void    *ptr;
+    void    *base;
+    size_t   bytes;
+    uint64_t ns;        /* CLOCK_MONOTONIC */
+    int      rc;        /* the runtime's return code */
+};
+constexpr size_t kMemEvents = 1024;
+mem_event g_events[kMemEvents];
+uint64_t  g_nevents;
+
+uint64_t now_ns()
+{
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+/* caller holds g_mu */
+void note_event(char kind, void *ptr, void *base, size_t bytes, int rc)
+{
+    g_events[g_nevents++ % kMemEvents] = mem_event{kind, ptr, base, bytes, now_ns(), rc};
+}
+
+/* ---- exported allocations (the key server's table) ----------------------- */
+struct export_rec {
+    int                kind;
+    void              *base;
+    size_t             size;
+    int                fd;          /* KIND_VMM: the shareable handle, open while exported */
+    unsigned long long buffer_id;   /* KIND_PLAIN: the runtime's id at export */
+    hipIpcMemHandle_t  ih;          /* KIND_PLAIN */
+};
+std::unordered_map<uint64_t, export_rec> g_exports;   /* key id -> record */
+std::unordered_map<void*, uint64_t> g_export_of;      /* allocation base -> key id */
+uint64_t g_next_id = 1;                               /* never reused */
+
+/* ---- the key blob (UCG_BUILTIN_DEV_IPC_HANDLE_BYTES, opaque to callers) --- */
+struct ipc_blob {
+    uint64_t magic;
+    uint32_t kind;
+    uint32_t pid;      /* exporter */
+    uint64_t token;    /* exporter's key server (random per process) */
+    uint64_t id;       /* key id at the exporter */
+    uint64_t offset;   /* of the exported pointer in its allocation */
+    uint64_t size;     /* of the allocation */
+};
+static_assert(sizeof(ipc_blob) <= UCG_BUILTIN_DEV_IPC_HANDLE_BYTES,
+              "IPC blob does not fit the ABI size");
+constexpr uint64_t kIpcMagic = 0x5543475f49504332ull;   /* "UCG_IPC2" */
+
+/* key server protocol: request {id}, reply {status, kind, size, ih} plus the
+ * allocation's fd (SCM_RIGHTS) for KIND_VMM */
+struct key_request {
+    uint64_t magic;
+    uint64_t id;
+};
+struct key_reply {
+    int32_t            status;      /* UCS_OK, or UCS_ERR_NO_RESOURCE: stale key */
+    uint32_t           kind;
+    uint64_t           size;
+    hipIpcMemHandle_t  ih;
+};
+
+uint64_t g_token;           /* 0 until the server runs */
+int      g_listen = -1;
+
+std::string server_name(uint32_t pid, uint64_t token)
+{
+    char b[64];
+    snprintf(b, sizeof(b), "xucg_ipc_%u_%016llx", pid, (unsigned long long)token);
+    return b;
+}
+
+socklen_t abstract_addr(const std::string &name, sockaddr_un *a)
+{
+    memset(a, 0, sizeof(*a));
+    a->sun_family = AF_UNIX;
+    memcpy(a->sun_path + 1, name.data(), name.size());       /* abstract namespace */
+    return (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + name.size());
+}
+
+bool read_full(int s, void *p, size_t n)
+{
+    char *c = static_cast<char*>(p);
+    while (n) {
+        const ssize_t r = read(s, c, n);
+        if (r <= 0) {
+            if (r < 0 && errno == EINTR) continue;
+            return false;
+        }
+        c += r;
+        n -= (size_t)r;
+    }
+    return true;
+}
+
+bool send_reply(int s, const key_reply &rep, int fd)
+{
+    iovec iov = {(void*)&rep, sizeof(rep)};
+    msghdr mh = {};
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    char cbuf[CMSG_SPACE(sizeof(int))];
+    if (fd >= 0) {
+        memset(cbuf, 0, sizeof(cbuf));
+        mh.msg_control = cbuf;
+        mh.msg_controllen = sizeof(cbuf);
+        cmsghdr *c = CMSG_FIRSTHDR(&mh);
+        c->cmsg_level = SOL_SOCKET;
+        c->cmsg_type = SCM_RIGHTS;
+        c->cmsg_len = CMSG_LEN(sizeof(int));
+        memcpy(CMSG_DATA(c), &fd, sizeof(int));
+    }
+    ssize_t r;
+    do {
+        r = sendmsg(s, &mh, MSG_NOSIGNAL);
+    } while (r < 0 && errno == EINTR);
+    return r == (ssize_t)sizeof(rep);
+}
+
+/* One request per connection. Only processes of this user are served. */
+void serve_one(int s)
+{
+    key_request rq;
+    key_reply rep;
+    memset(&rep, 0, sizeof(rep));
+    rep.status = UCS_ERR_INVALID_PARAM;
+    int fd = -1;
+    ucred cr;
+    socklen_t cl = sizeof(cr);
+    if (getsockopt(s, SOL_SOCKET, SO_PEERCRED, &cr, &cl) != 0 || cr.uid != getuid() ||
+        !read_full(s, &rq, sizeof(rq)) || rq.magic != kIpcMagic) {
+        send_reply(s, rep, -1);
+        return;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto it = g_exports.find(rq.id);
+        if (it == g_exports.end()) {
+            rep.status = UCS_ERR_NO_RESOURCE;            /* retired: freed since */
+        } else {
+            const export_rec &e = it->second;
+            rep.kind = (uint32_t)e.kind;
+            rep.size = e.size;
+            rep.status = UCS_OK;
+            if (e.kind == KIND_VMM) {
+                fd = dup(e.fd);
+                if (fd < 0) rep.status = UCS_ERR_IO_ERROR;
+            } else {
+                /* the allocation at that address must still be the exported one */
+                unsigned long long id = 0;
+                const hipError_t he = hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                                             (hipDeviceptr_t)e.base);
+                if (he != hipSuccess || id != e.buffer_id) {
+                    rep.status = UCS_ERR_NO_RESOURCE;
+                    (void)hipGetLastError();
+                } else {
+                    rep.ih = e.ih;
+                }
+            }
+        }
+    }
+    send_reply(s, rep, rep.status == UCS_OK ? fd : -1);
+    if (fd >= 0) {
+        close(fd);
+    }
+}
+
+void serve(int ls)
+{
+    for (;;) {
+        const int s = accept4(ls, nullptr, nullptr, SOCK_CLOEXEC);
+        if (s < 0) {
+            if (errno == EINTR || errno == ECONNABORTED || errno == EMFILE ||
+                errno == ENFILE || errno == ENOBUFS || errno == ENOMEM) {
+                continue;
+            }
+            return;                                   /* the socket is gone */
+        }
+        serve_one(s);
+        close(s);
+    }
+}
+
+/* a forked child has no server thread: it starts its own on first export */
+void after_fork_child()
+{
+    if (g_listen >= 0) {
+        close(g_listen);
+    }
+    g_listen = -1;
+    g_token = 0;
+}
+
+/* Start the key server once per process (first export). Caller holds g_mu. */
+ucs_status_t server_start()
+{
+    static std::once_flag once;
+    std::call_once(once, [] { pthread_atfork(nullptr, nullptr, after_fork_child); });
+    if (g_listen >= 0) {
+        return UCS_OK;
+    }
+    uint64_t tok = 0;
+    const int r = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+    if (r >= 0) {
+        if (read(r, &tok, sizeof(tok)) != (ssize_t)sizeof(tok)) tok = 0;
+        close(r);
+    }
+    tok ^= now_ns() ^ ((uint64_t)getpid() << 32);
+    tok |= 1;
+    const int ls = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (ls < 0) {
+        return set_error(UCS_ERR_IO_ERROR, "ipc key server", strerror(errno));
+    }
+    sockaddr_un a;
+    const socklen_t al = abstract_addr(server_name((uint32_t)getpid(), tok), &a);
+    if (bind(ls, (sockaddr*)&a, al) != 0 || listen(ls, 128) != 0) {
+        const int e = errno;
+        close(ls);
+        return set_error(UCS_ERR_IO_ERROR, "ipc key server", strerror(e));
+    }
+    std::thread(serve, ls).detach();
+    g_listen = ls;
+    g_token = tok;
+    return UCS_OK;
+}
+
+/* Ask member (pid, token) for key `id`: the reply and, for KIND_VMM, the fd */
+ucs_status_t fetch_key(const ipc_blob &b, key_reply *rep, int *fd)
+{
+    *fd = -1;
+    const int s = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    if (s < 0) {
+        return set_error(UCS_ERR_IO_ERROR, "ipc_import", strerror(errno));
+    }
+    sockaddr_un a;
+    const socklen_t al = abstract_addr(server_name(b.pid, b.token), &a);
+    int rc;
+    do {
+        rc = connect(s, (sockaddr*)&a, al);
+    } while (rc != 0 && errno == EINTR);
+    if (rc != 0) {
+        const int e = errno;
+        close(s);
+        return set_error(UCS_ERR_NO_RESOURCE, "ipc_import",
+                         (std::string("the exporter's key server is gone: ") + strerror(e)).c_str());
+    }
+    const key_request rq = {kIpcMagic, b.id};
+    char cbuf[CMSG_SPACE(sizeof(int))];
+    iovec iov = {rep, sizeof(*rep)};
+    msghdr mh = {};
+    mh.msg_iov = &iov;
+    mh.msg_iovlen = 1;
+    mh.msg_control = cbuf;
+    mh.msg_controllen = sizeof(cbuf);
+    ssize_t r = -1;
+    if (write(s, &rq, sizeof(rq)) == (ssize_t)sizeof(rq)) {
+        do {
+            r = recvmsg(s, &mh, MSG_WAITALL | MSG_CMSG_CLOEXEC);
+        } while (r < 0 && errno == EINTR);
+    }
+    close(s);
+    if (r != (ssize_t)sizeof(*rep)) {
+        return set_error(UCS_ERR_IO_ERROR, "ipc_import", "no reply from the key server");
+    }
+    for (cmsghdr *c = CMSG_FIRSTHDR(&mh); c; c = CMSG_NXTHDR(&mh, c)) {
+        if (c->cmsg_level == SOL_SOCKET && c->cmsg_type == SCM_RIGHTS) {
+            memcpy(fd, CMSG_DATA(c), sizeof(int));
+        }
+    }
+    if (rep->status != UCS_OK) {
+        if (*fd >= 0) {
+            close(*fd);
+            *fd = -1;
+        }
+        return set_error((ucs_status_t)rep->status, "ipc_import",
+                         rep->status == UCS_ERR_NO_RESOURCE
+                             ? "stale key: the exported allocation was freed since"
+                             : "the key server refused the key");
+    }
+    if (rep->kind == KIND_VMM && *fd < 0) {
+        return set_error(UCS_ERR_IO_ERROR, "ipc_import", "no file descriptor in the reply");
+    }
+    return UCS_OK;
+}
+
+/* ---- imports (mapped once per key, reference counted) -------------------- */
+struct import_rec {
+    int      kind;      /* KIND_VMM, KIND_PLAIN, or 0: this process's own memory */
+    char    *base;      /* the mapping (or the own allocation) */
+    size_t   size;
+    hipMemGenericAllocationHandle_t handle;   /* KIND_VMM */
+    unsigned refs;
+};
+typedef std::tuple<uint32_t, uint64_t, uint64_t> import_key;   /* pid, token, id */
+std::map<import_key, import_rec> g_imports;
+std::unordered_multimap<void*, import_key> g_import_ptr;     /* pointer handed out -> key */
+
+hipMemAccessDesc rw_access(int device)
+{
+    hipMemAccessDesc d;
+    memset(&d, 0, sizeof(d));
+    d.location.type = hipMemLocationTypeDevice;
+    d.location.id = device;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    return d;
+}
+
+/* map an imported VMM allocation (fd) at a new reservation of this process */
+ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
+{
+    hipMemGenericAllocationHandle_t h;
+    HIP_TRY(hipMemImportFromShareableHandle(&h, (void*)(intptr_t)fd,
+                                            hipMemHandleTypePosixFileDescriptor));
+    void *va = nullptr;
+    hipError_t e = hipMemAddressReserve(&va, size, kGran, nullptr, 0);
+    if (e == hipSuccess) {
+        e = hipMemMap(va, size, 0, h, 0);
+        if (e == hipSuccess) {
+            const hipMemAccessDesc d = rw_access(device);
+            e = hipMemSetAccess(va, size, &d, 1);
+            if (e != hipSuccess) {
+                (void)hipMemUnmap(va, size);
+            }
+        }
+        if (e != hipSuccess) {
+            (void)hipMemAddressFree(va, size);
+        }
+    }
+    if (e != hipSuccess) {
+        (void)hipMemRelease(h);
+        return hip_status(e, "ipc_import: map of the peer's allocation");
+    }
+    m->kind = KIND_VMM;
+    m->base = static_cast<char*>(va);
+    m->size = size;
+    m->handle = h;
+    return UCS_OK;
+}
+
+void unmap_import(import_rec &m)
+{
+    if (m.kind == KIND_VMM) {
+        (void)hipMemUnmap(m.base, m.size);
+        (void)hipMemAddressFree(m.base, m.size);
+        (void)hipMemRelease(m.handle);
+    } else if (m.kind == KIND_PLAIN) {
+        (void)hipIpcCloseMemHandle(m.base);
+    }
+}
+
+}  // namespace
+
+/* ---- peer mapping ---------------------------------------------------------- */
+ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
+                                        const void *dev_ptr, void *handle)
+{
+    if (ctx == nullptr || dev_ptr == nullptr || handle == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_export", "bad arguments");
+    }
+    HIP_TRY(hipSetDevice(dev_ctx_device(ctx)));
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    HIP_TRY(hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)dev_ptr));
+
+    std::lock_guard<std::mutex> g(g_mu);
+    ucs_status_t st = server_start();
+    if (st != UCS_OK) {
+        return st;
+    }
+    auto own = g_allocs.find((void*)base);
+    uint64_t id = 0;
+    auto ex = g_export_of.find((void*)base);
+    if (ex != g_export_of.end()) {
+        id = ex->second;
+        export_rec &e = g_exports[id];
+        if (e.kind == KIND_PLAIN) {
+            /* caller memory: the allocation at this address may be a new one */
+            unsigned long long bid = 0;
+            if (hipPointerGetAttribute(&bid, HIP_POINTER_ATTRIBUTE_BUFFER_ID, base) !=
+                    hipSuccess || bid != e.buffer_id || e.size != size) {
+                (void)hipGetLastError();
+                g_exports.erase(id);               /* its keys are stale now */
+                g_export_of.erase(ex);
+                id = 0;
+            }
+        }
+    }
+    if (id == 0) {
+        export_rec e;
+        memset(&e, 0, sizeof(e));
+        e.base = (void*)base;
+        e.size = size;
+        e.fd = -1;
+        if (own != g_allocs.end() && own->second.kind == KIND_VMM) {
+            e.kind = KIND_VMM;
+            int fd = -1;
+            HIP_TRY(hipMemExportToShareableHandle(&fd, own->second.handle,
+                                                  hipMemHandleTypePosixFileDescriptor, 0));
+            e.fd = fd;
+        } else {
+            e.kind = KIND_PLAIN;
+            HIP_TRY(hipPointerGetAttribute(&e.buffer_id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
+                                           base));
+            HIP_TRY(hipIpcGetMemHandle(&e.ih, (void*)base));
+        }
+        id = g_next_id++;
+        g_exports[id] = e;
+        g_export_of[(void*)base] = id;
+        if (own != g_allocs.end()) {
+            own->second.key_id = id;
+        }
+    }
+    note_event('X', (void*)dev_ptr, (void*)base, size, 0);
+    const export_rec &e = g_exports[id];
+    ipc_blob b;
+    memset(&b, 0, sizeof(b));
+    b.magic  = kIpcMagic;
+    b.kind   = (uint32_t)e.kind;
+    b.pid    = (uint32_t)getpid();
+    b.token  = g_token;
+    b.id     = id;
+    b.offset = (uint64_t)((const char*)dev_ptr - (const char*)base);
+    b.size   = (uint64_t)size;
+    memset(handle, 0, UCG_BUILTIN_DEV_IPC_HANDLE_BYTES);
+    memcpy(handle, &b, sizeof(b));
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
+                                        const void *handle, void **dev_ptr)
+{
+    if (ctx == nullptr || handle == nullptr || dev_ptr == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import", "bad arguments");
+    }
+    ipc_blob b;
+    memcpy(&b, handle, sizeof(b));
+    if (b.magic != kIpcMagic || b.offset >= b.size ||
+        (b.kind != KIND_VMM && b.kind != KIND_PLAIN)) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import", "not an exported handle");
+    }
+    const int device = dev_ctx_device(ctx);
+    HIP_TRY(hipSetDevice(device));
+    const import_key k{b.pid, b.token, b.id};
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto it = g_imports.find(k);
+        if (it != g_imports.end()) {
+            it->second.refs++;
+            *dev_ptr = it->second.base + b.offset;
+            g_import_ptr.emplace(*dev_ptr, k);
+            return UCS_OK;
+        }
+        if (b.pid == (uint32_t)getpid() && b.token == g_token) {
+            /* this process's own allocation: no mapping, but the key must
+             * still be live */
+            auto ex = g_exports.find(b.id);
+            if (ex == g_exports.end()) {
+                note_event('S', nullptr, nullptr, (size_t)b.size, 0);
+                return set_error(UCS_ERR_NO_RESOURCE, "ipc_import",
+                                 "stale key: the exported allocation was freed since");
+            }
+            import_rec m = {0, static_cast<char*>(ex->second.base), ex->second.size, {}, 1};
+            g_imports[k] = m;
+            *dev_ptr = m.base + b.offset;
+            g_import_ptr.emplace(*dev_ptr, k);
+            return UCS_OK;
+        }
+    }
+    key_reply rep;
+    int fd = -1;
+    ucs_status_t st = fetch_key(b, &rep, &fd);
+    if (st != UCS_OK) {
+        std::lock_guard<std::mutex> g(g_mu);
+        note_event('S', nullptr, nullptr, (size_t)b.size, (int)st);
+        return st;
+    }
+    if (rep.size != b.size || rep.kind != b.kind) {
+        if (fd >= 0) close(fd);
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_import",
+                         "the key server describes another allocation");
+    }
+    import_rec m;
+    memset(&m, 0, sizeof(m));
+    if (b.kind == KIND_VMM) {
+        st = map_vmm(fd, (size_t)b.size, device, &m);
+        close(fd);
+        if (st != UCS_OK) {
+            return st;
+        }
+    } else {
+        void *base = nullptr;
+        HIP_TRY(hipIpcOpenMemHandle(&base, rep.ih, hipIpcMemLazyEnablePeerAccess));
+        /* the mapping must span the exporter's allocation; where the runtime
+         * cannot answer the range query for an imported pointer, it must at
+         * least know the pointer as device memory */
+        hipDeviceptr_t mb = nullptr;
+        size_t ms = 0;
+        bool ok;
+        if (hipMemGetAddressRange(&mb, &ms, (hipDeviceptr_t)base) == hipSuccess) {
+            ok = mb == (hipDeviceptr_t)base && ms >= b.size;
+        } else {
+            (void)hipGetLastError();
+            hipPointerAttribute_t at;
+            memset(&at, 0, sizeof(at));
+            ok = hipPointerGetAttributes(&at, base) == hipSuccess &&
+                 at.type == hipMemoryTypeDevice;
+            (void)hipGetLastError();
+        }
+        if (!ok) {
+            (void)hipIpcCloseMemHandle(base);
+            return set_error(UCS_ERR_INVALID_PARAM, "ipc_import",
+                             "mapped range does not cover the exported allocation");
+        }
+        m.kind = KIND_PLAIN;
+        m.base = static_cast<char*>(base);
+        m.size = (size_t)b.size;
+    }
+    m.refs = 1;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_imports.find(k);
+    if (it != g_imports.end()) {
+        /* another thread mapped it meanwhile: keep that one */
+        unmap_import(m);
+        it->second.refs++;
+        *dev_ptr = it->second.base + b.offset;
+    } else {
+        g_imports[k] = m;
+        *dev_ptr = m.base + b.offset;
+    }
+    g_import_ptr.emplace(*dev_ptr, k);
+    note_event('I', *dev_ptr, g_imports[k].base, (size_t)b.size, 0);
+    return UCS_OK;
+}
+
+ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx, void *dev_ptr)
+{
+    if (ctx == nullptr || dev_ptr == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "ipc_release", "bad arguments");
+    }
+    import_rec m;
+    bool last = false;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto p = g_import_ptr.find(dev_ptr);
+        if (p == g_import_ptr.end()) {
+            return set_error(UCS_ERR_INVALID_PARAM, "ipc_release", "not an imported pointer");
+        }
+        const import_key k = p->second;
+        g_import_ptr.erase(p);
+        auto it = g_imports.find(k);
+        if (it != g_imports.end() && --it->second.refs == 0) {
+            m = it->second;
+            last = true;
+            g_imports.erase(it);
+        }
+    }
+    if (last && m.kind) {
+        /* nothing of this process may still read it (outside the lock: the
+         * key server keeps answering peers meanwhile) */
+        (void)hipSetDevice(dev_ctx_device(ctx));
+        const hipError_t e = hipDeviceSynchronize();
+        unmap_import(m);
+        std::lock_guard<std::mutex> g(g_mu);
+        note_event('C', dev_ptr, m.base, m.size, (int)e);
+    }
+    return UCS_OK;
+}
+
+/* ---- memory helpers -------------------------------------------------------- */
+void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
+{
+    void *p = nullptr;
+    if (ctx) {
+        (void)hipSetDevice(dev_ctx_device(ctx));
+    }
+    int device = 0;
+    (void)hipGetDevice(&device);
+    /* whole 2 MiB granules: a small hipMalloc may be carved out of a block
+     * the runtime shares with other allocations, and such memory cannot be
+     * exported through hipIpcGetMemHandle (ucg_builtin_dev_ipc_export) */
+    bytes = round_gran(bytes);
+    const hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+        hip_status(e, "hipMalloc");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0};
+    note_event('M', p, p, bytes, 0);
+    return p;
+}
+
+void *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
+{
+    int device = 0;
+    if (ctx) {
+        device = dev_ctx_device(ctx);
+        (void)hipSetDevice(device);
+    } else {
+        (void)hipGetDevice(&device);
+    }
+    bytes = round_gran(bytes);
+    hipMemAllocationProp prop;
+    memset(&prop, 0, sizeof(prop));
+    prop.type = hipMemAllocationTypePinned;
+    prop.requestedHandleType = hipMemHandleTypePosixFileDescriptor;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    hipMemGenericAllocationHandle_t h;
+    hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
+    if (e != hipSuccess) {
+        hip_status(e, "hipMemCreate");
+        return nullptr;
+    }
+    void *va = nullptr;
+    e = hipMemAddressReserve(&va, bytes, kGran, nullptr, 0);
+    if (e == hipSuccess) {
+        e = hipMemMap(va, bytes, 0, h, 0);
+        if (e == hipSuccess) {
+            const hipMemAccessDesc d = rw_access(device);
+            e = hipMemSetAccess(va, bytes, &d, 1);
+            if (e != hipSuccess) {
+                (void)hipMemUnmap(va, bytes);
+            }
+        }
+        if (e != hipSuccess) {
+            (void)hipMemAddressFree(va, bytes);
+        }
+    }
+    if (e != hipSuccess) {
+        (void)hipMemRelease(h);
+        hip_status(e, "shareable allocation (reserve / map / access)");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    g_allocs[va] = own_alloc{KIND_VMM, device, bytes, h, 0};
+    note_event('V', va, va, bytes, 0);
+    return va;
+}
+
+int ucg_builtin_dev_is_shareable(const void *ptr)
+{
+    std::lock_guard<std::mutex> g(g_mu);
+    for (const auto &kv : g_allocs) {
+        const char *b = static_cast<const char*>(kv.first);
+        if (kv.second.kind == KIND_VMM && (const char*)ptr >= b && (const char*)ptr < b + kv.second.bytes) {
+            return 1;
+        }
+    }
+    return 0;
+}
+
+void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
+{
+    if (ptr == nullptr) {
+        return;
+    }
+    own_alloc a;
+    bool own = false;
+    int fd = -1;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto it = g_allocs.find(ptr);
+        if (it != g_allocs.end()) {
+            a = it->second;
+            own = true;
+            g_allocs.erase(it);
+        }
+        /* retire its key: a peer's import of it is refused from now on */
+        auto ex = g_export_of.find(ptr);
+        if (ex != g_export_of.end()) {
+            fd = g_exports[ex->second].fd;
+            g_exports.erase(ex->second);
+            g_export_of.erase(ex);
+        }
+    }
+    if (fd >= 0) {
+        close(fd);
+    }
+    if (ctx) {
+        (void)hipSetDevice(dev_ctx_device(ctx));
+    }
+    hipError_t e;
+    if (own && a.kind == KIND_VMM) {
+        /* as hipFree does: nothing queued may still use it. Peers that mapped
+         * it keep the physical memory until they release their mapping. */
+        (void)hipSetDevice(a.device);
+        e = hipDeviceSynchronize();
+        (void)hipMemUnmap(ptr, a.bytes);
+        (void)hipMemAddressFree(ptr, a.bytes);
+        (void)hipMemRelease(a.handle);
+    } else {
+        e = hipFree(ptr);
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    note_event('F', ptr, ptr, own ? a.bytes : 0, (int)e);
+}
+
+/* torch.cuda.memory.CUDAPluggableAllocator entry points: every tensor of a
+ * process that installs them is a shareable allocation, so any tensor can be
+ * exported by its physical allocation (xucg_amd.use_shareable_torch_memory) */
+void *ucg_builtin_dev_torch_alloc(size_t bytes, int device, void *stream)
+{
+    (void)stream;
+    (void)hipSetDevice(device);
+    return ucg_builtin_dev_malloc_shareable(nullptr, bytes ? bytes : 1);
+}
+
+void ucg_builtin_dev_torch_free(void *ptr, size_t bytes, int device, void *stream)
+{
+    (void)bytes;
+    (void)stream;
+    (void)hipSetDevice(device);
+    ucg_builtin_dev_free(nullptr, ptr);        /* synchronises the device first */
+}
+
+/* Diagnostics for a buffer found corrupted (tests/_worker_topo.py): what the
+ * runtime says about the address now, whether it lies in a live allocation or
+ * an import of this shim, and the recorded memory events whose range comes
+ * within 4 MiB of it, oldest first. */
+size_t ucg_builtin_dev_debug_ptr(ucg_builtin_dev_ctx_t *ctx, const void *ptr, char *out,
+                                 size_t max)
+{
+    std::string t;
+    char line[256];
+    if (ctx) {
+        (void)hipSetDevice(dev_ctx_device(ctx));
+    }
+    hipDeviceptr_t base = nullptr;
+    size_t size = 0;
+    const hipError_t e = hipMemGetAddressRange(&base, &size, (hipDeviceptr_t)ptr);
+    snprintf(line, sizeof(line), "address %p: runtime range %s base %p size %zu\n", ptr,
+             e == hipSuccess ? "ok" : hipGetErrorString(e), (void*)base, size);
+    t += line;
+    (void)hipGetLastError();
+    hipPointerAttribute_t at;
+    memset(&at, 0, sizeof(at));
+    const hipError_t ea = hipPointerGetAttributes(&at, ptr);
+    snprintf(line, sizeof(line), "attributes %s: type %d device %d devptr %p\n",
+             ea == hipSuccess ? "ok" : hipGetErrorString(ea), (int)at.type, at.device,
+             at.devicePointer);
+    t += line;
+    (void)hipGetLastError();
+    const uintptr_t a = (uintptr_t)ptr, win = (uintptr_t)4 << 20;
+    std::lock_guard<std::mutex> g(g_mu);
+    for (const auto &kv : g_allocs) {
+        const uintptr_t p = (uintptr_t)kv.first;
+        if (a >= p && a < p + kv.second.bytes) {
+            snprintf(line, sizeof(line), "own allocation %p + %zu %s key %llu\n", kv.first,
+                     kv.second.bytes, kv.second.kind == KIND_VMM ? "shareable" : "plain",
+                     (unsigned long long)kv.second.key_id);
+            t += line;
+        }
+    }
+    for (const auto &kv : g_imports) {
+        const uintptr_t p = (uintptr_t)kv.second.base;
+        if (a >= p && a < p + kv.second.size) {
+            snprintf(line, sizeof(line), "import of pid %u key %llu mapped at %p + %zu (%s)\n",
+                     std::get<0>(kv.first), (unsigned long long)std::get<2>(kv.first),
+                     (void*)kv.second.base, kv.second.size,
+                     kv.second.kind == KIND_VMM ? "shareable" :
+                     kv.second.kind == KIND_PLAIN ? "hipIpc" : "own");
+            t += line;
+        }
+    }
+    const uint64_t first = g_nevents > kMemEvents ? g_nevents - kMemEvents : 0;
+    const uint64_t now = now_ns();
+    for (uint64_t i = first; i < g_nevents; i++) {
+        const mem_event &ev = g_events[i % kMemEvents];
+        const uintptr_t lo = (uintptr_t)(ev.base ? ev.base : ev.ptr);
+        if (lo + win > a && lo < a + win) {
+            snprintf(line, sizeof(line), "event #%llu %c ptr %p base %p bytes %zu rc %d, %.3f ms ago\n",
+                     (unsigned long long)i, ev.kind, ev.ptr, ev.base, ev.bytes, ev.rc,
+                     (double)(now - ev.ns) * 1e-6);
+            t += line;
+        }
+    }
+    if (out && max) {
+        const size_t n = t.size() < max - 1 ? t.size() : max - 1;
+        memcpy(out, t.data(), n);
+        out[n] = '\0';
+    }
+    return t.size();
+}

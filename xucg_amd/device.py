@@ -47,14 +47,17 @@ def device_count():
 
 
 class DevBuffer:
-    """A hipMalloc'ed buffer owned by a DevContext."""
+    """A device buffer owned by a DevContext: hipMalloc'ed, or (shareable)
+    HIP virtual memory that peers map by its physical allocation."""
 
-    def __init__(self, ctx, nbytes):
+    def __init__(self, ctx, nbytes, shareable=False):
         self.ctx = ctx
         self.nbytes = nbytes
-        self.ptr = _lib.dev().ucg_builtin_dev_malloc(ctx.handle, nbytes)
+        fn = (_lib.dev().ucg_builtin_dev_malloc_shareable if shareable
+              else _lib.dev().ucg_builtin_dev_malloc)
+        self.ptr = fn(ctx.handle, nbytes)
         if not self.ptr:
-            raise MemoryError(f"hipMalloc({nbytes}) failed: {_lib.last_error()}")
+            raise MemoryError(f"device allocation of {nbytes} B failed: {_lib.last_error()}")
 
     def offset(self, nbytes):
         return self.ptr + nbytes
@@ -175,8 +178,8 @@ class DevContext:
         check(_lib.dev().ucg_builtin_dev_sync(self.handle), "ucg_builtin_dev_sync")
 
     # -- memory -----------------------------------------------------------
-    def alloc(self, nbytes):
-        return DevBuffer(self, nbytes)
+    def alloc(self, nbytes, shareable=False):
+        return DevBuffer(self, nbytes, shareable)
 
     def debug_ptr(self, ptr):
         """what the runtime and the shim know about a device address, and the
@@ -284,3 +287,18 @@ class DevContext:
         _lib.dev().ucg_builtin_dev_counters(self.handle, out)
         return {"launches": out[0], "combined_bytes": out[1], "h2d_bytes": out[2],
                 "d2h_bytes": out[3], "zcopy_bytes": out[4], "signal_waits": out[5]}
+
+
+def use_shareable_torch_memory():
+    """Route torch's device allocations through the shim's shareable
+    allocator (torch.cuda.memory.CUDAPluggableAllocator over
+    ucg_builtin_dev_torch_alloc / _free), so that every tensor of this process
+    can be exported by its physical allocation (ucg_builtin_dev_ipc_export).
+    Must run before torch allocates any device memory in the process; it
+    replaces torch's caching allocator (every allocation is a VMM mapping of
+    whole 2 MiB granules, every free waits for the device)."""
+    import torch
+    _lib.dev()                       # built, and loaded after torch's HIP runtime
+    alloc = torch.cuda.memory.CUDAPluggableAllocator(
+        _lib.DEV_LIB, "ucg_builtin_dev_torch_alloc", "ucg_builtin_dev_torch_free")
+    torch.cuda.memory.change_current_allocator(alloc)
