@@ -135,9 +135,13 @@ typedef struct ucg_builtin_lgroup_params {
     unsigned       tree_radix;
     unsigned       sock_thresh;
     unsigned       recursive_factor;
+    int            mem_reg_opt_cnt;   /* BUILTIN_MEM_REG_OPT_CNT (builtin.c:49-50):
+                                         0 = UCX_BUILTIN_MEM_REG_OPT_CNT (10),
+                                         > 0 = that many starts, < 0 = never */
 } ucg_builtin_lgroup_params_t;
 
-/* group_id must be non-zero (builtin_control.c:645); `combine` is the
+/* group_id must be non-zero (builtin_control.c:645 asserts it; the plan
+ * component maps a caller's group id 0 to an internal one); `combine` is the
  * per-group combine state and stays owned by the caller. */
 ucs_status_t ucg_builtin_lgroup_create(ucg_builtin_shm_iface_t *iface,
                                        uint16_t group_id, unsigned member_count,

@@ -76,7 +76,7 @@ int main(int argc, char **argv)
     unsigned r;
     int i, ok, placed;
     uint8_t dist[UCG_BUILTIN_OPS_MAX_MEMBERS];
-    ucg_builtin_lgroup_params_t gp = {NULL, 0, 0, 0};
+    ucg_builtin_lgroup_params_t gp = {NULL, 0, 0, 0, 0};
     double t0, us;
     const int devbufs = getenv("C1_DEVICE_BUFFERS") != NULL;
     ucg_builtin_dev_ctx_t *dev = NULL;

@@ -143,6 +143,25 @@ def test_async_resend_timer_combines_on_its_thread():
     assert stats["timer_resends"] > 0 and stats["timer_combines"] > 0
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["staged", "device"])
+def test_async_resend_timer_device_combines(mode):
+    """Row a15 on the GPU: the resend timer's thread makes
+    the combine's HIP calls. staged: host buffers with every step staged on
+    the device, so the fragments the timer thread drains are device combines
+    (ucg_builtin_dev_combine, stage_end); device: device buffers, remote-key
+    steps, member 0's fold launched from its timer thread once its stuck
+    messages go out. Results bit-exact, no host combine, no device error."""
+    exe = os.path.join(ROOT, "tests", "c", "_build", "async_resend")
+    codes, outs = launch_exe(exe, 2, (shm_name(), mode), timeout=90)
+    assert codes == [0, 0], "\n".join(outs)
+    import json
+    stats = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][0])
+    assert stats["mode"] == mode
+    assert stats["timer_resends"] > 0 and stats["timer_combines"] > 0, stats
+    assert stats["host_calls"] == 0 and stats["device_calls"] > 0, stats
+
+
 @pytest.mark.parametrize("exe,world,args", [("component_test", 4, ("host",)),
                                              ("component_test", 3, ("host",)),
                                              ("async_resend", 2, None)])
@@ -522,3 +541,59 @@ def test_association_traced_against_reference_text(world, kind, keys, transport)
         # host master's (recursive over masters), start by start
         src = 0 if one_tree else (r - r % ppn if ppn < world else r)
         assert rows[r] == rows[src], (r, src, rows)
+
+
+def _stamped_object(name, owner, size=1 << 16):
+    """/dev/shm/<name> with the iface header of a set-up object (builtin_shm.c
+    seg_hdr_t: stamp at byte 64, then owner pid, instance, bytes, members)"""
+    import struct
+    path = "/dev/shm/" + name
+    with open(path, "wb") as f:
+        f.write(b"\0" * size)
+        f.seek(64)
+        f.write(struct.pack("<QQQQQ", 0x58554347534d3031, owner, 0x1234, size, 1))
+    return path
+
+
+def test_shm_iface_replaces_a_dead_jobs_object():
+    """an object left by a crashed job (its creator's pid is
+    gone) is unlinked and made anew by member 0, not shared."""
+    import subprocess
+    from xucg_amd import ops
+    dead = subprocess.Popen(["true"])
+    dead.wait()
+    name = shm_name()
+    path = _stamped_object(name, dead.pid)
+    it = ops.ShmIface(name, 1, 0)
+    try:
+        import struct
+        with open(path, "rb") as f:
+            f.seek(64)
+            stamp, owner = struct.unpack("<QQ", f.read(16))
+        assert owner == os.getpid() and stamp == 0x58554347534d3031
+    finally:
+        it.close()
+    assert not os.path.exists(path)
+
+
+def test_shm_iface_refuses_a_live_jobs_object():
+    """two live jobs under one name (no job uid) no longer share
+    rings: member 0 of the second gets UCS_ERR_BUSY."""
+    import xucg_amd
+    from xucg_amd import ops
+    name = shm_name()
+    path = _stamped_object(name, os.getppid())       # a live process
+    try:
+        with pytest.raises(xucg_amd.UcsError) as e:
+            ops.ShmIface(name, 1, 0)
+        assert e.value.status == -15
+    finally:
+        os.unlink(path)
+
+
+def test_shm_iface_reopened_at_once_by_every_member():
+    """Close and reopen of one name in a loop by 4 members: a member that
+    reopens before member 0 unlinked the closed object waits for the new
+    instance (the barrier of each instance would hang otherwise)."""
+    codes, outs = launch("_worker_reopen.py", 4, args=(shm_name(), 30), timeout=120)
+    assert codes == [0] * 4, "\n".join(outs)

@@ -253,8 +253,7 @@ static ucs_status_t ucg_builtin_create(ucg_plan_ctx_h pctx, ucg_group_ctx_h ctx,
         return UCS_ERR_INVALID_PARAM;          /* builtin.c:386-389 */
     }
     if (params->member_count == 0 || params->member_count > UCG_BUILTIN_OPS_MAX_MEMBERS ||
-        params->member_index >= params->member_count || params->id == 0 ||
-        params->distance == NULL) {
+        params->member_index >= params->member_count || params->distance == NULL) {
         return UCS_ERR_UNSUPPORTED;
     }
     memset(gctx, 0, sizeof(*gctx));
@@ -300,8 +299,14 @@ static ucs_status_t ucg_builtin_create(ucg_plan_ctx_h pctx, ucg_group_ctx_h ctx,
     lp.tree_radix       = bctx->config.tree.radix;
     lp.sock_thresh      = bctx->config.tree.sock_thresh;
     lp.recursive_factor = bctx->config.recursive.factor;
-    st = ucg_builtin_lgroup_create_ex(gctx->iface, params->id, gctx->size, gctx->my,
-                                      gctx->cmb, &lp, &gctx->lgroup);
+    /* the configured BUILTIN_MEM_REG_OPT_CNT (0: never register) */
+    lp.mem_reg_opt_cnt  = bctx->config.mem_reg_opt_cnt ? (int)bctx->config.mem_reg_opt_cnt : -1;
+    /* The wire header needs a non-zero group id (builtin_control.c:645
+     * asserts it); base/ accepts a caller's id 0 (ucg_group.c:302-303). The
+     * group's transport object is its own (iface_name), so any non-zero
+     * internal id is unique on it. */
+    st = ucg_builtin_lgroup_create_ex(gctx->iface, params->id ? params->id : 1, gctx->size,
+                                      gctx->my, gctx->cmb, &lp, &gctx->lgroup);
     if (st != UCS_OK) {
         goto err_iface;
     }

@@ -81,6 +81,7 @@ struct ucg_builtin_shm_iface {
     size_t    seg_bytes;
     char     *seg;
     uint64_t  barrier_gen;
+    ucs_status_t open_status;  /* why ucg_builtin_shm_iface_open failed */
     /* ops layer: groups by id and messages for groups not created yet
      * (the reference's bctx->group_by_id / bctx->unexpected, builtin.c:
      * 150-205) */
@@ -214,7 +215,8 @@ struct ucg_builtin_lgroup {
     int                      timer_stop;
     double                   timer_tick;
     _Atomic uint64_t         async_resends;
-    _Atomic uint64_t         async_combines;   /* host combines on the timer thread */
+    unsigned                 mem_reg_opt_cnt; /* starts before registering, 0 = never */
+    _Atomic uint64_t         async_combines;   /* combines and folds on the timer thread */
 };
 
 struct ucg_builtin_lcoll {
@@ -325,6 +327,7 @@ enum {
 /* builtin_ops.c */
 UCG_INTERNAL size_t parse_memunits(const char *s, size_t dflt);   /* builtin_combine.c */
 UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status);
+UCG_INTERNAL int ops_on_timer_thread(void);     /* the resend timer's thread */
 UCG_INTERNAL void lcoll_notify(ucg_builtin_lcoll_t *c);
 
 /* builtin_plan.c */

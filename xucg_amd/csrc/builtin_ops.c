@@ -34,6 +34,11 @@ static void step_execute(ucg_builtin_lcoll_t *c);
 /* set on the resend timer's thread: what it combines is counted */
 static __thread int on_timer_thread;
 
+UCG_INTERNAL int ops_on_timer_thread(void)
+{
+    return on_timer_thread;
+}
+
 /* UCS_ASYNC_BLOCK / UNBLOCK of the group (recursive: completion callbacks and
  * the stash drain re-enter the engine on the same thread) */
 static inline void group_block(ucg_builtin_lgroup_t *g)
@@ -559,8 +564,9 @@ static unsigned env_uint(const char *name, unsigned dflt)
     return (e && *e) ? (unsigned)strtoul(e, NULL, 0) : dflt;
 }
 
-/* BUILTIN_MEM_REG_OPT_CNT (builtin.c:49-50), 0 = never register */
-static unsigned mem_reg_opt_cnt(void)
+/* BUILTIN_MEM_REG_OPT_CNT (builtin.c:49-50) from the environment, 0 = never
+ * register; a group's parameters override it */
+static unsigned mem_reg_opt_cnt_env(void)
 {
     static unsigned v = (unsigned)-1;
     if (v == (unsigned)-1) {
@@ -636,6 +642,9 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
                      env_uint("UCX_BUILTIN_TREE_SOCKET_LEVEL_PPN_THRESH", 16);
     g->factor      = (params && params->recursive_factor) ? params->recursive_factor :
                      env_uint("UCX_BUILTIN_RECURSIVE_FACTOR", 2);
+    g->mem_reg_opt_cnt = (params && params->mem_reg_opt_cnt) ?
+                         (params->mem_reg_opt_cnt < 0 ? 0u : (unsigned)params->mem_reg_opt_cnt) :
+                         mem_reg_opt_cnt_env();
     iface->groups[group_id % UNEXP_GROUPS] = g;
     /* adopt messages that arrived before the group existed (builtin.c:
      * 424-446) */
@@ -1035,7 +1044,7 @@ static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id)
      * its recv buffer is registered, so that every later step's H2D and D2H
      * of it move by DMA */
     if (c->staged_dev && !c->rbuf_reg && c->length &&
-        ++c->dev_starts == mem_reg_opt_cnt() &&
+        ++c->dev_starts == g->mem_reg_opt_cnt &&
         ucg_builtin_dev_mem_kind(c->rbuf) == UCG_DEV_MEM_HOST &&
         ucg_builtin_combine_mem_reg(g->cmb, c->rbuf, c->length) == UCS_OK) {
         c->rbuf_reg = 1;

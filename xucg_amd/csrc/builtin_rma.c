@@ -377,6 +377,9 @@ static ucs_status_t rma_fold(ucg_builtin_lcoll_t *c, void *dst, const void *cons
 {
     unsigned m;
     ucs_status_t st = UCS_OK;
+    if (ops_on_timer_thread()) {
+        c->g->async_combines++;         /* a15: the fold on the resend timer */
+    }
     if (c->rma == RMA_DEV) {
         const double t0 = now_s();
         rma_trace(c, "fold", dst, c->length, srcs, n);
@@ -491,7 +494,13 @@ static int rma_receive(ucg_builtin_lcoll_t *c, const op_step_t *s)
     void *dst;
     ucs_status_t st;
 
-    if (c->rdy_cnt[k] < s->recv_cnt) {
+    /* the receive half starts once this member's messages are out: the
+     * reference's step sends all it has before draining what came in
+     * (ucg_builtin_step_execute, then check_pending: builtin_data.c:584-668,
+     * builtin_comp_step.inl:403-462). Sends stopped at UCS_ERR_NO_RESOURCE
+     * resume from progress or from the resend timer (builtin.c:260-294),
+     * which then folds on its own thread. */
+    if (c->rdy_cnt[k] < s->recv_cnt || c->send_pending) {
         return 0;
     }
     if (c->cur_buf == 2) {
@@ -609,6 +618,9 @@ static ucs_status_t rma_butterfly(ucg_builtin_lcoll_t *c, void *dst, const void 
     const void *val[16];
     unsigned h, m;
     ucs_status_t st = UCS_OK;
+    if (ops_on_timer_thread()) {
+        c->g->async_combines++;
+    }
     if (c->rma == RMA_DEV) {
         const double t0 = now_s();
         rma_trace(c, "butterfly", dst, bytes, srcs, N);
@@ -725,8 +737,8 @@ static int oneshot_receive(ucg_builtin_lcoll_t *c, unsigned phase)
     size_t lo, n, full_lo, full_n;
     unsigned r, k, i;
 
-    if (c->rdy_cnt[phase] < N - 1) {
-        return 0;
+    if (c->rdy_cnt[phase] < N - 1 || c->send_pending) {
+        return 0;                       /* see rma_receive */
     }
     peer[my] = rma_local(c, oneshot_buf(c, phase));
     for (i = 0; i < N - 1; i++) {

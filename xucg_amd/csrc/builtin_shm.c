@@ -8,8 +8,10 @@
 #define _GNU_SOURCE
 #include "builtin_int.h"
 
+#include <errno.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
 #include <stdio.h>
 #include <string.h>
 #include <sys/mman.h>
@@ -39,14 +41,194 @@ static incast_cell_t *incast_cell(ucg_builtin_shm_iface_t *it, unsigned member,
                             (size_t)idx * it->incast_cell_size);
 }
 
+/* The object's header (the first SEG_CTL_BYTES): the barrier counter at 0,
+ * then who made it. Member 0 creates the object (O_EXCL) and stamps it with
+ * its pid and a random instance; the others map it once it is stamped by a
+ * live creator and the name still refers to that instance. An object left
+ * behind by a dead creator (a crashed job) is unlinked and made anew; one
+ * whose creator is alive belongs to another job with the same name and is
+ * refused (UCS_ERR_BUSY: set a job uid). Closing marks the object closed
+ * before the last barrier, so a member that reopens the name at once waits
+ * for the next instance. ADVICE r03: two jobs without a job uid, or a new job
+ * over a crashed one's object, shared rings and the barrier counter. */
+typedef struct {
+    _Atomic uint64_t arrive;            /* ucg_builtin_shm_barrier */
+    uint64_t         pad[7];
+    _Atomic uint64_t stamp;             /* SHM_STAMP once set up, SHM_CLOSED at close */
+    uint64_t         owner;             /* the creator's pid */
+    uint64_t         instance;          /* random, per creation */
+    uint64_t         seg_bytes;
+    uint64_t         members;
+} seg_hdr_t;
+_Static_assert(sizeof(seg_hdr_t) <= SEG_CTL_BYTES, "segment header size");
+#define SHM_STAMP  0x58554347534d3031ull         /* "XUCGSM01" */
+#define SHM_CLOSED 0x58554347534d4344ull
+
+static int pid_alive(uint64_t pid)
+{
+    return pid != 0 && (kill((pid_t)pid, 0) == 0 || errno != ESRCH);
+}
+
+/* the header of the object the name refers to now (zeros if none) */
+static void peek_hdr(const char *name, seg_hdr_t *out)
+{
+    struct stat sb;
+    seg_hdr_t *h;
+    int fd = shm_open(name, O_RDONLY, 0);
+    memset(out, 0, sizeof(*out));
+    if (fd < 0) {
+        return;
+    }
+    if (fstat(fd, &sb) == 0 && (size_t)sb.st_size >= sizeof(seg_hdr_t)) {
+        h = mmap(NULL, sizeof(seg_hdr_t), PROT_READ, MAP_SHARED, fd, 0);
+        if (h != MAP_FAILED) {
+            out->stamp     = atomic_load_explicit(&h->stamp, memory_order_acquire);
+            out->owner     = h->owner;
+            out->instance  = h->instance;
+            out->seg_bytes = h->seg_bytes;
+            out->members   = h->members;
+            munmap(h, sizeof(seg_hdr_t));
+        }
+    }
+    close(fd);
+}
+
+static uint64_t random_u64(void)
+{
+    uint64_t v = 0;
+    int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+    if (fd >= 0) {
+        if (read(fd, &v, sizeof(v)) != (ssize_t)sizeof(v)) {
+            v = 0;
+        }
+        close(fd);
+    }
+    return (v ^ (uint64_t)(now_s() * 1e9) ^ ((uint64_t)getpid() << 40)) | 1;
+}
+
+/* member 0: a new object under the name */
+static int iface_create(ucg_builtin_shm_iface_t *it, double t0)
+{
+    seg_hdr_t ph;
+    int fd;
+    for (;;) {
+        fd = shm_open(it->name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd >= 0 || errno != EEXIST) {
+            break;
+        }
+        peek_hdr(it->name, &ph);
+        if (ph.stamp == SHM_STAMP && pid_alive(ph.owner)) {
+            fprintf(stderr, "ucg_builtin_shm_iface_open(%s): in use by live process %llu "
+                    "(another job with this name: set a job uid)\n", it->name,
+                    (unsigned long long)ph.owner);
+            it->open_status = UCS_ERR_BUSY;
+            return -1;
+        }
+        /* a dead creator's object, a closed one, or one never set up */
+        if (ph.stamp != 0 || now_s() - t0 > 1.0) {
+            shm_unlink(it->name);
+        } else {
+            usleep(1000);
+        }
+    }
+    if (fd < 0 || ftruncate(fd, (off_t)it->seg_bytes) != 0) {
+        if (fd >= 0) {
+            close(fd);
+            shm_unlink(it->name);
+        }
+        it->open_status = UCS_ERR_IO_ERROR;
+        return -1;
+    }
+    return fd;
+}
+
+static ucs_status_t iface_map(ucg_builtin_shm_iface_t *it)
+{
+    const double t0 = now_s(), lim = wait_timeout_s();
+    struct stat stt;
+    seg_hdr_t *h, ph;
+    int fd;
+
+    for (;;) {
+        if (now_s() - t0 > lim) {
+            fprintf(stderr, "ucg_builtin_shm_iface_open(%s): no usable object after %.0f s\n",
+                    it->name, lim);
+            it->open_status = UCS_ERR_TIMED_OUT;
+            return it->open_status;
+        }
+        if (it->my == 0) {
+            fd = iface_create(it, t0);
+            if (fd < 0) {
+                return it->open_status;
+            }
+        } else {
+            fd = shm_open(it->name, O_RDWR, 0);
+            if (fd >= 0 && (fstat(fd, &stt) != 0 || (size_t)stt.st_size < it->seg_bytes)) {
+                close(fd);                          /* not sized yet */
+                fd = -1;
+            }
+            if (fd < 0) {
+                usleep(1000);                       /* member 0 has not made it yet */
+                continue;
+            }
+        }
+        it->seg = mmap(NULL, it->seg_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (it->seg == MAP_FAILED) {
+            it->seg = NULL;
+            it->open_status = UCS_ERR_NO_MEMORY;
+            return it->open_status;
+        }
+        h = (seg_hdr_t*)it->seg;
+        if (it->my == 0) {
+            /* a fresh object is zero-filled: every ring starts empty */
+            h->owner     = (uint64_t)getpid();
+            h->instance  = random_u64();
+            h->seg_bytes = it->seg_bytes;
+            h->members   = it->members;
+            atomic_store_explicit(&h->stamp, SHM_STAMP, memory_order_release);
+            return UCS_OK;
+        }
+        /* a peer: wait for the creator's stamp on this very object, unless
+         * the name moves on to another one meanwhile */
+        while (atomic_load_explicit(&h->stamp, memory_order_acquire) == 0 &&
+               now_s() - t0 <= lim) {
+            usleep(200);
+            peek_hdr(it->name, &ph);
+            if (ph.stamp == SHM_STAMP && ph.instance != h->instance) {
+                break;
+            }
+        }
+        if (atomic_load_explicit(&h->stamp, memory_order_acquire) == SHM_STAMP &&
+            pid_alive(h->owner) && h->seg_bytes == it->seg_bytes &&
+            h->members == it->members) {
+            peek_hdr(it->name, &ph);
+            if (ph.instance == h->instance) {
+                return UCS_OK;                      /* still the named object */
+            }
+        } else if (atomic_load_explicit(&h->stamp, memory_order_acquire) == SHM_STAMP &&
+                   pid_alive(h->owner)) {
+            fprintf(stderr, "ucg_builtin_shm_iface_open(%s): a live object of another "
+                    "layout (%llu members, %llu B; here %u, %zu)\n", it->name,
+                    (unsigned long long)h->members, (unsigned long long)h->seg_bytes,
+                    it->members, it->seg_bytes);
+            munmap(it->seg, it->seg_bytes);
+            it->seg = NULL;
+            it->open_status = UCS_ERR_BUSY;
+            return it->open_status;
+        }
+        munmap(it->seg, it->seg_bytes);             /* stale or closed: again */
+        it->seg = NULL;
+        usleep(1000);
+    }
+}
+
 ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
                                         unsigned my_index, size_t max_short,
                                         unsigned ring_cells,
                                         ucg_builtin_shm_iface_t **iface_p)
 {
     ucg_builtin_shm_iface_t *it;
-    int fd;
-    struct stat stt;
 
     if (name == NULL || iface_p == NULL || members == 0 ||
         members > UCG_BUILTIN_OPS_MAX_MEMBERS || my_index >= members ||
@@ -78,23 +260,10 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
     it->incast_base      = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
     it->seg_bytes        = it->incast_base + (size_t)members * it->incast_bytes;
 
-    fd = shm_open(it->name, O_CREAT | O_RDWR, 0600);
-    if (fd < 0) {
+    if (iface_map(it) != UCS_OK) {
+        ucs_status_t st = it->open_status;
         free(it);
-        return UCS_ERR_IO_ERROR;
-    }
-    /* a fresh object is zero-filled: every ring starts empty (head = tail) */
-    if (fstat(fd, &stt) != 0 ||
-        ((size_t)stt.st_size < it->seg_bytes && ftruncate(fd, it->seg_bytes) != 0)) {
-        close(fd);
-        free(it);
-        return UCS_ERR_IO_ERROR;
-    }
-    it->seg = mmap(NULL, it->seg_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    close(fd);
-    if (it->seg == MAP_FAILED) {
-        free(it);
-        return UCS_ERR_NO_MEMORY;
+        return st;
     }
     ucg_builtin_shm_barrier(it);   /* everybody mapped before any send */
     *iface_p = it;
@@ -106,6 +275,12 @@ void ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *it)
     stash_t *m;
     if (it == NULL) {
         return;
+    }
+    if (it->my == 0) {
+        /* closed before the last barrier: a member reopening the name at
+         * once waits for the next instance (iface_map) */
+        atomic_store_explicit(&((seg_hdr_t*)it->seg)->stamp, SHM_CLOSED,
+                              memory_order_release);
     }
     ucg_builtin_shm_barrier(it);
     munmap(it->seg, it->seg_bytes);
@@ -126,7 +301,7 @@ size_t ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *it)
 
 void ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
 {
-    _Atomic uint64_t *arrive = (_Atomic uint64_t*)it->seg;
+    _Atomic uint64_t *arrive = &((seg_hdr_t*)it->seg)->arrive;
     uint64_t gen = ++it->barrier_gen;
     double t0 = now_s(), lim = wait_timeout_s();
     atomic_fetch_add_explicit(arrive, 1, memory_order_acq_rel);

@@ -388,12 +388,50 @@ hipMemAccessDesc rw_access(int device)
     return d;
 }
 
+/* How hipMemImportFromShareableHandle takes a POSIX fd: as the value cast
+ * to a pointer (CUDA's convention; /opt/rocm 7.2's runtime) or as the address
+ * of an int holding it (the ROCm 7.0 runtime PyTorch bundles dereferences
+ * it: the value convention crashed there, r04c). Found on first use and
+ * remembered: the address form goes first, because the value runtime takes
+ * the address's low 32 bits as an fd number, which is never an open fd when
+ * it exceeds RLIMIT_NOFILE (so that call just fails), while passing a small
+ * fd value to the dereferencing runtime would fault. -1 unknown, 0 value,
+ * 1 address. */
+std::atomic<int> g_fd_convention{-1};
+
+hipError_t import_fd(hipMemGenericAllocationHandle_t *h, int fd)
+{
+    const hipMemAllocationHandleType t = hipMemHandleTypePosixFileDescriptor;
+    int conv = g_fd_convention.load(std::memory_order_relaxed);
+    if (conv != 0) {
+        /* an int whose address has low 32 bits far above any fd number */
+        static thread_local int box[1 << 12];
+        int *p = box;
+        while (((uint32_t)(uintptr_t)p) < (1u << 24) && p + 1 < box + (1 << 12)) {
+            p += 1024;
+        }
+        *p = fd;
+        if (((uint32_t)(uintptr_t)p) >= (1u << 24) || conv == 1) {
+            const hipError_t e = hipMemImportFromShareableHandle(h, (void*)p, t);
+            if (e == hipSuccess || conv == 1) {
+                if (e == hipSuccess) g_fd_convention.store(1, std::memory_order_relaxed);
+                return e;
+            }
+            (void)hipGetLastError();
+        }
+    }
+    const hipError_t e = hipMemImportFromShareableHandle(h, (void*)(intptr_t)fd, t);
+    if (e == hipSuccess) {
+        g_fd_convention.store(0, std::memory_order_relaxed);
+    }
+    return e;
+}
+
 /* map an imported VMM allocation (fd) at a new reservation of this process */
 ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
 {
     hipMemGenericAllocationHandle_t h;
-    HIP_TRY(hipMemImportFromShareableHandle(&h, (void*)(intptr_t)fd,
-                                            hipMemHandleTypePosixFileDescriptor));
+    HIP_TRY(import_fd(&h, fd));
     void *va = nullptr;
     hipError_t e = hipMemAddressReserve(&va, size, kGran, nullptr, 0);
     if (e == hipSuccess) {

@@ -367,7 +367,14 @@ static int do_import(const char *name, size_t mib)
         }
         double t0 = now_s();
         hipMemGenericAllocationHandle_t h;
-        CHECK(hipMemImportFromShareableHandle(&h, (void*)(intptr_t)fd,
+        /* VMM_FD_CONV=pointer: pass the address of the fd, not its value */
+        const char *conv = getenv("VMM_FD_CONV");
+        int fdv = fd;
+        int rtv = 0;
+        (void)hipRuntimeGetVersion(&rtv);
+        printf("import: runtime %d, fd convention %s\n", rtv, conv ? conv : "value");
+        CHECK(hipMemImportFromShareableHandle(&h, (conv && conv[0] == 'p') ? (void*)&fdv
+                                                  : (void*)(intptr_t)fd,
                                               hipMemHandleTypePosixFileDescriptor));
         void *va = nullptr;
         CHECK(hipMemAddressReserve(&va, m.size, gran, nullptr, 0));

@@ -26,7 +26,8 @@ class ReduceParams(ctypes.Structure):
 class GroupParams(ctypes.Structure):
     """ucg_builtin_lgroup_params_t (include/ucg_builtin_ops.h)."""
     _fields_ = [("distance", ctypes.POINTER(ctypes.c_uint8)), ("tree_radix", ctypes.c_uint),
-                ("sock_thresh", ctypes.c_uint), ("recursive_factor", ctypes.c_uint)]
+                ("sock_thresh", ctypes.c_uint), ("recursive_factor", ctypes.c_uint),
+                ("mem_reg_opt_cnt", ctypes.c_int)]
 
 
 class CombineConfig(ctypes.Structure):
