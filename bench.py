@@ -1151,6 +1151,9 @@ def collective_child():
                            "probe": detail}
         else:
             peer_memory["probe"] = detail
+    if not SHAREABLE_PEER_MEMORY[0]:
+        # the engine's registered buffers then take hipIpc keys too
+        os.environ["UCX_BUILTIN_DEV_SHAREABLE"] = "n"
     torch.cuda.set_device(local_rank)
     # the engine's waits give up after this long instead of outliving the child
     os.environ.setdefault("UCX_BUILTIN_WAIT_TIMEOUT", "30")

@@ -75,3 +75,57 @@ def test_host_library_exports_the_plan_component():
     assert name == b"builtin"
     head = (ctypes.c_void_p * 2).in_dll(lib, "ucg_plan_components_list")
     assert head[1] != ctypes.addressof(head), "component not in ucg_plan_components_list"
+
+
+def _kernel_metadata(obj):
+    """(name, vgpr_count, group_segment_fixed_size) of every gfx950 kernel in
+    a hipcc object: the .hip_fatbin section, unbundled, its AMDGPU notes"""
+    import re
+    import subprocess
+    import tempfile
+    llvm = "/opt/rocm/lib/llvm/bin"
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb"), os.path.join(d, "co")
+        subprocess.run([f"{llvm}/llvm-objcopy", f"--dump-section=.hip_fatbin={fb}", obj,
+                        os.path.join(d, "junk")], check=True, capture_output=True)
+        subprocess.run([f"{llvm}/clang-offload-bundler", "--type=o", "--unbundle",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fb}",
+                        f"--output={co}"], check=True, capture_output=True)
+        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", co], check=True,
+                               capture_output=True, text=True).stdout
+    out = []
+    for block in notes.split("\n  - .agpr_count:")[1:]:
+        name = re.search(r"\n    \.name:\s+(\S+)", block).group(1)
+        vgpr = int(re.search(r"\n    \.vgpr_count:\s+(\d+)", block).group(1))
+        lds = int(re.search(r"\n    \.group_segment_fixed_size:\s+(\d+)", block).group(1))
+        out.append((name, vgpr, lds))
+    return out
+
+
+def test_kernel_resources():
+    """Round 4: no product kernel allocates LDS, and the
+    occupancy cap of the multi-operand kernels is their register allocation:
+    every capped k_reduce_multi / k_reduce_tree (last template argument 1)
+    holds at least 168 VGPRs - at most 3 waves per SIMD, 12 per CU (a few
+    byte-wide kernels need more registers of their own) - while the uncapped
+    fp32 / fp64 SUM forms fit more. Read from the built objects' code-object
+    metadata."""
+    import glob
+    import re
+    objs = sorted(glob.glob(os.path.join(ROOT, "xucg_amd", "csrc", "_obj", "dev_inst_*.o")) +
+                  glob.glob(os.path.join(ROOT, "xucg_amd", "csrc", "_obj", "dev_combine.o")))
+    if not objs or not os.path.exists("/opt/rocm/lib/llvm/bin/clang-offload-bundler"):
+        pytest.skip("the device objects are not built here")
+    capped = uncapped = 0
+    for obj in objs:
+        for name, vgpr, lds in _kernel_metadata(obj):
+            assert lds == 0, (obj, name, lds)
+            m = re.match(r"_ZN6ucgdev1[34]k_reduce_(multi|tree)I([fd])?.*ELi([01])EEEv", name)
+            if m:
+                if m.group(3) == "1":
+                    capped += 1
+                    assert vgpr >= 168, (name, vgpr)
+                elif m.group(2):
+                    uncapped += 1
+                    assert vgpr < 168, (name, vgpr)
+    assert capped > 0 and uncapped > 0, (capped, uncapped)

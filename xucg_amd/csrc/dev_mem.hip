@@ -713,6 +713,13 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
 
 void *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
 {
+    /* UCX_BUILTIN_DEV_SHAREABLE=n: plain hipMalloc memory (hipIpc keys) where
+     * peers cannot map each other's virtual-memory allocations; read at every
+     * call, so a process can switch after probing (bench.py) */
+    const char *knob = getenv("UCX_BUILTIN_DEV_SHAREABLE");
+    if (knob && (knob[0] == 'n' || knob[0] == '0')) {
+        return ucg_builtin_dev_malloc(ctx, bytes);
+    }
     int device = 0;
     if (ctx) {
         device = dev_ctx_device(ctx);
