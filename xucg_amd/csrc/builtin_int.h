@@ -203,6 +203,8 @@ struct ucg_builtin_lgroup {
      * always names the memory it named when it was sent */
     struct rma_pool         *pool;
     unsigned                 npool;
+    void                    *arena;           /* device memory made with the group */
+    size_t                   arena_bytes, arena_used;
     struct rma_imp          *imp;
     unsigned                 nimp;
     /* the worker's async context (UCS_ASYNC_BLOCK, builtin.c:263-267, 331-335):
@@ -328,6 +330,7 @@ enum {
 UCG_INTERNAL size_t parse_memunits(const char *s, size_t dflt);   /* builtin_combine.c */
 UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status);
 UCG_INTERNAL int ops_on_timer_thread(void);     /* the resend timer's thread */
+UCG_INTERNAL void rma_group_init(ucg_builtin_lgroup_t *g);
 UCG_INTERNAL void lcoll_notify(ucg_builtin_lcoll_t *c);
 
 /* builtin_plan.c */

@@ -645,6 +645,7 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
     g->mem_reg_opt_cnt = (params && params->mem_reg_opt_cnt) ?
                          (params->mem_reg_opt_cnt < 0 ? 0u : (unsigned)params->mem_reg_opt_cnt) :
                          mem_reg_opt_cnt_env();
+    rma_group_init(g);
     iface->groups[group_id % UNEXP_GROUPS] = g;
     /* adopt messages that arrived before the group existed (builtin.c:
      * 424-446) */

@@ -58,6 +58,7 @@ struct rma_pool {
     int      kind;
     int      busy;
     int      user;            /* handed out by ucg_builtin_lgroup_mem_alloc */
+    int      in_arena;        /* carved out of the group's device arena */
     uint8_t  key[UCG_BUILTIN_DEV_IPC_HANDLE_BYTES];
 };
 
@@ -173,6 +174,21 @@ static size_t shm_key_bytes(const void *key)
     return (size_t)k.bytes;
 }
 
+/* UCX_BUILTIN_DEV_POOL_BYTES (default 32 MiB, 0 = none): the device arena
+ * made with a group that has a device, out of which its registered buffers
+ * are carved while it lasts */
+UCG_INTERNAL void rma_group_init(ucg_builtin_lgroup_t *g)
+{
+    const size_t bytes = parse_memunits(getenv("UCX_BUILTIN_DEV_POOL_BYTES"),
+                                        (size_t)32 << 20);
+    g->arena = NULL;
+    g->arena_bytes = g->arena_used = 0;
+    if (bytes && ucg_builtin_combine_has_device(g->cmb)) {
+        g->arena = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
+        g->arena_bytes = g->arena ? bytes : 0;
+    }
+}
+
 /* registered buffers come in size classes - at least 64 KiB, eight per
  * power of two (at most 12.5 % over the request) - so that ops of many
  * different sizes share buffers: pool memory is never returned before the
@@ -214,20 +230,34 @@ static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
     }
     g->pool = p;
     p = &g->pool[g->npool];
-    p->bytes = bytes;
-    p->kind  = kind;
-    p->busy  = 1;
-    p->user  = 0;
+    p->bytes    = bytes;
+    p->kind     = kind;
+    p->busy     = 1;
+    p->user     = 0;
+    p->in_arena = 0;
     if (kind == RMA_SHM) {
         p->ptr = shm_seg_alloc(bytes, p->key);
         return p->ptr ? (int)g->npool++ : -1;
     }
-    p->ptr = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
-    if (p->ptr == NULL) {
-        return -1;
+    if (g->arena && g->arena_used + bytes <= g->arena_bytes) {
+        /* from the arena made with the group: no allocation on the op path
+         * (the zeroed fresh allocations), and the peers map the
+         * whole arena once (one key, offsets) */
+        p->ptr = (char*)g->arena + g->arena_used;
+        p->in_arena = 1;
+        g->arena_used += bytes;
+    } else {
+        p->ptr = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
+        if (p->ptr == NULL) {
+            return -1;
+        }
     }
     if (ucg_builtin_combine_dev_export(g->cmb, p->ptr, p->key) != UCS_OK) {
-        ucg_builtin_combine_dev_free(g->cmb, p->ptr);
+        if (!p->in_arena) {
+            ucg_builtin_combine_dev_free(g->cmb, p->ptr);
+        } else {
+            g->arena_used -= bytes;
+        }
         return -1;
     }
     return (int)g->npool++;
@@ -290,9 +320,13 @@ UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
             memcpy(&k, g->pool[i].key, sizeof(k));
             munmap(g->pool[i].ptr, g->pool[i].bytes);
             shm_unlink(k.name);
-        } else {
+        } else if (!g->pool[i].in_arena) {
             ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
         }
+    }
+    if (g->arena) {
+        ucg_builtin_combine_dev_free(g->cmb, g->arena);
+        g->arena = NULL;
     }
     free(g->imp);
     free(g->pool);
