@@ -562,31 +562,30 @@ ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
     const int device = dev_ctx_device(ctx);
     HIP_TRY(hipSetDevice(device));
     const import_key k{b.pid, b.token, b.id};
-    {
+    const bool self = b.pid == (uint32_t)getpid() && b.token == g_token;
+    if (self) {
+        /* this process's own allocation: no mapping, but the key must still
+         * be live */
         std::lock_guard<std::mutex> g(g_mu);
+        auto ex = g_exports.find(b.id);
+        if (ex == g_exports.end()) {
+            note_event('S', nullptr, nullptr, (size_t)b.size, 0);
+            return set_error(UCS_ERR_NO_RESOURCE, "ipc_import",
+                             "stale key: the exported allocation was freed since");
+        }
         auto it = g_imports.find(k);
         if (it != g_imports.end()) {
             it->second.refs++;
-            *dev_ptr = it->second.base + b.offset;
-            g_import_ptr.emplace(*dev_ptr, k);
-            return UCS_OK;
+        } else {
+            g_imports[k] = import_rec{0, static_cast<char*>(ex->second.base),
+                                      ex->second.size, {}, 1};
         }
-        if (b.pid == (uint32_t)getpid() && b.token == g_token) {
-            /* this process's own allocation: no mapping, but the key must
-             * still be live */
-            auto ex = g_exports.find(b.id);
-            if (ex == g_exports.end()) {
-                note_event('S', nullptr, nullptr, (size_t)b.size, 0);
-                return set_error(UCS_ERR_NO_RESOURCE, "ipc_import",
-                                 "stale key: the exported allocation was freed since");
-            }
-            import_rec m = {0, static_cast<char*>(ex->second.base), ex->second.size, {}, 1};
-            g_imports[k] = m;
-            *dev_ptr = m.base + b.offset;
-            g_import_ptr.emplace(*dev_ptr, k);
-            return UCS_OK;
-        }
+        *dev_ptr = static_cast<char*>(ex->second.base) + b.offset;
+        g_import_ptr.emplace(*dev_ptr, k);
+        return UCS_OK;
     }
+    /* every import asks the exporter, so a retired key is refused even while
+     * an earlier import of it is still held here (which keeps its mapping) */
     key_reply rep;
     int fd = -1;
     ucs_status_t st = fetch_key(b, &rep, &fd);
@@ -594,6 +593,17 @@ ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
         std::lock_guard<std::mutex> g(g_mu);
         note_event('S', nullptr, nullptr, (size_t)b.size, (int)st);
         return st;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto it = g_imports.find(k);
+        if (it != g_imports.end()) {
+            if (fd >= 0) close(fd);
+            it->second.refs++;
+            *dev_ptr = it->second.base + b.offset;
+            g_import_ptr.emplace(*dev_ptr, k);
+            return UCS_OK;
+        }
     }
     if (rep.size != b.size || rep.kind != b.kind) {
         if (fd >= 0) close(fd);
