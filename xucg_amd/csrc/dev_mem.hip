@@ -458,12 +458,21 @@ ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
     return UCS_OK;
 }
 
+/* Address ranges of this shim's mappings are never given back (round 4). A
+ * range mapped again to other physical memory was read through stale
+ * translations: peers read the previous allocation's data, or zeros, through
+ * a fresh mapping of a new allocation at an old address
+ * (tools/va_reuse_probe). So an allocation or import, once
+ * unmapped, leaves its reservation behind: the process's virtual address
+ * space (128 TiB) absorbs that, physical memory goes back at once. */
+std::atomic<uint64_t> g_va_retired{0};
+
 void unmap_import(import_rec &m)
 {
     if (m.kind == KIND_VMM) {
         (void)hipMemUnmap(m.base, m.size);
-        (void)hipMemAddressFree(m.base, m.size);
         (void)hipMemRelease(m.handle);
+        g_va_retired += m.size;
     } else if (m.kind == KIND_PLAIN) {
         (void)hipIpcCloseMemHandle(m.base);
     }
@@ -825,8 +834,8 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         (void)hipSetDevice(a.device);
         e = hipDeviceSynchronize();
         (void)hipMemUnmap(ptr, a.bytes);
-        (void)hipMemAddressFree(ptr, a.bytes);
         (void)hipMemRelease(a.handle);
+        g_va_retired += a.bytes;           /* the range is never reused */
     } else {
         e = hipFree(ptr);
     }
