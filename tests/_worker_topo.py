@@ -90,10 +90,15 @@ GUARD_BYTE = 0xA5
 
 class Guarded:
     """A device buffer between two guard zones of a known pattern: a write
-    past either end of the buffer is found when it is freed."""
+    past either end of the buffer is found when it is freed. The buffer is
+    shareable memory, at an address never used before in this process: a
+    hipMalloc at a recycled address can take a DMA upload into the previous
+    allocation's pages (tools/va_reuse_probe), which is what
+    zeroed these workers' buffers in round 3. XUCG_TOPO_PLAIN=1 keeps hipMalloc."""
 
     def __init__(self, dctx, nbytes):
-        self.raw = dctx.alloc(nbytes + 2 * GUARD)
+        plain = os.environ.get("XUCG_TOPO_PLAIN") == "1"
+        self.raw = dctx.alloc(nbytes + 2 * GUARD, shareable=not plain)
         self.nbytes = nbytes
         self.ptr = self.raw.ptr + GUARD
         pat = np.full(GUARD, GUARD_BYTE, np.uint8)

@@ -473,13 +473,16 @@ def test_mem_kind(dev_ctx):
     a = np.zeros(64, np.float32)
     hb = xucg_amd.HostBuffer(4096)
     db = dev_ctx.alloc(4096)
+    sb = dev_ctx.alloc(4096, shareable=True)     # HIP virtual memory
     try:
         assert f(a.ctypes.data) == 0
         assert f(hb.ptr) == 1
         assert f(db.ptr) == 2 and f(db.ptr + 1000) == 2
+        assert f(sb.ptr) == 2 and f(sb.ptr + 1000) == 2
     finally:
         hb.free()
         db.free()
+        sb.free()
 
 
 @pytest.mark.gpu
