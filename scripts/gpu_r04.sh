@@ -1,0 +1,31 @@
+#!/bin/bash
+# Round-4 evidence on the GPU box, one step per argument, each under its own
+# time limit, stopping at the first failure:
+#   bench    the driver's command (python bench.py), then smoke()
+#   profile  rocprofv3 trace + FETCH_SIZE / WRITE_SIZE passes of bench.py and the
+#            per-launch HBM traffic (scripts/profile_round.sh, pmc_summary.py)
+#   layout   the two operand layouts under TCP UTCL1 / UTCL2 / traffic counters
+#   shift    the realigning multi-operand kernels' traffic and L2 hits
+# usage: scripts/gpu_r04.sh TAG step...
+set -u
+TAG=$1; shift
+OUT=gpurun_out/$TAG
+mkdir -p $OUT
+for s in "$@"; do
+  echo "step $s $(date +%T)" >> $OUT/steps.log
+  case $s in
+  bench)
+    timeout -k 10 500 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
+    timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { tail -5 $OUT/smoke.log; exit 1; } ;;
+  profile)
+    bash scripts/profile_round.sh $TAG/prof > $OUT/profile.log 2>&1 || { tail -5 $OUT/profile.log; exit 1; }
+    P=$OUT/prof
+    python3 scripts/pmc_summary.py $(find $P/pmc_fetch -name "*counter_collection.csv" | head -1) \
+        $(find $P/pmc_write -name "*counter_collection.csv" | head -1) $OUT/pmc_traffic.json > /dev/null 2>&1 ;;
+  layout)
+    bash scripts/layout_pmc.sh $TAG/layout > $OUT/layout.log 2>&1 || { tail -5 $OUT/layout.log; exit 1; } ;;
+  shift)
+    bash scripts/shift_pmc.sh $OUT/shift > $OUT/shift.log 2>&1 || { tail -5 $OUT/shift.log; exit 1; } ;;
+  esac
+  echo "done $s $(date +%T)" >> $OUT/steps.log
+done

@@ -12,7 +12,10 @@
  * Every form is checked bit for bit against `none`. Operands are separate
  * allocations of S bytes, fp32 SUM, "exact" values.
  *
- *   tune_cap [log2 elements per operand = 24] [rounds = 5]
+ *   tune_cap [log2 elements per operand = 24] [rounds = 5] [joint]
+ *
+ * `joint`: operands and output carved out of one allocation, back to back
+ * (bench.py's one_shot_shape layout) instead of one allocation each.
  *
  * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
  */
@@ -21,6 +24,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
@@ -161,17 +165,31 @@ int main(int argc, char **argv)
     const int rounds = argc > 2 ? atoi(argv[2]) : 5;
     const int iters  = 10;
     const size_t n = (size_t)1 << lg, nvec = n / 4;
+    const bool joint = argc > 3 && strcmp(argv[3], "joint") == 0;
     std::vector<float*> bufs(kMaxMulti);
     SrcList all;
+    float *arena = nullptr;
+    if (joint) {
+        CHECK(hipMalloc(&arena, (size_t)(kMaxMulti + 2) * n * 4));
+    }
     for (int m = 0; m < kMaxMulti; m++) {
-        CHECK(hipMalloc(&bufs[m], n * 4));
+        if (joint) {
+            bufs[m] = arena + (size_t)m * n;
+        } else {
+            CHECK(hipMalloc(&bufs[m], n * 4));
+        }
         hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
                            (void*)bufs[m], 0, 100ull + m, n);
         all.p[m] = bufs[m];
     }
     float *out, *ref;
-    CHECK(hipMalloc(&out, n * 4));
-    CHECK(hipMalloc(&ref, n * 4));
+    if (joint) {
+        out = arena + (size_t)kMaxMulti * n;
+        ref = out + n;
+    } else {
+        CHECK(hipMalloc(&out, n * 4));
+        CHECK(hipMalloc(&ref, n * 4));
+    }
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
     CHECK(hipDeviceSynchronize());
@@ -191,8 +209,9 @@ int main(int argc, char **argv)
     };
     for (int ops : {4, 8, 16}) {
         add(ops, 0, 0);
-        for (int w : {8, 12, 16, 20, 24}) {
+        for (int w : {6, 8, 10, 12, 16}) {
             for (int form : {1, 4}) {
+                if (form == 4 && (w == 6 || w == 10)) continue;   /* not a VGPR step */
                 add(ops, form, w);
             }
         }
@@ -232,8 +251,9 @@ int main(int argc, char **argv)
             c.us.push_back(1000.f * ms / iters);
         }
     }
-    printf("%zu MiB per operand, fp32 SUM, %% of 8 TB/s on (operands + 1) * S bytes, "
-           "median of %d rounds\n", n * 4 >> 20, rounds);
+    printf("%zu MiB per operand (%s), fp32 SUM, %% of 8 TB/s on (operands + 1) * S bytes, "
+           "median of %d rounds\n", n * 4 >> 20, joint ? "one allocation" : "separate allocations",
+           rounds);
     for (auto &c : cs) {
         auto v = c.us;
         std::sort(v.begin(), v.end());
