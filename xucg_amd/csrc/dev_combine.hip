@@ -220,8 +220,14 @@ static ucs_status_t ring_init(ucg_builtin_dev_ctx_t *ctx)
     const size_t total = ctx->slot_bytes * ctx->nslots;
     HIP_TRY(hipHostMalloc((void**)&ctx->h_ring, total, hipHostMallocDefault));
     HIP_TRY(hipHostGetDevicePointer((void**)&ctx->h_ring_dev, ctx->h_ring, 0));
-    HIP_TRY(hipMalloc((void**)&ctx->d_ring, total));
-    HIP_TRY(hipMalloc((void**)&ctx->d_ring2, total));
+    /* device slots at addresses never used before: the copy engine writes
+     * them, and a recycled address can take a DMA write into the previous
+     * allocation's pages (tools/va_reuse_probe) */
+    ctx->d_ring  = static_cast<char*>(ucg_builtin_dev_malloc_shareable(ctx, total));
+    ctx->d_ring2 = static_cast<char*>(ucg_builtin_dev_malloc_shareable(ctx, total));
+    if (ctx->d_ring == nullptr || ctx->d_ring2 == nullptr) {
+        return UCS_ERR_NO_MEMORY;          /* the reason is in the last error */
+    }
     ctx->slot_ev   = new hipEvent_t[ctx->nslots];
     ctx->slot_used = new bool[ctx->nslots];
     for (unsigned i = 0; i < ctx->nslots; i++) {
@@ -528,15 +534,9 @@ void ucg_builtin_dev_ctx_destroy(ucg_builtin_dev_ctx_t *ctx)
     if (ctx->h_done) {
         (void)hipHostFree(ctx->h_done);
     }
-    if (ctx->d_ring) {
-        (void)hipFree(ctx->d_ring);
-    }
-    if (ctx->d_ring2) {
-        (void)hipFree(ctx->d_ring2);
-    }
-    if (ctx->d_acc) {
-        (void)hipFree(ctx->d_acc);
-    }
+    ucg_builtin_dev_free(ctx, ctx->d_ring);
+    ucg_builtin_dev_free(ctx, ctx->d_ring2);
+    ucg_builtin_dev_free(ctx, ctx->d_acc);
     if (ctx->stream && ctx->own_stream) {
         (void)hipStreamDestroy(ctx->stream);
     }
@@ -1059,11 +1059,13 @@ ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
     }
     if (bytes > ctx->d_acc_cap) {
         HIP_TRY(hipStreamSynchronize(ctx->stream));
-        if (ctx->d_acc) {
-            HIP_TRY(hipFree(ctx->d_acc));
-            ctx->d_acc = nullptr;
+        ucg_builtin_dev_free(ctx, ctx->d_acc);     /* NULL is a no-op */
+        ctx->d_acc_cap = 0;
+        /* a fresh address, as the ring's (the H2D mirror copy writes it) */
+        ctx->d_acc = static_cast<char*>(ucg_builtin_dev_malloc_shareable(ctx, bytes));
+        if (ctx->d_acc == nullptr) {
+            return UCS_ERR_NO_MEMORY;
         }
-        HIP_TRY(hipMalloc((void**)&ctx->d_acc, bytes));
         ctx->d_acc_cap = bytes;
     }
     ctx->acc = ctx->d_acc;
