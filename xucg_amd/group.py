@@ -157,13 +157,16 @@ class PeerBuffers:
 
     ptrs[r] is a device pointer to member r's buffer (the local one for
     r == rank). Collective: every member must construct it together, and
-    close it together before any member frees its buffer (HIP leaves a free
-    under a live importer undefined); close() ends with a barrier for that.
-    A buffer once exported should stay allocated for the life of the process:
-    a HIP IPC key is (pid, address, size), so a buffer freed and allocated
-    again at the same address hands the peers a key that can resolve to the
-    old memory (bench.py keeps its exported tensors; the device shim parks its
-    own exported allocations)."""
+    close it together; close() ends with a barrier, after which each member
+    may free its buffer. A key names the buffer's physical allocation
+    (ucg_builtin_dev_ipc_export): memory from the shim's shareable allocator
+    (ctx.alloc(..., shareable=True), or any tensor after
+    xucg_amd.use_shareable_torch_memory()) is mapped by its file descriptor,
+    other memory by hipIpc, checked against the runtime's buffer id; a freed
+    buffer's keys are refused. Memory from torch's own caching
+    allocator recycles addresses, which this platform can serve through stale
+    translations, so bench.py keeps such exported tensors
+    allocated until its phases end."""
 
     def __init__(self, ctx, local_ptr, rank, world, dist, group=None):
         self.ctx = ctx
