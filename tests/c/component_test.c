@@ -500,7 +500,8 @@ int main(int argc, char **argv)
     memset(&grp.params, 0, sizeof(grp.params));
     grp.params.field_mask   = UCG_GROUP_PARAM_FIELD_ID | UCG_GROUP_PARAM_FIELD_MEMBER_COUNT |
                               UCG_GROUP_PARAM_FIELD_MEMBER_INDEX | UCG_GROUP_PARAM_FIELD_DISTANCES;
-    grp.params.id           = 3;
+    /* COMP_GROUP_ID: the caller's group id (base/ accepts 0, ucg_group.c:302-303) */
+    grp.params.id           = getenv("COMP_GROUP_ID") ? (ucg_group_id_t)atoi(getenv("COMP_GROUP_ID")) : 3;
     grp.params.member_count = world;
     grp.params.member_index = rank;
     grp.params.distance     = grp.distance;

@@ -54,8 +54,8 @@ def ref_exe(tmp_path_factory):
     return str(exe)
 
 
-def _run(exe, world, mode="host"):
-    codes, outs = launch_exe(exe, world, args=(mode,), timeout=120)
+def _run(exe, world, mode="host", env=None):
+    codes, outs = launch_exe(exe, world, args=(mode,), timeout=120, env_extra=env)
     assert codes == [0] * world, "\n".join(outs)
     assert all(f"rank {r}: ok" in outs[r] for r in range(world)), "\n".join(outs)
     return outs
@@ -77,6 +77,13 @@ def test_vtable_host_buffers(world):
         # component->print: the reference plan for 4 members
         assert "Planner:       builtin" in outs[0]
         assert "recursive doubling" in outs[0]
+
+
+def test_vtable_group_id_zero():
+    """a caller's group id 0 (which base/ accepts) is planned and
+    runs; the wire gets a non-zero internal id (builtin_control.c:645 needs
+    one) on the group's own transport object."""
+    _run(EXE, 2, env={"COMP_GROUP_ID": "0"})
 
 
 @pytest.mark.parametrize("world", [4, 3])
