@@ -447,6 +447,31 @@ def test_ipc_keys_name_allocations_and_retire_on_free(dev_ctx, shareable):
 
 
 @pytest.mark.gpu
+def test_shareable_allocations_never_reuse_an_address(dev_ctx):
+    """Round 4: an address mapped again to other physical memory
+    took DMA writes into the previous allocation's pages in 98 of 200 rounds
+    (tools/va_reuse_probe). The shim's shareable allocations never reuse an
+    address: 60 rounds of allocate, DMA upload, kernel read-back (copy_multi
+    into a second buffer), free - every address new, every read right."""
+    seen = set()
+    n = (6 << 20) // 4
+    out = dev_ctx.alloc(n * 4, shareable=True)
+    try:
+        for r in range(60):
+            b = dev_ctx.alloc(n * 4, shareable=True)
+            assert b.ptr not in seen, r
+            seen.add(b.ptr)
+            b.upload(np.full(n, r + 1, np.uint32))                 # DMA write
+            assert dev_ctx.copy_multi([out.ptr], [b.ptr], n * 4) == 0   # kernel read
+            dev_ctx.sync()
+            got = out.download(np.uint32, n)
+            assert (got == r + 1).all(), (r, int((got != r + 1).sum()))
+            b.free()
+    finally:
+        out.free()
+
+
+@pytest.mark.gpu
 def test_ipc_import_rejects_foreign_and_dead_keys(dev_ctx):
     """A blob that is no key, and a key whose exporter's key server is gone,
     fail loudly at import."""
