@@ -357,11 +357,14 @@ __device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, unsigned r)
  * plain path. All loads are issued before the first shuffle. Same
  * association as k_reduce_multi, so the same bits.
  */
-template <typename T, int OP, int N>
+template <typename T, int OP, int N, int CAP = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                      size_t tail)
 {
+    if constexpr (CAP) {
+        UCG_MULTI_CAP_CLOBBER();     /* A/B only (tools/tune_misalign) */
+    }
     constexpr int V    = 16 / sizeof(T);
     const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
     auto fs = [](T a, T b) { return Comb<T, OP>::apply(a, b); };

@@ -155,6 +155,9 @@ int main(int argc, char **argv)
         {"N=8 shift (product)", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_reduce_multi_shift<float, 0, 8>), dim3(gm), dim3(kReduceBlock),
                                 0, 0, dst, sl, 0u, (size_t)0, nvm, (size_t)0); }, {}},
+        {"N=8 shift, VGPR-capped", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_multi_shift<float, 0, 8, 1>), dim3(gm), dim3(kReduceBlock),
+                                0, 0, dst, sl, 0u, (size_t)0, nvm, (size_t)0); }, {}},
         {"N=8 plain misaligned (capped)", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_multi_plain_misaligned<8>), dim3(gm), dim3(kReduceBlock), 0, 0,
                                 dst, sl, nvm); }, {}},
@@ -162,16 +165,17 @@ int main(int argc, char **argv)
 
     /* bits: the misaligned forms against the product's realigning forms */
     std::vector<uint32_t> a(n), b(n);
-    for (int pair : {1, 4, 7}) {
+    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}};
+    for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, n * 4, hipMemcpyDeviceToDevice));   /* same start */
-            cs[pair + k].run();
+            cs[pr[k]].run();
             CHECK(hipDeviceSynchronize());
             CHECK(hipMemcpy(k ? b.data() : a.data(), dst, n * 4, hipMemcpyDeviceToHost));
         }
-        const size_t cmp = pair == 7 ? nm : n;
+        const size_t cmp = pr[0] == 7 ? nm : n;
         if (!std::equal(a.begin(), a.begin() + cmp, b.begin())) {
-            printf("MISMATCH %s vs %s\n", cs[pair].name.c_str(), cs[pair + 1].name.c_str());
+            printf("MISMATCH %s vs %s\n", cs[pr[0]].name.c_str(), cs[pr[1]].name.c_str());
             return 3;
         }
     }
