@@ -6,6 +6,9 @@
 #            per-launch HBM traffic (scripts/profile_round.sh, pmc_summary.py)
 #   layout   the two operand layouts under TCP UTCL1 / UTCL2 / traffic counters
 #   shift    the realigning multi-operand kernels' traffic and L2 hits
+#   suite    pytest -m gpu (test failures are recorded and the script goes
+#            on; a crash, abort or time limit stops it)
+#   ab       the occupancy-cap and misalignment A/B tools
 # usage: scripts/gpu_r04.sh TAG step...
 set -u
 TAG=$1; shift
@@ -24,6 +27,15 @@ for s in "$@"; do
         $(find $P/pmc_write -name "*counter_collection.csv" | head -1) $OUT/pmc_traffic.json > /dev/null 2>&1 ;;
   layout)
     bash scripts/layout_pmc.sh $TAG/layout > $OUT/layout.log 2>&1 || { tail -5 $OUT/layout.log; exit 1; } ;;
+  suite)
+    timeout -k 10 850 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread \
+        -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+    rc=$?; echo "pytest rc $rc" >> $OUT/steps.log
+    [ $rc -le 1 ] || exit 1 ;;
+  ab)
+    timeout -k 10 200 tools/tune_cap 24 5 joint > $OUT/tune_cap_joint.txt 2>&1 || exit 1
+    timeout -k 10 200 tools/tune_cap 24 5 > $OUT/tune_cap.txt 2>&1 || exit 1
+    timeout -k 10 120 tools/tune_misalign 5 > $OUT/tune_misalign.txt 2>&1 || exit 1 ;;
   shift)
     bash scripts/shift_pmc.sh $OUT/shift > $OUT/shift.log 2>&1 || { tail -5 $OUT/shift.log; exit 1; } ;;
   esac

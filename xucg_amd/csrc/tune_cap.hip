@@ -114,6 +114,34 @@ k_multi_vgpr(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+/* two adjacent tiles per one-wave workgroup, every load of both issued
+ * before the first combine: twice the bytes in flight per wave, half the
+ * workgroups (U = 2), optionally also VGPR-capped */
+template <int N, int CAP>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_u2(float *dst, SrcList srcs, size_t nvec)
+{
+    if constexpr (CAP) {
+        UCG_MULTI_CAP_CLOBBER();
+    }
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    const size_t i0 = (size_t)blockIdx.x * 2 * kReduceBlock + threadIdx.x;
+    const size_t i1 = i0 + kReduceBlock;
+    u32x4 a[N], b[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        const u32x4 *p = reinterpret_cast<const u32x4*>(srcs.p[m]);
+        a[m] = ld16<1>(p + (i0 < nvec ? i0 : nvec - 1));
+        b[m] = ld16<1>(p + (i1 < nvec ? i1 : nvec - 1));
+    }
+    if (i0 < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i0, rd_tree<N>(a, fv));
+    }
+    if (i1 < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i1, rd_tree<N>(b, fv));
+    }
+}
+
 template <int N>
 static void run_vgpr(int w, float *d, const SrcList &s, size_t nv, unsigned tiles, hipStream_t q)
 {
@@ -142,6 +170,14 @@ static void run(int form, int w, float *d, const SrcList &s, size_t nv, hipStrea
     }
     if (form == 4) {
         run_vgpr<N>(w, d, s, nv, tiles, q);
+        return;
+    }
+    if (form == 5 || form == 6) {
+        const unsigned g2 = (tiles + 1) / 2;
+        if (form == 5)
+            hipLaunchKernelGGL((k_multi_u2<N, 0>), dim3(g2), dim3(kReduceBlock), 0, q, d, s, nv);
+        else
+            hipLaunchKernelGGL((k_multi_u2<N, 1>), dim3(g2), dim3(kReduceBlock), 0, q, d, s, nv);
         return;
     }
     unsigned g = (unsigned)(256 * w);
@@ -194,11 +230,11 @@ int main(int argc, char **argv)
     CHECK(hipStreamCreate(&st));
     CHECK(hipDeviceSynchronize());
 
-    static const char *fname[] = {"none", "lds", "loop", "pipe", "vgpr"};
+    static const char *fname[] = {"none", "lds", "loop", "pipe", "vgpr", "u2", "u2+vgpr"};
     std::vector<Case> cs;
     auto add = [&](int ops, int form, int w) {
         char nm[64];
-        snprintf(nm, sizeof(nm), "N=%d %s W=%d", ops, fname[form], form ? w : 0);
+        snprintf(nm, sizeof(nm), "N=%d %s W=%d", ops, fname[form], w);
         std::function<void(float*, size_t, hipStream_t)> f;
         switch (ops) {
         case 4:  f = [=](float *d, size_t nv, hipStream_t q) { run<4>(form, w, d, all, nv, q); }; break;
@@ -209,6 +245,8 @@ int main(int argc, char **argv)
     };
     for (int ops : {4, 8, 16}) {
         add(ops, 0, 0);
+        add(ops, 5, 0);
+        add(ops, 6, 12);
         for (int w : {6, 8, 10, 12, 16}) {
             for (int form : {1, 4}) {
                 if (form == 4 && (w == 6 || w == 10)) continue;   /* not a VGPR step */
