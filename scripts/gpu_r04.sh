@@ -9,6 +9,8 @@
 #   suite    pytest -m gpu (test failures are recorded and the script goes
 #            on; a crash, abort or time limit stops it)
 #   ab       the occupancy-cap and misalignment A/B tools
+#   ab2      the misalignment A/B and its FETCH_SIZE pass per kernel
+#   ipc      the multi-process shareable-key tests (topology, one-shot, churn)
 # usage: scripts/gpu_r04.sh TAG step...
 set -u
 TAG=$1; shift
@@ -36,6 +38,18 @@ for s in "$@"; do
     timeout -k 10 200 tools/tune_cap 24 5 joint > $OUT/tune_cap_joint.txt 2>&1 || exit 1
     timeout -k 10 200 tools/tune_cap 24 5 > $OUT/tune_cap.txt 2>&1 || exit 1
     timeout -k 10 120 tools/tune_misalign 5 > $OUT/tune_misalign.txt 2>&1 || exit 1 ;;
+  ab2)
+    timeout -k 10 120 tools/tune_misalign 5 > $OUT/tune_misalign.txt 2>&1 || exit 1
+    export TMPDIR=/tmp
+    timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/misalign_pmc/pmc_FETCH_SIZE \
+        -o s -- tools/tune_misalign 1 > $OUT/misalign_pmc.txt 2>&1 || exit 1
+    python3 scripts/pmc_kernels.py $OUT/misalign_pmc > $OUT/misalign_pmc_by_kernel.txt 2>&1 ;;
+  ipc)
+    timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
+        -p no:cacheprovider -k "oneshot_reduce_scatter_over_ipc or engine_placements_device_buffers or ipc_keys or churn" \
+        > $OUT/pytest_ipc.log 2>&1
+    rc=$?; echo "pytest rc $rc" >> $OUT/steps.log
+    [ $rc -le 1 ] || exit 1 ;;
   shift)
     bash scripts/shift_pmc.sh $OUT/shift > $OUT/shift.log 2>&1 || { tail -5 $OUT/shift.log; exit 1; } ;;
   esac

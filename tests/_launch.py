@@ -31,6 +31,10 @@ def launch_exe(exe, world, args=(), timeout=240, python=False, env_extra=None):
     env["MASTER_PORT"] = str(port)
     env["WORLD_SIZE"] = str(world)
     env.setdefault("OMP_NUM_THREADS", "1")
+    # a worker that crashes names where: its Python stack, and the native one
+    # (xucg_amd/csrc/dev_mem.hip, XUCG_NATIVE_BACKTRACE)
+    env.setdefault("PYTHONFAULTHANDLER", "1")
+    env.setdefault("XUCG_NATIVE_BACKTRACE", "1")
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))

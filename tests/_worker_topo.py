@@ -292,7 +292,11 @@ def main():
                 st = coll.run()
                 got = back(rbuf, inputs[rank]) if rbuf is not None else None
                 if st != 0:
-                    fail(f"{kind} {dt} {op} root={root} start {rep} status={st}")
+                    why = ""
+                    if dctx is not None:
+                        from xucg_amd import _lib
+                        why = f" (device shim: {_lib.last_error()})"
+                    fail(f"{kind} {dt} {op} root={root} start {rep} status={st}{why}")
                 elif got is not None and not (O.bits(got) == O.bits(want[rank])).all():
                     bad = np.nonzero(O.bits(got) != O.bits(want[rank]))[0]
                     fail(f"{kind} {dt} {op} n={count} root={root} start {rep}: "

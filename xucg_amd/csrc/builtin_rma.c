@@ -285,6 +285,10 @@ static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
     st = (kind == RMA_SHM) ? shm_seg_import(key, ptr) :
                              ucg_builtin_combine_dev_import(g->cmb, key, ptr);
     if (st != UCS_OK) {
+        if (rma_trace_on()) {
+            fprintf(stderr, "[rma %u] import of member %u's buffer failed (%d): %s\n", g->my,
+                    peer, (int)st, kind == RMA_SHM ? "shared memory" : ucg_builtin_dev_last_error());
+        }
         return st;
     }
     if (rma_trace_on()) {

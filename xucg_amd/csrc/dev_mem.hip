@@ -30,6 +30,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <execinfo.h>
+#include <signal.h>
 #include <sys/socket.h>
 #include <sys/un.h>
 #include <fcntl.h>
@@ -391,47 +393,92 @@ hipMemAccessDesc rw_access(int device)
 /* How hipMemImportFromShareableHandle takes a POSIX fd: as the value cast
  * to a pointer (CUDA's convention; /opt/rocm 7.2's runtime) or as the address
  * of an int holding it (the ROCm 7.0 runtime PyTorch bundles dereferences
- * it: the value convention crashed there, r04c). Found on first use and
- * remembered: the address form goes first, because the value runtime takes
- * the address's low 32 bits as an fd number, which is never an open fd when
- * it exceeds RLIMIT_NOFILE (so that call just fails), while passing a small
- * fd value to the dereferencing runtime would fault. -1 unknown, 0 value,
- * 1 address. */
+ * it: the value convention crashed there, r04c). Found once per process on an
+ * allocation of its own (detect_fd_convention) and remembered. -1 unknown,
+ * 0 value, 1 address. */
 std::atomic<int> g_fd_convention{-1};
 
-hipError_t import_fd(hipMemGenericAllocationHandle_t *h, int fd)
+/* The int the address form points at. Its address's low 32 bits must be at
+ * least 2^24, far above any fd number: of two addresses 16 MiB apart one
+ * always is, so the box spans 16 MiB of untouched (unbacked) bss. */
+int g_fd_box[((16u << 20) + 64) / sizeof(int)];
+std::mutex g_fd_box_mu;
+
+int *fd_box()
+{
+    int *p = g_fd_box;
+    if ((uint32_t)(uintptr_t)p < (1u << 24)) {
+        p += (16u << 20) / sizeof(int);
+    }
+    return p;
+}
+
+/* Find the convention once, on an allocation of this process's own: an
+ * address-form import of an fd known to be good fails only on a value-form
+ * runtime, and only then is the value form tried (on that same good fd). A
+ * failing import of a peer's fd can then never send the value form to a
+ * dereferencing runtime. Caller holds g_fd_box_mu. */
+int detect_fd_convention(int device)
 {
     const hipMemAllocationHandleType t = hipMemHandleTypePosixFileDescriptor;
-    int conv = g_fd_convention.load(std::memory_order_relaxed);
-    if (conv != 0) {
-        /* an int whose address has low 32 bits far above any fd number */
-        static thread_local int box[1 << 12];
-        int *p = box;
-        while (((uint32_t)(uintptr_t)p) < (1u << 24) && p + 1 < box + (1 << 12)) {
-            p += 1024;
-        }
+    hipMemAllocationProp prop;
+    memset(&prop, 0, sizeof(prop));
+    prop.type = hipMemAllocationTypePinned;
+    prop.requestedHandleType = t;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    hipMemGenericAllocationHandle_t own, imp;
+    if (hipMemCreate(&own, kGran, &prop, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    int fd = -1, conv = -1;
+    if (hipMemExportToShareableHandle(&fd, own, t, 0) == hipSuccess && fd >= 0) {
+        int *p = fd_box();
         *p = fd;
-        if (((uint32_t)(uintptr_t)p) >= (1u << 24) || conv == 1) {
-            const hipError_t e = hipMemImportFromShareableHandle(h, (void*)p, t);
-            if (e == hipSuccess || conv == 1) {
-                if (e == hipSuccess) g_fd_convention.store(1, std::memory_order_relaxed);
-                return e;
-            }
+        if (hipMemImportFromShareableHandle(&imp, (void*)p, t) == hipSuccess) {
+            conv = 1;
+        } else {
             (void)hipGetLastError();
+            if (hipMemImportFromShareableHandle(&imp, (void*)(intptr_t)fd, t) == hipSuccess) {
+                conv = 0;
+            }
         }
+        if (conv >= 0) {
+            (void)hipMemRelease(imp);
+        }
+        close(fd);
     }
-    const hipError_t e = hipMemImportFromShareableHandle(h, (void*)(intptr_t)fd, t);
-    if (e == hipSuccess) {
-        g_fd_convention.store(0, std::memory_order_relaxed);
+    (void)hipGetLastError();
+    (void)hipMemRelease(own);
+    return conv;
+}
+
+hipError_t import_fd(hipMemGenericAllocationHandle_t *h, int fd, int device)
+{
+    const hipMemAllocationHandleType t = hipMemHandleTypePosixFileDescriptor;
+    std::lock_guard<std::mutex> g(g_fd_box_mu);
+    int conv = g_fd_convention.load(std::memory_order_relaxed);
+    if (conv < 0) {
+        conv = detect_fd_convention(device);
+        if (conv < 0) {
+            return hipErrorNotSupported;        /* no shareable memory here */
+        }
+        g_fd_convention.store(conv, std::memory_order_relaxed);
     }
-    return e;
+    if (conv == 1) {
+        int *p = fd_box();
+        *p = fd;
+        return hipMemImportFromShareableHandle(h, (void*)p, t);
+    }
+    return hipMemImportFromShareableHandle(h, (void*)(intptr_t)fd, t);
 }
 
 /* map an imported VMM allocation (fd) at a new reservation of this process */
 ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
 {
     hipMemGenericAllocationHandle_t h;
-    HIP_TRY(import_fd(&h, fd));
+    HIP_TRY(import_fd(&h, fd, device));
     void *va = nullptr;
     hipError_t e = hipMemAddressReserve(&va, size, kGran, nullptr, 0);
     if (e == hipSuccess) {
@@ -478,6 +525,43 @@ void unmap_import(import_rec &m)
     }
 }
 
+}  // namespace
+
+/* XUCG_NATIVE_BACKTRACE=1 (diagnostics, host code only): a SIGSEGV or
+ * SIGBUS prints the native stack to stderr, then the previous handler (e.g.
+ * Python's faulthandler) runs as before. Offsets into this library resolve
+ * with addr2line against the same build. */
+namespace {
+struct sigaction g_prev_segv, g_prev_bus;
+
+void native_backtrace(int sig, siginfo_t *si, void *uc)
+{
+    static const char hdr[] = "xucg: fatal signal, native stack:\n";
+    (void)!write(2, hdr, sizeof(hdr) - 1);
+    void *f[64];
+    backtrace_symbols_fd(f, backtrace(f, 64), 2);
+    const struct sigaction &prev = sig == SIGBUS ? g_prev_bus : g_prev_segv;
+    sigaction(sig, &prev, nullptr);          /* the fault repeats into it */
+    (void)si;
+    (void)uc;
+}
+
+__attribute__((constructor)) void native_backtrace_init()
+{
+    const char *e = getenv("XUCG_NATIVE_BACKTRACE");
+    if (e == nullptr || e[0] != '1') {
+        return;
+    }
+    void *f[1];
+    (void)backtrace(f, 1);                   /* load libgcc before any fault */
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = native_backtrace;
+    sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+    sigaction(SIGBUS, &sa, &g_prev_bus);
+}
 }  // namespace
 
 /* ---- peer mapping ---------------------------------------------------------- */

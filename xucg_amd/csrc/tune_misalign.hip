@@ -91,6 +91,79 @@ k_copy_plain_misaligned(u32x4 *out, const float *src, size_t nvec)
     }
 }
 
+/* The realigning forms read one 16-B vector past the wave's tile (lane 63's
+ * `ex`), the first vector of the next tile: PMC put the realigning kernels at
+ * 1.043-1.045 x the algorithmic FETCH_SIZE (r04j/shift), that line fetched
+ * twice. Candidates, all on the product's XCD tile map:
+ *   EXNT 0   `ex` as a temporal load (the tile loads stay non-temporal)
+ *   U 2      a wave realigns two adjacent tiles (128 vectors): tile 0's lane
+ *            63 takes tile 1's first vector by readfirstlane, so one extra
+ *            vector per 2 KiB instead of per 1 KiB
+ * N = 1 is the all-gather row copy, N > 1 the one-shot combine (rd_tree). */
+template <int N, int EXNT, int U, int CAP>
+__global__ void __launch_bounds__(kReduceBlock)
+k_ms(float *dst, SrcList srcs, size_t nvec)
+{
+    if constexpr (CAP) {
+        UCG_MULTI_CAP_CLOBBER();
+    }
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    const unsigned ntiles = gridDim.x;
+    const size_t base = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, ntiles) * (kReduceBlock * U);
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    u32x4 lo[U][N], ex[N];
+    unsigned r[N];
+    const u32x4 *a4[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        const char *p = reinterpret_cast<const char*>(srcs.p[m]);
+        r[m]  = (unsigned)((uintptr_t)p & 15);
+        a4[m] = reinterpret_cast<const u32x4*>(p - r[m]);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const size_t i = base + (size_t)u * kReduceBlock + threadIdx.x;
+            lo[u][m] = ld16<1>(a4[m] + (i < nvec ? i : nvec));
+        }
+        const size_t e = base + (size_t)U * kReduceBlock;
+        ex[m] = ld16<EXNT>(a4[m] + (last_lane && e <= nvec ? e : nvec));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        u32x4 val[N];
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            u32x4 hi;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                hi[k] = from_next_lane(lo[u][m][k]);
+            }
+            if (u + 1 < U) {
+                u32x4 nx;
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    nx[k] = __builtin_amdgcn_readfirstlane(lo[u + 1 < U ? u + 1 : u][m][k]);
+                }
+                if (last_lane) hi = nx;
+            } else if (last_lane) {
+                hi = ex[m];
+            }
+            val[m] = funnel16(lo[u][m], hi, r[m]);
+        }
+        const size_t i = base + (size_t)u * kReduceBlock + threadIdx.x;
+        if (i < nvec) {
+            st16<1>(reinterpret_cast<u32x4*>(dst) + i, N == 1 ? val[0] : rd_tree<N>(val, fv));
+        }
+    }
+}
+
+template <int N, int EXNT, int U, int CAP>
+static void run_ms(float *dst, const SrcList &s, size_t nvec)
+{
+    const unsigned g = (unsigned)((nvec + kReduceBlock * U - 1) / (kReduceBlock * U));
+    hipLaunchKernelGGL((k_ms<N, EXNT, U, CAP>), dim3(g), dim3(kReduceBlock), 0, 0, dst, s, nvec);
+}
+
 struct Case {
     std::string name;
     double bytes;
@@ -128,6 +201,8 @@ int main(int argc, char **argv)
                        (void*)ref, 1, 9ull, n);
     CHECK(hipDeviceSynchronize());
     const unsigned g2 = (unsigned)(nvec / kReduceBlock), gm = (unsigned)(nvm / kReduceBlock);
+    SrcList s1 = sl_al;
+    s1.p[0] = s4;
 
     std::vector<Case> cs = {
         {"2-op aligned k_reduce", 3.0 * n * 4, [&] {
@@ -161,11 +236,18 @@ int main(int argc, char **argv)
         {"N=8 plain misaligned (capped)", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_multi_plain_misaligned<8>), dim3(gm), dim3(kReduceBlock), 0, 0,
                                 dst, sl, nvm); }, {}},
+        {"copy shift, ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 1, 0>(dst, s1, nvec); }, {}},
+        {"copy shift, U=2", 2.0 * n * 4, [&] { run_ms<1, 1, 2, 0>(dst, s1, nvec); }, {}},
+        {"copy shift, U=2 ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 2, 0>(dst, s1, nvec); }, {}},
+        {"N=8 shift capped, ex temporal", 9.0 * nm * 4, [&] { run_ms<8, 0, 1, 1>(dst, sl, nvm); }, {}},
+        {"N=8 shift capped, U=2", 9.0 * nm * 4, [&] { run_ms<8, 1, 2, 1>(dst, sl, nvm); }, {}},
+        {"N=8 shift capped, U=2 ex temporal", 9.0 * nm * 4, [&] { run_ms<8, 0, 2, 1>(dst, sl, nvm); }, {}},
     };
 
     /* bits: the misaligned forms against the product's realigning forms */
     std::vector<uint32_t> a(n), b(n);
-    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}};
+    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {4, 10}, {4, 11}, {4, 12},
+                            {7, 13}, {7, 14}, {7, 15}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, n * 4, hipMemcpyDeviceToDevice));   /* same start */
@@ -173,7 +255,7 @@ int main(int argc, char **argv)
             CHECK(hipDeviceSynchronize());
             CHECK(hipMemcpy(k ? b.data() : a.data(), dst, n * 4, hipMemcpyDeviceToHost));
         }
-        const size_t cmp = pr[0] == 7 ? nm : n;
+        const size_t cmp = pr[0] == 7 ? nm : n;   /* N = 8 writes nm elements */
         if (!std::equal(a.begin(), a.begin() + cmp, b.begin())) {
             printf("MISMATCH %s vs %s\n", cs[pr[0]].name.c_str(), cs[pr[1]].name.c_str());
             return 3;
