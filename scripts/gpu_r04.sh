@@ -31,7 +31,7 @@ for s in "$@"; do
     bash scripts/layout_pmc.sh $TAG/layout > $OUT/layout.log 2>&1 || { tail -5 $OUT/layout.log; exit 1; } ;;
   suite)
     timeout -k 10 850 python -u -m pytest tests -m gpu -v --timeout 400 --timeout-method thread \
-        -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+        -p no:cacheprovider --durations=25 > $OUT/pytest_gpu.log 2>&1
     rc=$?; echo "pytest rc $rc" >> $OUT/steps.log
     [ $rc -le 1 ] || exit 1 ;;
   ab)

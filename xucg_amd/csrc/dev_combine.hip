@@ -729,7 +729,7 @@ __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbyt
         const u32x4 *a4      = reinterpret_cast<const u32x4*>(sp - rs);
         const bool last_lane = threadIdx.x == kReduceBlock - 1;
         const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
-        const u32x4 ex = ld16<1>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
+        const u32x4 ex = ld16<0>(a4 + (last_lane && i < nvec ? i + 1 : nvec));  /* temporal */
         u32x4 hi;
 #pragma unroll
         for (int k = 0; k < 4; k++) {

@@ -91,7 +91,9 @@ __device__ __forceinline__ u32x4 vapply(u32x4 s, u32x4 d)
  * XCD, and is fetched into two L2s: PMC shows 1/16 more FETCH_SIZE than the
  * aligned kernel, and the kernel ran 4 points slower. Here XCD x takes chunks
  * of kXcdChunk consecutive tiles, so the neighbouring tile is processed on
- * the same XCD one workgroup earlier or later and the line is an L2 hit.
+ * the same XCD one workgroup earlier or later and the line is an L2 hit -
+ * provided that extra load is temporal: issued non-temporally it still
+ * fetched 1.04-1.12 x the algorithmic bytes (round 4, profiles/r04/r04k).
  * A bijection on [0, ntiles): whole rounds of 8 are remapped, a ragged last
  * round keeps the identity. */
 constexpr unsigned kXcdChunk = 64;
@@ -212,7 +214,10 @@ k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
      * serialising them) and store nothing */
     const u32x4 b  = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
     const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
-    const u32x4 ex = ld16<1>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
+    /* temporal: that vector is the next tile's first, which its own wave
+     * loads non-temporally; a non-temporal load here could evict the line
+     * before the neighbour's load and fetch it from HBM twice */
+    const u32x4 ex = ld16<0>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
     __builtin_amdgcn_sched_barrier(0);  /* keep the shuffles behind all loads */
     /* A[i + 1]: the next lane's load; lane 63 loaded it itself */
     u32x4 hi;
@@ -363,7 +368,7 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
                      size_t tail)
 {
     if constexpr (CAP) {
-        UCG_MULTI_CAP_CLOBBER();     /* A/B only (tools/tune_misalign) */
+        UCG_MULTI_CAP_CLOBBER();
     }
     constexpr int V    = 16 / sizeof(T);
     const size_t gtid  = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
@@ -410,7 +415,7 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
          * k_reduce_shift); an out-of-phase operand also needs A[nvec] */
         const size_t lim = nvec - (r[m] == 0);
         val[m] = ld16<1>(a4[m] + (i < lim ? i : lim));
-        ex[m]  = ld16<1>(a4[m] + (last_lane && i < lim ? i + 1 : lim));
+        ex[m]  = ld16<0>(a4[m] + (last_lane && i < lim ? i + 1 : lim));   /* temporal */
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -500,10 +505,13 @@ k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t
  * k_reduce_tree's (acc = srcs[m] (op) acc, m = 1 .. n-1), so the same bits.
  * Operands past n load srcs[0] again and are not combined.
  */
-template <typename T, int OP, int NMAX>
+template <typename T, int OP, int NMAX, int CAP = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_tree_shift(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
 {
+    if constexpr (CAP) {
+        UCG_MULTI_CAP_CLOBBER();
+    }
     constexpr int V   = 16 / sizeof(T);
     const size_t gtid = (size_t)blockIdx.x * kReduceBlock + threadIdx.x;
 
@@ -544,7 +552,7 @@ k_reduce_tree_shift(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, 
         a4[m] = reinterpret_cast<const u32x4*>(p - r[m]);
         const size_t lim = nvec - (r[m] == 0);
         val[m] = ld16<1>(a4[m] + (i < lim ? i : lim));
-        ex[m]  = ld16<1>(a4[m] + (last_lane && i < lim ? i + 1 : lim));
+        ex[m]  = ld16<0>(a4[m] + (last_lane && i < lim ? i + 1 : lim));   /* temporal */
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll

@@ -190,8 +190,9 @@ reduce_row(std::integer_sequence<int, OPS...>)
 typedef hipError_t (*multi_fn_t)(void *dst, const SrcList &srcs, unsigned n,
                                  unsigned self, size_t count, hipStream_t st);
 
-/* Occupancy cap of the multi-operand kernels (kMultiCap, dev_kernels.h):
- * with 4 or more operands the aligned forms run capped. The uncapped forms
+/* Occupancy cap of the multi-operand kernels (UCG_MULTI_CAP_CLOBBER,
+ * dev_kernels.h): with 4 or more operands (tree: NMAX 8 or 16) the aligned
+ * and the realigning forms run capped. The uncapped forms
  * are also built for fp32 and fp64 SUM, for A/B runs in one process
  * (ucg_builtin_dev_set_multi_cap(0): bench.py's one-shot reduce-scatter over
  * xGMI); every other pair always runs capped. */
@@ -254,15 +255,20 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
                                        d + off, sl, self, h, chunk, t);
             }
         } else {
-            /* some operand out of phase with dst: realigned in registers
-             * (uncapped: the realigning form lost 2-4 points under a cap on
-             * two boxes, profiles/r03/shift2) */
+            /* some operand out of phase with dst: realigned in registers,
+             * capped as the aligned form (round 4: with its next-tile loads
+             * temporal, 84.8 % capped against 78.1 % uncapped) */
             size_t items = chunk;
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
-            hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N>), dim3(grid), dim3(kReduceBlock),
-                               0, st, d + off, sl, self, h, chunk, t);
+            if (cap) {
+                hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N, can_cap>), dim3(grid),
+                                   dim3(kReduceBlock), 0, st, d + off, sl, self, h, chunk, t);
+            } else if constexpr (!can_cap || uncapped_ab<T, OP>()) {
+                hipLaunchKernelGGL((k_reduce_multi_shift<T, OP, N, 0>), dim3(grid),
+                                   dim3(kReduceBlock), 0, st, d + off, sl, self, h, chunk, t);
+            }
         }
         done += chunk;
     } while (done < nvec);
@@ -366,9 +372,14 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, kReduceBlock, 0x7fffffff);
-            /* uncapped, as k_reduce_multi_shift */
-            hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX>), dim3(grid),
-                               dim3(kReduceBlock), 0, st, d + off, sl, n, h, chunk, t);
+            /* capped as k_reduce_multi_shift */
+            if (cap) {
+                hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX, can_cap>), dim3(grid),
+                                   dim3(kReduceBlock), 0, st, d + off, sl, n, h, chunk, t);
+            } else if constexpr (!can_cap || uncapped_ab<T, OP>()) {
+                hipLaunchKernelGGL((k_reduce_tree_shift<T, OP, NMAX, 0>), dim3(grid),
+                                   dim3(kReduceBlock), 0, st, d + off, sl, n, h, chunk, t);
+            }
         }
         done += chunk;
     } while (done < nvec);
