@@ -164,6 +164,47 @@ static void run_ms(float *dst, const SrcList &s, size_t nvec)
     hipLaunchKernelGGL((k_ms<N, EXNT, U, CAP>), dim3(g), dim3(kReduceBlock), 0, 0, dst, s, nvec);
 }
 
+/* The all-gather of 8 rows whose sources are all 4 B out of dst's phase
+ * (k_gather_multi's case). The product deals workgroups round-robin over the
+ * rows (MAP 0: row = b % 8, tile = b / 8, so row r runs on XCD r); MAP 1
+ * walks the rows one after another on the XCD tile map of k_ms (a row's
+ * tiles in runs of 64 per XCD). Both realign as k_ms<1, EXNT, 1>. PMC put
+ * the product at 1.047 x the algorithmic FETCH_SIZE with either ex policy
+ * (r04j, r04l), against 1.002 x for the one-source copy with a temporal ex. */
+template <int EXNT, int MAP>
+__global__ void __launch_bounds__(kReduceBlock)
+k_gather_ms(char *dst, SrcList srcs, size_t row_bytes, size_t nvec)
+{
+    const unsigned tpr = (unsigned)((nvec + kReduceBlock - 1) / kReduceBlock);
+    unsigned r, t;
+    if (MAP == 0) {
+        r = blockIdx.x % 8;
+        t = blockIdx.x / 8;
+    } else {
+        const unsigned g = xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x);
+        r = g / tpr;
+        t = g % tpr;
+    }
+    const char *p = static_cast<const char*>(srcs.p[r]);
+    const unsigned rs = (unsigned)((uintptr_t)p & 15);
+    const u32x4 *a4 = reinterpret_cast<const u32x4*>(p - rs);
+    const size_t i = (size_t)t * kReduceBlock + threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
+    const u32x4 ex = ld16<EXNT>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
+    u32x4 hi;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        hi[k] = from_next_lane(lo[k]);
+    }
+    if (last_lane) {
+        hi = ex;
+    }
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst + (size_t)r * row_bytes) + i, funnel16(lo, hi, rs));
+    }
+}
+
 struct Case {
     std::string name;
     double bytes;
@@ -236,6 +277,15 @@ int main(int argc, char **argv)
         {"N=8 plain misaligned (capped)", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_multi_plain_misaligned<8>), dim3(gm), dim3(kReduceBlock), 0, 0,
                                 dst, sl, nvm); }, {}},
+        {"gather 8 rows, round-robin, ex nt", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<1, 0>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, ex temporal", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<0, 0>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows, XCD map, ex temporal", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<0, 1>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
         {"copy shift, ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 1, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2", 2.0 * n * 4, [&] { run_ms<1, 1, 2, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2 ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 2, 0>(dst, s1, nvec); }, {}},
@@ -246,8 +296,8 @@ int main(int argc, char **argv)
 
     /* bits: the misaligned forms against the product's realigning forms */
     std::vector<uint32_t> a(n), b(n);
-    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {4, 10}, {4, 11}, {4, 12},
-                            {7, 13}, {7, 14}, {7, 15}};
+    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {4, 13},
+                            {4, 14}, {4, 15}, {7, 16}, {7, 17}, {7, 18}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, n * 4, hipMemcpyDeviceToDevice));   /* same start */
@@ -255,7 +305,7 @@ int main(int argc, char **argv)
             CHECK(hipDeviceSynchronize());
             CHECK(hipMemcpy(k ? b.data() : a.data(), dst, n * 4, hipMemcpyDeviceToHost));
         }
-        const size_t cmp = pr[0] == 7 ? nm : n;   /* N = 8 writes nm elements */
+        const size_t cmp = pr[0] == 7 ? nm : n;   /* N = 8 writes nm elements, a gather 8 nm = n */
         if (!std::equal(a.begin(), a.begin() + cmp, b.begin())) {
             printf("MISMATCH %s vs %s\n", cs[pr[0]].name.c_str(), cs[pr[1]].name.c_str());
             return 3;
