@@ -217,10 +217,12 @@ int main(int argc, char **argv)
     const int rounds = argc > 1 ? atoi(argv[1]) : 5;
     const size_t n = (size_t)1 << 26, nvec = n / 4;
     const size_t nm = (size_t)1 << 24, nvm = nm / 4;
+    /* dst holds the largest output: n elements, or the gather's 8 rows of nm */
+    const size_t nd = std::max(n, 8 * nm);
     float *src, *dst, *ref;
     CHECK(hipMalloc(&src, n * 4 + 4096));
-    CHECK(hipMalloc(&dst, n * 4));
-    CHECK(hipMalloc(&ref, n * 4));
+    CHECK(hipMalloc(&dst, nd * 4));
+    CHECK(hipMalloc(&ref, nd * 4));
     const float *s4 = src + 1;                        /* 4 B past dst's phase */
     std::vector<float*> ops(8);
     SrcList sl, sl_al;
@@ -239,7 +241,7 @@ int main(int argc, char **argv)
     hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
                        (void*)dst, 1, 8ull, n);
     hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
-                       (void*)ref, 1, 9ull, n);
+                       (void*)ref, 1, 9ull, nd);
     CHECK(hipDeviceSynchronize());
     const unsigned g2 = (unsigned)(nvec / kReduceBlock), gm = (unsigned)(nvm / kReduceBlock);
     SrcList s1 = sl_al;
@@ -295,17 +297,18 @@ int main(int argc, char **argv)
     };
 
     /* bits: the misaligned forms against the product's realigning forms */
-    std::vector<uint32_t> a(n), b(n);
+    std::vector<uint32_t> a(nd), b(nd);
     const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {4, 13},
                             {4, 14}, {4, 15}, {7, 16}, {7, 17}, {7, 18}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
-            CHECK(hipMemcpy(dst, ref, n * 4, hipMemcpyDeviceToDevice));   /* same start */
+            CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
             cs[pr[k]].run();
             CHECK(hipDeviceSynchronize());
-            CHECK(hipMemcpy(k ? b.data() : a.data(), dst, n * 4, hipMemcpyDeviceToHost));
+            CHECK(hipMemcpy(k ? b.data() : a.data(), dst, nd * 4, hipMemcpyDeviceToHost));
         }
-        const size_t cmp = pr[0] == 7 ? nm : n;   /* N = 8 writes nm elements, a gather 8 nm = n */
+        /* N = 8 writes nm elements, a gather 8 nm, the rest n */
+        const size_t cmp = pr[0] == 7 ? nm : pr[0] == 10 ? 8 * nm : n;
         if (!std::equal(a.begin(), a.begin() + cmp, b.begin())) {
             printf("MISMATCH %s vs %s\n", cs[pr[0]].name.c_str(), cs[pr[1]].name.c_str());
             return 3;
