@@ -288,6 +288,21 @@ int main(int argc, char **argv)
         {"gather 8 rows, XCD map, ex temporal", 2.0 * 8 * nm * 4, [&] {
              hipLaunchKernelGGL((k_gather_ms<0, 1>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
                                 (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"N=8 aligned capped, XCD map", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_multi<float, 0, 8, 1, 1>), dim3(gm), dim3(kReduceBlock),
+                                0, 0, dst, sl_al, 0u, (size_t)0, nvm, (size_t)0); }, {}},
+        {"N=4 aligned capped", 5.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_multi<float, 0, 4, 0, 1>), dim3(gm), dim3(kReduceBlock),
+                                0, 0, dst, sl_al, 0u, (size_t)0, nvm, (size_t)0); }, {}},
+        {"N=4 aligned capped, XCD map", 5.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_multi<float, 0, 4, 1, 1>), dim3(gm), dim3(kReduceBlock),
+                                0, 0, dst, sl_al, 0u, (size_t)0, nvm, (size_t)0); }, {}},
+        {"tree n=8 aligned capped", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_tree<float, 0, 8, 0, 1>), dim3(gm), dim3(kReduceBlock),
+                                0, 0, dst, sl_al, 8u, (size_t)0, nvm, (size_t)0); }, {}},
+        {"tree n=8 aligned capped, XCD map", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_tree<float, 0, 8, 1, 1>), dim3(gm), dim3(kReduceBlock),
+                                0, 0, dst, sl_al, 8u, (size_t)0, nvm, (size_t)0); }, {}},
         {"copy shift, ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 1, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2", 2.0 * n * 4, [&] { run_ms<1, 1, 2, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2 ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 2, 0>(dst, s1, nvec); }, {}},
@@ -298,8 +313,9 @@ int main(int argc, char **argv)
 
     /* bits: the misaligned forms against the product's realigning forms */
     std::vector<uint32_t> a(nd), b(nd);
-    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {4, 13},
-                            {4, 14}, {4, 15}, {7, 16}, {7, 17}, {7, 18}};
+    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {6, 13},
+                            {14, 15}, {16, 17}, {4, 18}, {4, 19}, {4, 20}, {7, 21}, {7, 22},
+                            {7, 23}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
@@ -308,7 +324,8 @@ int main(int argc, char **argv)
             CHECK(hipMemcpy(k ? b.data() : a.data(), dst, nd * 4, hipMemcpyDeviceToHost));
         }
         /* N = 8 writes nm elements, a gather 8 nm, the rest n */
-        const size_t cmp = pr[0] == 7 ? nm : pr[0] == 10 ? 8 * nm : n;
+        const size_t cmp = (pr[0] == 7 || pr[0] == 6 || pr[0] == 14 || pr[0] == 16) ? nm
+                           : pr[0] == 10 ? 8 * nm : n;
         if (!std::equal(a.begin(), a.begin() + cmp, b.begin())) {
             printf("MISMATCH %s vs %s\n", cs[pr[0]].name.c_str(), cs[pr[1]].name.c_str());
             return 3;
