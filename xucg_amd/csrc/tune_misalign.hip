@@ -303,6 +303,18 @@ int main(int argc, char **argv)
         {"tree n=8 aligned capped, XCD map", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_reduce_tree<float, 0, 8, 1, 1>), dim3(gm), dim3(kReduceBlock),
                                 0, 0, dst, sl_al, 8u, (size_t)0, nvm, (size_t)0); }, {}},
+        {"N=8 aligned via the shift kernel (capped)", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_multi_shift<float, 0, 8, 1>), dim3(gm),
+                                dim3(kReduceBlock), 0, 0, dst, sl_al, 0u, (size_t)0, nvm,
+                                (size_t)0); }, {}},
+        {"N=4 aligned via the shift kernel (capped)", 5.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_multi_shift<float, 0, 4, 1>), dim3(gm),
+                                dim3(kReduceBlock), 0, 0, dst, sl_al, 0u, (size_t)0, nvm,
+                                (size_t)0); }, {}},
+        {"tree n=8 aligned via the shift kernel (capped)", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_tree_shift<float, 0, 8, 1>), dim3(gm),
+                                dim3(kReduceBlock), 0, 0, dst, sl_al, 8u, (size_t)0, nvm,
+                                (size_t)0); }, {}},
         {"copy shift, ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 1, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2", 2.0 * n * 4, [&] { run_ms<1, 1, 2, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2 ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 2, 0>(dst, s1, nvec); }, {}},
@@ -314,8 +326,8 @@ int main(int argc, char **argv)
     /* bits: the misaligned forms against the product's realigning forms */
     std::vector<uint32_t> a(nd), b(nd);
     const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {6, 13},
-                            {14, 15}, {16, 17}, {4, 18}, {4, 19}, {4, 20}, {7, 21}, {7, 22},
-                            {7, 23}};
+                            {14, 15}, {16, 17}, {6, 18}, {14, 19}, {16, 20}, {4, 21}, {4, 22},
+                            {4, 23}, {7, 24}, {7, 25}, {7, 26}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
