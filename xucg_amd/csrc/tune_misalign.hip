@@ -205,6 +205,50 @@ k_gather_ms(char *dst, SrcList srcs, size_t row_bytes, size_t nvec)
     }
 }
 
+/* In-phase operands (round 4, r04o): the realigning kernel fed in-phase
+ * operands read 84.8 % where k_reduce_multi read 79.9 % (capped, N = 8). What
+ * of the realigning kernel does it? All forms capped, on the XCD tile map:
+ *   MODE 0  clamped unmasked loads + sched barrier, nothing else
+ *   MODE 1  as 0, plus the temporal loads of the realigning kernel (lane 63
+ *           the next tile's first vector, the other lanes the operand's last),
+ *           kept alive and unused
+ *   MODE 2  as 0, plus lane 63's next-tile load alone (masked) */
+template <int N, int MODE>
+__global__ void __launch_bounds__(kReduceBlock)
+k_mx(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    const size_t i = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                     threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    u32x4 val[N], ex[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        const u32x4 *a4 = reinterpret_cast<const u32x4*>(srcs.p[m]);
+        val[m] = ld16<1>(a4 + (i < nvec ? i : nvec - 1));
+        if (MODE == 1) {
+            ex[m] = ld16<0>(a4 + (last_lane && i + 1 < nvec ? i + 1 : nvec - 1));
+        } else if (MODE == 2) {
+            if (last_lane && i + 1 < nvec) {
+                ex[m] = ld16<0>(a4 + i + 1);
+            } else {
+                ex[m] = u32x4{0, 0, 0, 0};
+            }
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (MODE != 0) {
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            asm volatile("" :: "v"(ex[m][0]));
+        }
+    }
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val, fv));
+    }
+}
+
 struct Case {
     std::string name;
     double bytes;
@@ -315,6 +359,15 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k_reduce_tree_shift<float, 0, 8, 1>), dim3(gm),
                                 dim3(kReduceBlock), 0, 0, dst, sl_al, 8u, (size_t)0, nvm,
                                 (size_t)0); }, {}},
+        {"N=8 aligned, clamp + barrier", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_mx<8, 0>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
+                                nvm); }, {}},
+        {"N=8 aligned, + temporal extra loads", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_mx<8, 1>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
+                                nvm); }, {}},
+        {"N=8 aligned, + lane-63 next-tile load", 9.0 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_mx<8, 2>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
+                                nvm); }, {}},
         {"copy shift, ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 1, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2", 2.0 * n * 4, [&] { run_ms<1, 1, 2, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2 ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 2, 0>(dst, s1, nvec); }, {}},
@@ -326,8 +379,8 @@ int main(int argc, char **argv)
     /* bits: the misaligned forms against the product's realigning forms */
     std::vector<uint32_t> a(nd), b(nd);
     const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {6, 13},
-                            {14, 15}, {16, 17}, {6, 18}, {14, 19}, {16, 20}, {4, 21}, {4, 22},
-                            {4, 23}, {7, 24}, {7, 25}, {7, 26}};
+                            {14, 15}, {16, 17}, {6, 18}, {14, 19}, {16, 20}, {6, 21}, {6, 22},
+                            {6, 23}, {4, 24}, {4, 25}, {4, 26}, {7, 27}, {7, 28}, {7, 29}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
