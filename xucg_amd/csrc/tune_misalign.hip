@@ -249,6 +249,43 @@ k_mx(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+/* The 2-operand combine (the headline kernel, k_reduce<.., XM=0>), in phase,
+ * with the pieces of the realigning kernel that sped the 8-operand form:
+ *   MODE 0  clamped unmasked loads + sched barrier
+ *   MODE 1  + a temporal load of src: lane 63 the next tile's first vector,
+ *           the other lanes src's last vector (as k_reduce_shift's `ex`)
+ *   MODE 2  + the same for dst
+ *   MODE 3  + only the other lanes' load (every lane src's last vector)
+ * XMAP 1: the XCD tile map. */
+template <int MODE, int XMAP>
+__global__ void __launch_bounds__(kReduceBlock)
+k2x(float *dst, const float *src, size_t nvec)
+{
+    const size_t tile = XMAP ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t i = tile * kReduceBlock + threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4 = reinterpret_cast<u32x4*>(dst);
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const u32x4 a = ld16<1>(s4 + ic);
+    const u32x4 b = ld16<1>(d4 + ic);
+    u32x4 e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
+    const size_t nx = (MODE != 3 && last_lane && i + 1 < nvec) ? i + 1 : nvec - 1;
+    if (MODE >= 1) {
+        e0 = ld16<0>(s4 + nx);
+    }
+    if (MODE == 2) {
+        e1 = ld16<0>(d4 + nx);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (MODE >= 1) {
+        asm volatile("" :: "v"(e0[0]), "v"(e1[0]));
+    }
+    if (i < nvec) {
+        st16<1>(d4 + i, vapply<float, 0>(a, b));
+    }
+}
+
 struct Case {
     std::string name;
     double bytes;
@@ -368,6 +405,19 @@ int main(int argc, char **argv)
         {"N=8 aligned, + lane-63 next-tile load", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_mx<8, 2>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
                                 nvm); }, {}},
+        {"2-op clamp + barrier", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"2-op + temporal src extra", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<1, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"2-op + temporal src, dst extra", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<2, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"2-op + uniform last-vector load", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<3, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"2-op + temporal src extra, XCD map", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<1, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"2-op aligned via the shift kernel", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_shift<float, 0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0,
+                                dst, (const float*)src, (size_t)0, nvec, (size_t)0, 0u); }, {}},
         {"copy shift, ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 1, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2", 2.0 * n * 4, [&] { run_ms<1, 1, 2, 0>(dst, s1, nvec); }, {}},
         {"copy shift, U=2 ex temporal", 2.0 * n * 4, [&] { run_ms<1, 0, 2, 0>(dst, s1, nvec); }, {}},
@@ -380,7 +430,8 @@ int main(int argc, char **argv)
     std::vector<uint32_t> a(nd), b(nd);
     const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {6, 13},
                             {14, 15}, {16, 17}, {6, 18}, {14, 19}, {16, 20}, {6, 21}, {6, 22},
-                            {6, 23}, {4, 24}, {4, 25}, {4, 26}, {7, 27}, {7, 28}, {7, 29}};
+                            {6, 23}, {0, 24}, {0, 25}, {0, 26}, {0, 27}, {0, 28}, {0, 29},
+                            {4, 30}, {4, 31}, {4, 32}, {7, 33}, {7, 34}, {7, 35}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
