@@ -13,7 +13,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 0>"
+KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 1, 1>"
 GRID = (1 << 26) // 4
 
 

@@ -14,7 +14,7 @@ import json
 import statistics
 import sys
 
-KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 0>"
+KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 1, 1>"
 COUNT = 1 << 26
 GRID = COUNT // 4          # one 16-B vector (4 fp32) per lane
 

@@ -121,8 +121,18 @@ __device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
  * combine from 56% (grid-stride loop, temporal) to 85% of 8 TB/s with
  * one-wave workgroups and U = 1 (profiles/r01). The ragged head
  * (until dst is 16-B aligned) and tail (< 16 B) are done by the first lanes.
+ *
+ * PF (the product's form since round 4; U = 1, one wave per workgroup): the
+ * XCD-aware tile map, and lane 63 also loads the next tile's first src vector
+ * with a temporal load and discards it, as the realigning kernel's `ex`. The
+ * next tile runs on the same XCD, so the line is fetched once and waits in
+ * L2 for its own wave; HBM bytes stay at 1.003 x. The realigning kernel had
+ * run 2 points above this one on six boxes; this form matched it, against
+ * neither the map nor the load alone (tools/tune_misalign, profiles/r04/r04q,
+ * DESIGN.md 3). Loads are clamped and unmasked behind a sched barrier, as in
+ * k_reduce_shift.
  */
-template <typename T, int OP, int U, int NT, int BS, int XM = 0>
+template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0>
 __global__ void __launch_bounds__(BS)
 k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 {
@@ -140,6 +150,25 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 
     const u32x4 *s4   = reinterpret_cast<const u32x4*>(src + head);
     u32x4 *d4         = reinterpret_cast<u32x4*>(dst + head);
+    if constexpr (PF) {
+        static_assert(U == 1 && BS == 64, "one vector per lane, one wave per workgroup");
+        if (nvec == 0) {
+            return;
+        }
+        const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * BS +
+                          threadIdx.x;
+        const size_t ic = i < nvec ? i : nvec - 1;
+        const bool last_lane = threadIdx.x == BS - 1;
+        const u32x4 a  = ld16<NT>(s4 + ic);
+        const u32x4 b  = ld16<NT>(d4 + ic);
+        const u32x4 pf = ld16<0>(s4 + (last_lane && i + 1 < nvec ? i + 1 : nvec - 1));
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" :: "v"(pf[0]));     /* the load stays; its value is unused */
+        if (i < nvec) {
+            st16<NT>(d4 + i, vapply<T, OP>(a, b));
+        }
+        return;
+    }
     /* XM: the XCD-aware tile map, for a src whose vectors straddle 128-B
      * lines (its edge lines are then shared with the neighbouring tiles) */
     const size_t tile = XM ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x;

@@ -69,13 +69,14 @@ inline size_t line_head(const void *dst, size_t count)
     return h < count ? h : count;
 }
 
-/* XCD-aware tile map when a source's vectors straddle lines (see k_reduce) */
+/* XCD-aware tile map when a source's vectors straddle lines (k_reduce_multi,
+ * k_reduce_tree; the 2-operand combine always takes it, k_reduce's PF form) */
 inline bool straddles_lines(const void *p)
 {
     return ((uintptr_t)p & (kLine - 1)) != 0;
 }
 
-template <typename T, int OP, int XM>
+template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
     constexpr size_t V = 16 / sizeof(T);
@@ -86,11 +87,11 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStre
         const size_t off = first ? 0 : head + done * V;
         /* one tile of U vectors per lane: grid sized to the chunk (no loop),
          * and to the head's lanes */
-        unsigned grid = grid_for(chunk, (size_t)kReduceBlock * kReduceU, 0x7fffffff);
+        unsigned grid = grid_for(chunk, (size_t)kReduceBlock, 0x7fffffff);
         if (first && div_up(head, kReduceBlock) > grid) {
             grid = (unsigned)div_up(head, kReduceBlock);
         }
-        hipLaunchKernelGGL((k_reduce<T, OP, kReduceU, 1, kReduceBlock, XM>), dim3(grid),
+        hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, 1>), dim3(grid),
                            dim3(kReduceBlock), 0, st, d + off, s + off, first ? head : 0,
                            chunk, last ? tail : 0);
         done += chunk;
@@ -160,11 +161,7 @@ hipError_t launch_reduce(void *dst, const void *src, size_t count, hipStream_t s
         }
         return hipGetLastError();
     }
-    if (straddles_lines(s + head)) {
-        launch_vec<T, OP, 1>(d, s, head, nvec, tail, st);
-    } else {
-        launch_vec<T, OP, 0>(d, s, head, nvec, tail, st);
-    }
+    launch_vec<T, OP>(d, s, head, nvec, tail, st);
     return hipGetLastError();
 }
 

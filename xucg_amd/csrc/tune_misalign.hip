@@ -329,7 +329,7 @@ int main(int argc, char **argv)
     s1.p[0] = s4;
 
     std::vector<Case> cs = {
-        {"2-op aligned k_reduce", 3.0 * n * 4, [&] {
+        {"2-op aligned k_reduce (round 3's form)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
                                 nvec, (size_t)0); }, {}},
@@ -405,6 +405,10 @@ int main(int argc, char **argv)
         {"N=8 aligned, + lane-63 next-tile load", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_mx<8, 2>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
                                 nvm); }, {}},
+        {"2-op product (k_reduce PF: XCD map + temporal next-tile load)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 1>), dim3(g2),
+                                dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
+                                nvec, (size_t)0); }, {}},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2x<0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op + temporal src extra", 3.0 * n * 4, [&] {
@@ -431,7 +435,7 @@ int main(int argc, char **argv)
     const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {6, 13},
                             {14, 15}, {16, 17}, {6, 18}, {14, 19}, {16, 20}, {6, 21}, {6, 22},
                             {6, 23}, {0, 24}, {0, 25}, {0, 26}, {0, 27}, {0, 28}, {0, 29},
-                            {4, 30}, {4, 31}, {4, 32}, {7, 33}, {7, 34}, {7, 35}};
+                            {0, 30}, {4, 31}, {4, 32}, {4, 33}, {7, 34}, {7, 35}, {7, 36}};
     for (const auto &pr : pairs) {
         for (int k = 0; k < 2; k++) {
             CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
