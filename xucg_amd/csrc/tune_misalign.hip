@@ -257,11 +257,11 @@ k_mx(float *dst, SrcList srcs, size_t nvec)
  *   MODE 2  + the same for dst
  *   MODE 3  + only the other lanes' load (every lane src's last vector)
  * XMAP 1: the XCD tile map. */
-template <int MODE, int XMAP>
+template <int MODE, int XMAP, unsigned C = kXcdChunk>
 __global__ void __launch_bounds__(kReduceBlock)
 k2x(float *dst, const float *src, size_t nvec)
 {
-    const size_t tile = XMAP ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x;
+    const size_t tile = XMAP ? xcd_tile<C>(blockIdx.x, gridDim.x) : blockIdx.x;
     const size_t i = tile * kReduceBlock + threadIdx.x;
     const bool last_lane = threadIdx.x == kReduceBlock - 1;
     const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
@@ -305,6 +305,16 @@ int main(int argc, char **argv)
     CHECK(hipMalloc(&dst, nd * 4));
     CHECK(hipMalloc(&ref, nd * 4));
     const float *s4 = src + 1;                        /* 4 B past dst's phase */
+    /* the north-star size: 2 x 1 GiB, in phase */
+    const size_t ng = (size_t)1 << 28, nvg = ng / 4;
+    const unsigned gg = (unsigned)(nvg / kReduceBlock);
+    float *srcg, *dstg;
+    CHECK(hipMalloc(&srcg, ng * 4));
+    CHECK(hipMalloc(&dstg, ng * 4));
+    hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
+                       (void*)srcg, 1, 11ull, ng);
+    hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
+                       (void*)dstg, 1, 12ull, ng);
     std::vector<float*> ops(8);
     SrcList sl, sl_al;
     for (int m = 0; m < 8; m++) {
@@ -409,6 +419,26 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 1>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
                                 nvec, (size_t)0); }, {}},
+        {"1 GiB: round 3's k_reduce", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(gg),
+                                dim3(kReduceBlock), 0, 0, dstg, (const float*)srcg, (size_t)0,
+                                nvg, (size_t)0); }, {}},
+        {"1 GiB: product (PF, chunk 64)", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 1>), dim3(gg),
+                                dim3(kReduceBlock), 0, 0, dstg, (const float*)srcg, (size_t)0,
+                                nvg, (size_t)0); }, {}},
+        {"1 GiB: PF, chunk 128", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2x<1, 1, 128>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg,
+                                srcg, nvg); }, {}},
+        {"1 GiB: PF, chunk 32", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2x<1, 1, 32>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg,
+                                srcg, nvg); }, {}},
+        {"256 MiB: PF, chunk 128", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<1, 1, 128>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src,
+                                nvec); }, {}},
+        {"256 MiB: PF, chunk 32", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2x<1, 1, 32>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src,
+                                nvec); }, {}},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2x<0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op + temporal src extra", 3.0 * n * 4, [&] {
@@ -430,24 +460,80 @@ int main(int argc, char **argv)
         {"N=8 shift capped, U=2 ex temporal", 9.0 * nm * 4, [&] { run_ms<8, 0, 2, 1>(dst, sl, nvm); }, {}},
     };
 
-    /* bits: the misaligned forms against the product's realigning forms */
-    std::vector<uint32_t> a(nd), b(nd);
-    const int pairs[][2] = {{1, 2}, {4, 5}, {7, 8}, {7, 9}, {10, 11}, {10, 12}, {6, 13},
-                            {14, 15}, {16, 17}, {6, 18}, {14, 19}, {16, 20}, {6, 21}, {6, 22},
-                            {6, 23}, {0, 24}, {0, 25}, {0, 26}, {0, 27}, {0, 28}, {0, 29},
-                            {0, 30}, {4, 31}, {4, 32}, {4, 33}, {7, 34}, {7, 35}, {7, 36}};
-    for (const auto &pr : pairs) {
-        for (int k = 0; k < 2; k++) {
-            CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));  /* same start */
-            cs[pr[k]].run();
-            CHECK(hipDeviceSynchronize());
-            CHECK(hipMemcpy(k ? b.data() : a.data(), dst, nd * 4, hipMemcpyDeviceToHost));
+    /* bits: every form against its reference form, by name; each run starts
+     * from the same output contents */
+    auto idx = [&](const char *nm_) {
+        for (size_t k = 0; k < cs.size(); k++) {
+            if (cs[k].name == nm_) return (int)k;
         }
-        /* N = 8 writes nm elements, a gather 8 nm, the rest n */
-        const size_t cmp = (pr[0] == 7 || pr[0] == 6 || pr[0] == 14 || pr[0] == 16) ? nm
-                           : pr[0] == 10 ? 8 * nm : n;
-        if (!std::equal(a.begin(), a.begin() + cmp, b.begin())) {
-            printf("MISMATCH %s vs %s\n", cs[pr[0]].name.c_str(), cs[pr[1]].name.c_str());
+        fprintf(stderr, "no case %s\n", nm_);
+        exit(2);
+    };
+    const char *pairs[][2] = {
+        {"2-op shift (product)", "2-op plain misaligned"},
+        {"copy shift (product's copy_row)", "copy plain misaligned"},
+        {"N=8 shift (product)", "N=8 shift, VGPR-capped"},
+        {"N=8 shift (product)", "N=8 plain misaligned (capped)"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, ex temporal"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, XCD map, ex temporal"},
+        {"N=8 aligned (capped)", "N=8 aligned capped, XCD map"},
+        {"N=4 aligned capped", "N=4 aligned capped, XCD map"},
+        {"tree n=8 aligned capped", "tree n=8 aligned capped, XCD map"},
+        {"N=8 aligned (capped)", "N=8 aligned via the shift kernel (capped)"},
+        {"N=4 aligned capped", "N=4 aligned via the shift kernel (capped)"},
+        {"tree n=8 aligned capped", "tree n=8 aligned via the shift kernel (capped)"},
+        {"N=8 aligned (capped)", "N=8 aligned, clamp + barrier"},
+        {"N=8 aligned (capped)", "N=8 aligned, + temporal extra loads"},
+        {"N=8 aligned (capped)", "N=8 aligned, + lane-63 next-tile load"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op product (k_reduce PF: XCD map + temporal next-tile load)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op clamp + barrier"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op + temporal src extra"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op + temporal src, dst extra"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op + uniform last-vector load"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op + temporal src extra, XCD map"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op aligned via the shift kernel"},
+        {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 128"},
+        {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 32"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: product (PF, chunk 64)"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF, chunk 128"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF, chunk 32"},
+        {"copy shift (product's copy_row)", "copy shift, ex temporal"},
+        {"copy shift (product's copy_row)", "copy shift, U=2"},
+        {"copy shift (product's copy_row)", "copy shift, U=2 ex temporal"},
+        {"N=8 shift (product)", "N=8 shift capped, ex temporal"},
+        {"N=8 shift (product)", "N=8 shift capped, U=2"},
+        {"N=8 shift (product)", "N=8 shift capped, U=2 ex temporal"},
+    };
+    std::vector<uint32_t> a(nd), b(nd);
+    std::vector<uint32_t> ag, bg;
+    for (const auto &pr : pairs) {
+        const std::string first = pr[0];
+        const bool big = first.rfind("1 GiB", 0) == 0;
+        /* N = 8 / 4 and the tree write nm elements, a gather 8 nm, 1 GiB ng,
+         * the rest n */
+        const size_t cmp = big ? ng
+                         : (first.rfind("N=", 0) == 0 || first.rfind("tree", 0) == 0) ? nm
+                         : first.rfind("gather", 0) == 0 ? 8 * nm : n;
+        if (big && ag.empty()) {
+            ag.resize(ng);
+            bg.resize(ng);
+        }
+        for (int k = 0; k < 2; k++) {
+            if (big) {
+                hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
+                                   (void*)dstg, 1, 12ull, ng);
+            } else {
+                CHECK(hipMemcpy(dst, ref, nd * 4, hipMemcpyDeviceToDevice));
+            }
+            cs[idx(pr[k])].run();
+            CHECK(hipDeviceSynchronize());
+            uint32_t *h = big ? (k ? bg.data() : ag.data()) : (k ? b.data() : a.data());
+            CHECK(hipMemcpy(h, big ? dstg : dst, (big ? ng : nd) * 4, hipMemcpyDeviceToHost));
+        }
+        const bool same = big ? std::equal(ag.begin(), ag.end(), bg.begin())
+                              : std::equal(a.begin(), a.begin() + cmp, b.begin());
+        if (!same) {
+            printf("MISMATCH %s vs %s\n", pr[0], pr[1]);
             return 3;
         }
     }
