@@ -291,6 +291,7 @@ struct Case {
     double bytes;
     std::function<void()> run;
     std::vector<float> us;
+    bool flushed = false;   /* each launch timed alone after a 3 GiB stream */
 };
 
 int main(int argc, char **argv)
@@ -315,6 +316,12 @@ int main(int argc, char **argv)
                        (void*)srcg, 1, 11ull, ng);
     hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
                        (void*)dstg, 1, 12ull, ng);
+    const unsigned gg0 = (unsigned)(((ng / 4) + kReduceBlock - 1) / kReduceBlock);
+    auto flush = [&] {
+        hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(gg0),
+                           dim3(kReduceBlock), 0, 0, dstg, (const float*)srcg, (size_t)0,
+                           ng / 4, (size_t)0);
+    };
     std::vector<float*> ops(8);
     SrcList sl, sl_al;
     for (int m = 0; m < 8; m++) {
@@ -439,6 +446,17 @@ int main(int argc, char **argv)
         {"256 MiB: PF, chunk 32", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2x<1, 1, 32>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src,
                                 nvec); }, {}},
+        {"256 MiB cache-flushed: round 3's k_reduce", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(g2),
+                                dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
+                                nvec, (size_t)0); }, {}, true},
+        {"256 MiB cache-flushed: product (PF)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 1>), dim3(g2),
+                                dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
+                                nvec, (size_t)0); }, {}, true},
+        {"256 MiB cache-flushed: realigning kernel, src 4 B off", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_shift<float, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0,
+                                dst, s4, (size_t)0, nvec, (size_t)0, 0u); }, {}, true},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2x<0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op + temporal src extra", 3.0 * n * 4, [&] {
@@ -492,6 +510,7 @@ int main(int argc, char **argv)
         {"2-op aligned k_reduce (round 3's form)", "2-op + uniform last-vector load"},
         {"2-op aligned k_reduce (round 3's form)", "2-op + temporal src extra, XCD map"},
         {"2-op aligned k_reduce (round 3's form)", "2-op aligned via the shift kernel"},
+        {"2-op aligned k_reduce (round 3's form)", "256 MiB cache-flushed: product (PF)"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 128"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 32"},
         {"1 GiB: round 3's k_reduce", "1 GiB: product (PF, chunk 64)"},
@@ -543,6 +562,24 @@ int main(int argc, char **argv)
     for (int r = 0; r < rounds; r++) {
         for (auto &c : cs) {
             c.run();
+            if (c.flushed) {
+                /* the 1 GiB combine between launches streams 3 GiB through
+                 * L2 and the 256 MiB Infinity Cache: nothing of the previous
+                 * launch's operands is left in either */
+                float tot = 0;
+                for (int i = 0; i < 20; i++) {
+                    flush();
+                    CHECK(hipEventRecord(e0, 0));
+                    c.run();
+                    CHECK(hipEventRecord(e1, 0));
+                    CHECK(hipEventSynchronize(e1));
+                    float ms;
+                    CHECK(hipEventElapsedTime(&ms, e0, e1));
+                    tot += ms;
+                }
+                c.us.push_back(1000.f * tot / 20);
+                continue;
+            }
             CHECK(hipEventRecord(e0, 0));
             for (int i = 0; i < 20; i++) {
                 c.run();
@@ -560,7 +597,7 @@ int main(int argc, char **argv)
         auto v = c.us;
         std::sort(v.begin(), v.end());
         const double med = v[v.size() / 2];
-        printf("%-32s %9.2f us %6.1f %%\n", c.name.c_str(), med,
+        printf("%-56s %9.2f us %6.1f %%\n", c.name.c_str(), med,
                100.0 * c.bytes / (med * 1e-6) / 8e12);
     }
     return 0;
