@@ -286,6 +286,36 @@ k2x(float *dst, const float *src, size_t nvec)
     }
 }
 
+/* More of the PF idea (2-operand combine, XCD map): the last K lanes each
+ * load one line of tile + DIST (lane 63 its first line, lane 62 its second,
+ * ...) temporally and discard it; DST also does so for dst. */
+template <int K, int DST, int DIST>
+__global__ void __launch_bounds__(kReduceBlock)
+k2p(float *dst, const float *src, size_t nvec)
+{
+    const size_t tile = xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x);
+    const unsigned lane = threadIdx.x;
+    const size_t i = tile * kReduceBlock + lane;
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4 = reinterpret_cast<u32x4*>(dst);
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const u32x4 a = ld16<1>(s4 + ic);
+    const u32x4 b = ld16<1>(d4 + ic);
+    const unsigned k = kReduceBlock - 1 - lane;          /* 0 for lane 63 */
+    const size_t want = (tile + DIST) * kReduceBlock + (size_t)k * 8;
+    const size_t nx = (k < (unsigned)K && want < nvec) ? want : nvec - 1;
+    const u32x4 e0 = ld16<0>(s4 + nx);
+    u32x4 e1 = {0, 0, 0, 0};
+    if (DST) {
+        e1 = ld16<0>(d4 + nx);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" :: "v"(e0[0]), "v"(e1[0]));
+    if (i < nvec) {
+        st16<1>(d4 + i, vapply<float, 0>(a, b));
+    }
+}
+
 struct Case {
     std::string name;
     double bytes;
@@ -457,6 +487,16 @@ int main(int argc, char **argv)
         {"256 MiB cache-flushed: realigning kernel, src 4 B off", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce_shift<float, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0,
                                 dst, s4, (size_t)0, nvec, (size_t)0, 0u); }, {}, true},
+        {"PF: 2 lines of the next tile", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<2, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 4 lines of the next tile", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: src and dst line of the next tile", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<1, 1, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: first line two tiles ahead", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<1, 0, 2>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 1 line (k2p, = product)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<1, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2x<0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op + temporal src extra", 3.0 * n * 4, [&] {
@@ -512,6 +552,11 @@ int main(int argc, char **argv)
         {"2-op aligned k_reduce (round 3's form)", "2-op aligned via the shift kernel"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB cache-flushed: product (PF)"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 128"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 2 lines of the next tile"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of the next tile"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: src and dst line of the next tile"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: first line two tiles ahead"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 1 line (k2p, = product)"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 32"},
         {"1 GiB: round 3's k_reduce", "1 GiB: product (PF, chunk 64)"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF, chunk 128"},
