@@ -289,11 +289,11 @@ k2x(float *dst, const float *src, size_t nvec)
 /* More of the PF idea (2-operand combine, XCD map): the last K lanes each
  * load one line of tile + DIST (lane 63 its first line, lane 62 its second,
  * ...) temporally and discard it; DST also does so for dst. */
-template <int K, int DST, int DIST>
+template <int K, int DST, int DIST, unsigned C = kXcdChunk>
 __global__ void __launch_bounds__(kReduceBlock)
 k2p(float *dst, const float *src, size_t nvec)
 {
-    const size_t tile = xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x);
+    const size_t tile = xcd_tile<C>(blockIdx.x, gridDim.x);
     const unsigned lane = threadIdx.x;
     const size_t i = tile * kReduceBlock + lane;
     const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
@@ -495,6 +495,22 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k2p<1, 1, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"PF: first line two tiles ahead", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2p<1, 0, 2>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 8 lines (the whole next tile)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<8, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 4 lines of src and of dst", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 1, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 2 lines, chunk 128", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<2, 0, 1, 128>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 4 lines, chunk 128", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1, 128>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"1 GiB: PF 2 lines", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2p<2, 0, 1>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
+        {"1 GiB: PF 4 lines", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
+        {"1 GiB: PF 4 lines, chunk 128", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1, 128>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
+        {"256 MiB cache-flushed: PF 4 lines", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}, true},
         {"PF: 1 line (k2p, = product)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2p<1, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
@@ -557,6 +573,13 @@ int main(int argc, char **argv)
         {"2-op aligned k_reduce (round 3's form)", "PF: src and dst line of the next tile"},
         {"2-op aligned k_reduce (round 3's form)", "PF: first line two tiles ahead"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 1 line (k2p, = product)"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 8 lines (the whole next tile)"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of src and of dst"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 2 lines, chunk 128"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines, chunk 128"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF 2 lines"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines, chunk 128"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 32"},
         {"1 GiB: round 3's k_reduce", "1 GiB: product (PF, chunk 64)"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF, chunk 128"},
