@@ -13,7 +13,7 @@ import os
 import statistics
 import sys
 
-KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 1, 1>"
+KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 1, "   # PF form, any prefetch depth
 GRID = (1 << 26) // 4
 
 

@@ -14,9 +14,12 @@ import json
 import statistics
 import sys
 
-KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 1, 1>"
+KERNEL = "ucgdev::k_reduce<float, 0, 1, 1, 64, 1, "   # PF form, any prefetch depth
 COUNT = 1 << 26
 GRID = COUNT // 4          # one 16-B vector (4 fp32) per lane
+
+
+NAMES = set()
 
 
 def values(path, counter):
@@ -25,6 +28,7 @@ def values(path, counter):
         if KERNEL in r["Kernel_Name"] and int(r["Grid_Size"]) == GRID and \
                 r["Counter_Name"] == counter:
             out.append(float(r["Counter_Value"]))
+            NAMES.add(r["Kernel_Name"].split("(")[0].replace("void ", ""))
     return out
 
 
@@ -36,7 +40,7 @@ def main():
     hbm = int(round((2 * f_kb + w_kb) * 1024))
     alg = 3 * 4 * COUNT
     res = {str(COUNT): {
-        "kernel": KERNEL, "grid_threads": GRID, "launches": [len(fetch), len(write)],
+        "kernel": " / ".join(sorted(NAMES)), "grid_threads": GRID, "launches": [len(fetch), len(write)],
         "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
         "hbm_bytes_per_launch": hbm, "algorithmic_bytes_per_launch": alg,
         "ratio_to_algorithmic": round(hbm / alg, 5),

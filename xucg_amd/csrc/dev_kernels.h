@@ -122,15 +122,15 @@ __device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
  * one-wave workgroups and U = 1 (profiles/r01). The ragged head
  * (until dst is 16-B aligned) and tail (< 16 B) are done by the first lanes.
  *
- * PF (the product's form since round 4; U = 1, one wave per workgroup): the
- * XCD-aware tile map, and lane 63 also loads the next tile's first src vector
- * with a temporal load and discards it, as the realigning kernel's `ex`. The
- * next tile runs on the same XCD, so the line is fetched once and waits in
- * L2 for its own wave; HBM bytes stay at 1.003 x. The realigning kernel had
- * run 2 points above this one on six boxes; this form matched it, against
- * neither the map nor the load alone (tools/tune_misalign, profiles/r04/r04q,
- * DESIGN.md 3). Loads are clamped and unmasked behind a sched barrier, as in
- * k_reduce_shift.
+ * PF > 0 (the product's form since round 4; U = 1, one wave per workgroup):
+ * the XCD-aware tile map, and the last PF lanes also load the first PF lines
+ * of the next tile's src with temporal loads and discard them (PF = 1: lane
+ * 63's vector, as the realigning kernel's `ex`). The next tile runs on the
+ * same XCD, so those lines are fetched once and wait in L2 for their own
+ * wave. The realigning kernel had run 2 points above the plain one on six
+ * boxes; this form matched it, against neither the map nor the load alone
+ * (tools/tune_misalign, profiles/r04/r04q-r04v). Loads are
+ * clamped and unmasked behind a sched barrier, as in k_reduce_shift.
  */
 template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0>
 __global__ void __launch_bounds__(BS)
@@ -151,17 +151,22 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
     const u32x4 *s4   = reinterpret_cast<const u32x4*>(src + head);
     u32x4 *d4         = reinterpret_cast<u32x4*>(dst + head);
     if constexpr (PF) {
-        static_assert(U == 1 && BS == 64, "one vector per lane, one wave per workgroup");
+        static_assert(U == 1 && BS == 64 && PF <= 8,
+                      "one vector per lane, one wave per workgroup, at most a tile ahead");
         if (nvec == 0) {
             return;
         }
         const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * BS +
                           threadIdx.x;
         const size_t ic = i < nvec ? i : nvec - 1;
-        const bool last_lane = threadIdx.x == BS - 1;
+        /* the last PF lanes take one 128-B line (8 vectors) each of the next
+         * tile's src, lane 63 its first; every other lane reloads the last
+         * vector (one line, an L2 hit), so the load needs no branch */
+        const unsigned k = BS - 1 - threadIdx.x;
+        const size_t want = (i - threadIdx.x + BS) + (size_t)k * 8;
         const u32x4 a  = ld16<NT>(s4 + ic);
         const u32x4 b  = ld16<NT>(d4 + ic);
-        const u32x4 pf = ld16<0>(s4 + (last_lane && i + 1 < nvec ? i + 1 : nvec - 1));
+        const u32x4 pf = ld16<0>(s4 + (k < (unsigned)PF && want < nvec ? want : nvec - 1));
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("" :: "v"(pf[0]));     /* the load stays; its value is unused */
         if (i < nvec) {

@@ -76,6 +76,10 @@ inline bool straddles_lines(const void *p)
     return ((uintptr_t)p & (kLine - 1)) != 0;
 }
 
+/* lines of the next tile's src each wave of the 2-operand combine loads
+ * ahead (k_reduce's PF form) */
+constexpr int kPrefetchLines = 1;
+
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
@@ -91,7 +95,7 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStre
         if (first && div_up(head, kReduceBlock) > grid) {
             grid = (unsigned)div_up(head, kReduceBlock);
         }
-        hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, 1>), dim3(grid),
+        hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, kPrefetchLines>), dim3(grid),
                            dim3(kReduceBlock), 0, st, d + off, s + off, first ? head : 0,
                            chunk, last ? tail : 0);
         done += chunk;
