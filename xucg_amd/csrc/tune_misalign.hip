@@ -452,7 +452,11 @@ int main(int argc, char **argv)
         {"N=8 aligned, + lane-63 next-tile load", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_mx<8, 2>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
                                 nvm); }, {}},
-        {"2-op product (k_reduce PF: XCD map + temporal next-tile load)", 3.0 * n * 4, [&] {
+        {"2-op product: k_reduce PF=4 (next tile's first 4 lines)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 4>), dim3(g2),
+                                dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
+                                nvec, (size_t)0); }, {}},
+        {"2-op k_reduce PF=1 (next-tile first line)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 1>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
                                 nvec, (size_t)0); }, {}},
@@ -460,7 +464,7 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(gg),
                                 dim3(kReduceBlock), 0, 0, dstg, (const float*)srcg, (size_t)0,
                                 nvg, (size_t)0); }, {}},
-        {"1 GiB: product (PF, chunk 64)", 3.0 * ng * 4, [&] {
+        {"1 GiB: k_reduce PF=1", 3.0 * ng * 4, [&] {
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 1>), dim3(gg),
                                 dim3(kReduceBlock), 0, 0, dstg, (const float*)srcg, (size_t)0,
                                 nvg, (size_t)0); }, {}},
@@ -511,7 +515,7 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k2p<4, 0, 1, 128>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
         {"256 MiB cache-flushed: PF 4 lines", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2p<4, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}, true},
-        {"PF: 1 line (k2p, = product)", 3.0 * n * 4, [&] {
+        {"PF: 1 line (k2p)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2p<1, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2x<0, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
@@ -559,7 +563,7 @@ int main(int argc, char **argv)
         {"N=8 aligned (capped)", "N=8 aligned, clamp + barrier"},
         {"N=8 aligned (capped)", "N=8 aligned, + temporal extra loads"},
         {"N=8 aligned (capped)", "N=8 aligned, + lane-63 next-tile load"},
-        {"2-op aligned k_reduce (round 3's form)", "2-op product (k_reduce PF: XCD map + temporal next-tile load)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op k_reduce PF=1 (next-tile first line)"},
         {"2-op aligned k_reduce (round 3's form)", "2-op clamp + barrier"},
         {"2-op aligned k_reduce (round 3's form)", "2-op + temporal src extra"},
         {"2-op aligned k_reduce (round 3's form)", "2-op + temporal src, dst extra"},
@@ -572,7 +576,8 @@ int main(int argc, char **argv)
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of the next tile"},
         {"2-op aligned k_reduce (round 3's form)", "PF: src and dst line of the next tile"},
         {"2-op aligned k_reduce (round 3's form)", "PF: first line two tiles ahead"},
-        {"2-op aligned k_reduce (round 3's form)", "PF: 1 line (k2p, = product)"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 1 line (k2p)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op product: k_reduce PF=4 (next tile's first 4 lines)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 8 lines (the whole next tile)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of src and of dst"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 2 lines, chunk 128"},
@@ -581,7 +586,7 @@ int main(int argc, char **argv)
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines, chunk 128"},
         {"2-op aligned k_reduce (round 3's form)", "256 MiB: PF, chunk 32"},
-        {"1 GiB: round 3's k_reduce", "1 GiB: product (PF, chunk 64)"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: k_reduce PF=1"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF, chunk 128"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF, chunk 32"},
         {"copy shift (product's copy_row)", "copy shift, ex temporal"},
