@@ -216,11 +216,12 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t x)
     return __shfl_down(x, 1, 64);
 }
 
-template <typename T, int OP, int Q>
+template <typename T, int OP, int Q, int PF = 1>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
                unsigned rb)
 {
+    static_assert(PF >= 1 && PF <= 8, "lane 63's load is the next tile's first vector");
     constexpr int V   = 16 / sizeof(T);
     constexpr int BS  = kReduceBlock;
     const size_t gtid = (size_t)blockIdx.x * BS + threadIdx.x;
@@ -250,8 +251,13 @@ k_reduce_shift(T *dst, const T *src, size_t head, size_t nvec, size_t tail,
     const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
     /* temporal: that vector is the next tile's first, which its own wave
      * loads non-temporally; a non-temporal load here could evict the line
-     * before the neighbour's load and fetch it from HBM twice */
-    const u32x4 ex = ld16<0>(a4 + (last_lane && i < nvec ? i + 1 : nvec));
+     * before the neighbour's load and fetch it from HBM twice.
+     * Lanes 63 - 1 .. 63 - (PF - 1) load the next tile's following lines in
+     * the same instruction and discard them (k_reduce's PF form); lane 63's
+     * is A[i + 1] itself. A[nvec] holds src bytes (rb or Q > 0). */
+    const unsigned k  = BS - 1 - threadIdx.x;
+    const size_t want = (i - threadIdx.x + BS) + (size_t)k * 8;
+    const u32x4 ex = ld16<0>(a4 + (k < (unsigned)PF && want <= nvec ? want : nvec));
     __builtin_amdgcn_sched_barrier(0);  /* keep the shuffles behind all loads */
     /* A[i + 1]: the next lane's load; lane 63 loaded it itself */
     u32x4 hi;

@@ -124,7 +124,8 @@ void launch_shift(T *d, const T *s, size_t head, size_t nvec, size_t tail,
             if (first && head > items) items = head;
             if (last && tail > items) items = tail;
             const unsigned grid = grid_for(items, (size_t)kReduceBlock, 0x7fffffff);
-            hipLaunchKernelGGL((k_reduce_shift<T, OP, Q>), dim3(grid), dim3(kReduceBlock),
+            hipLaunchKernelGGL((k_reduce_shift<T, OP, Q, kPrefetchLines>), dim3(grid),
+                               dim3(kReduceBlock),
                                0, st, d + off, s + off, first ? head : 0, chunk,
                                last ? tail : 0, rb);
             done += chunk;

@@ -380,8 +380,11 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
                                 nvec, (size_t)0); }, {}},
-        {"2-op shift (product)", 3.0 * n * 4, [&] {
+        {"2-op shift, 1 line ahead (round 4 r04l-r04w)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce_shift<float, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0,
+                                dst, s4, (size_t)0, nvec, (size_t)0, 0u); }, {}},
+        {"2-op shift, 4 lines ahead (product)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce_shift<float, 0, 1, 4>), dim3(g2), dim3(kReduceBlock), 0, 0,
                                 dst, s4, (size_t)0, nvec, (size_t)0, 0u); }, {}},
         {"2-op plain misaligned", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL(k_plain_misaligned, dim3(g2), dim3(kReduceBlock), 0, 0,
@@ -548,7 +551,8 @@ int main(int argc, char **argv)
         exit(2);
     };
     const char *pairs[][2] = {
-        {"2-op shift (product)", "2-op plain misaligned"},
+        {"2-op shift, 1 line ahead (round 4 r04l-r04w)", "2-op plain misaligned"},
+        {"2-op shift, 1 line ahead (round 4 r04l-r04w)", "2-op shift, 4 lines ahead (product)"},
         {"copy shift (product's copy_row)", "copy plain misaligned"},
         {"N=8 shift (product)", "N=8 shift, VGPR-capped"},
         {"N=8 shift (product)", "N=8 plain misaligned (capped)"},
