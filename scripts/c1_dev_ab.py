@@ -3,12 +3,17 @@
 same command as bench.py's extra.c1_loopback_allreduce_4kib_fp32
 .device_buffers_* legs, alternating settings over several repetitions.
 
-    python scripts/c1_dev_ab.py OUT.json [reps]
+    python scripts/c1_dev_ab.py OUT.json [reps] [r03|r04]
 
-Settings: the default library (the context's second stream created with it),
-UCX_BUILTIN_DEV_D2H_STREAM=lazy (created on first use, round 2's default),
-the same with GPU_MAX_HW_QUEUES=2, the default with GPU_MAX_HW_QUEUES=1, and
-the completion by hipStreamSynchronize (UCX_BUILTIN_DEV_COMPLETION=sync).
+r03 settings: the default library (the context's second stream created with
+it), UCX_BUILTIN_DEV_D2H_STREAM=lazy (created on first use, round 2's
+default), the same with GPU_MAX_HW_QUEUES=2, the default with
+GPU_MAX_HW_QUEUES=1, and the completion by hipStreamSynchronize
+(UCX_BUILTIN_DEV_COMPLETION=sync).
+r04 settings (the device-buffer latency went from 12 to 95 us between the
+rounds): the default; hipMalloc memory and hipIpc keys instead of shareable
+memory (UCX_BUILTIN_DEV_SHAREABLE=n); no pool arena
+(UCX_BUILTIN_DEV_POOL_BYTES=0); both; the send buffer not registered.
 The parent never touches the GPU: ranks are child processes."""
 import json
 import os
@@ -20,14 +25,22 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 EXE = os.path.join(ROOT, "tests", "c", "_build", "c1_allreduce")
 
 
-def run(world, count, iters, env_extra):
+def run(world, count, iters, env_extra, prof=None):
+    """prof: a directory; rank 0 then runs under rocprofv3 (kernel and HIP API
+    traces with their statistics, no counters)"""
     allowed = sorted(os.sched_getaffinity(0))
     name = f"ucg_ab_{os.getpid()}_{uuid.uuid4().hex[:6]}"
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), C1_DEVICE_BUFFERS="1",
-                   C1_REGISTERED="1", UCX_BUILTIN_WAIT_TIMEOUT="60", **env_extra)
-        procs.append(subprocess.Popen([EXE, name, str(iters), "256", str(count)], env=env,
+                   C1_REGISTERED="1", UCX_BUILTIN_WAIT_TIMEOUT="60")
+        env.update(env_extra)
+        env = {k: v for k, v in env.items() if v is not None}
+        cmd = [EXE, name, str(iters), "256", str(count)]
+        if prof and r == 0:
+            cmd = ["rocprofv3", "--kernel-trace", "--hip-trace", "--stats", "--output-format",
+                   "csv", "-d", prof, "-o", "c1", "--"] + cmd
+        procs.append(subprocess.Popen(cmd, env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                                       text=True,
                                       preexec_fn=lambda c=allowed[r % len(allowed)]:
@@ -41,10 +54,19 @@ def run(world, count, iters, env_extra):
 
 def main():
     out, reps = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    settings = {"default": {}, "d2h_lazy": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy"},
-                "d2h_lazy_hwq2": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy", "GPU_MAX_HW_QUEUES": "2"},
-                "hwq1": {"GPU_MAX_HW_QUEUES": "1"},
-                "sync": {"UCX_BUILTIN_DEV_COMPLETION": "sync"}}
+    if (sys.argv[3] if len(sys.argv) > 3 else "r04") == "r03":
+        settings = {"default": {}, "d2h_lazy": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy"},
+                    "d2h_lazy_hwq2": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy",
+                                      "GPU_MAX_HW_QUEUES": "2"},
+                    "hwq1": {"GPU_MAX_HW_QUEUES": "1"},
+                    "sync": {"UCX_BUILTIN_DEV_COMPLETION": "sync"}}
+    else:
+        settings = {"default": {},
+                    "plain_memory": {"UCX_BUILTIN_DEV_SHAREABLE": "n"},
+                    "no_arena": {"UCX_BUILTIN_DEV_POOL_BYTES": "0"},
+                    "plain_no_arena": {"UCX_BUILTIN_DEV_SHAREABLE": "n",
+                                       "UCX_BUILTIN_DEV_POOL_BYTES": "0"},
+                    "send_not_registered": {"C1_REGISTERED": None}}
     res = {k: {"4kib_us": [], "64mib_us": []} for k in settings}
     for rep in range(reps):
         for k, env in settings.items():
@@ -54,6 +76,9 @@ def main():
                 if not r.get("bit_exact", False):
                     res[k].setdefault("errors", []).append(r)
         print(json.dumps({"rep": rep, **res}), flush=True)
+    if os.environ.get("C1_AB_PROFILE"):
+        res["profiled_default_4kib"] = run(4, 1024, 2000, {}, prof=os.environ["C1_AB_PROFILE"])
+        print(json.dumps(res["profiled_default_4kib"]), flush=True)
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
 

@@ -11,6 +11,7 @@
 #   ab       the occupancy-cap and misalignment A/B tools
 #   ab2      the misalignment A/B and its FETCH_SIZE pass per kernel
 #   ipc      the multi-process shareable-key tests (topology, one-shot, churn)
+#   c1ab     the device-buffer allreduce latency A/B (scripts/c1_dev_ab.py)
 # usage: scripts/gpu_r04.sh TAG step...
 set -u
 TAG=$1; shift
@@ -50,6 +51,9 @@ for s in "$@"; do
         > $OUT/pytest_ipc.log 2>&1
     rc=$?; echo "pytest rc $rc" >> $OUT/steps.log
     [ $rc -le 1 ] || exit 1 ;;
+  c1ab)
+    C1_AB_PROFILE=$OUT/c1prof timeout -k 10 500 python -u scripts/c1_dev_ab.py $OUT/c1_dev_ab.json 1 r04 \
+        > $OUT/c1_dev_ab.log 2>&1 || { tail -5 $OUT/c1_dev_ab.log; exit 1; } ;;
   shift)
     bash scripts/shift_pmc.sh $OUT/shift > $OUT/shift.log 2>&1 || { tail -5 $OUT/shift.log; exit 1; } ;;
   esac
