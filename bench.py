@@ -1126,11 +1126,14 @@ def shareable_memory_probe(store, rank, world, local_rank):
 def collective_child():
     """--collective-child: one rank of the collective phases (see above).
     XUCG_COLLECTIVE_BACKEND=gloo is the 1-GPU rehearsal (HostStagedDist).
-    torch's device memory comes from the shim's shareable allocator when
-    every rank can map every other rank's (shareable_memory_probe), so every
-    exported tensor is keyed by its physical allocation; otherwise the phases
-    run on torch's own allocator with hipIpc keys (XUCG_SHAREABLE_TORCH=n
-    forces that)."""
+    The phases run on torch's own allocator with hipIpc keys, which the
+    shim checks against the allocation's buffer id; exported tensors stay
+    allocated until the phases end. XUCG_SHAREABLE_TORCH=y instead takes
+    torch's device memory from the shim's shareable allocator when every rank
+    can map every other rank's (shareable_memory_probe), so every exported
+    tensor is keyed by its physical allocation. It is not the default:
+    kernels reading peers' imported shareable allocations ran 5-10x longer
+    on one GPU (profiles/r04/r04y)."""
     import datetime
     import torch
     import torch.distributed as dist
@@ -1142,7 +1145,7 @@ def collective_child():
     store = dist.TCPStore(os.environ.get("MASTER_ADDR", "127.0.0.1"),
                           int(os.environ["MASTER_PORT"]), world, rank == 0, timeout=timeout)
     peer_memory = {"kind": "hipIpc (torch's caching allocator)"}
-    if os.environ.get("XUCG_SHAREABLE_TORCH", "y")[:1] not in ("n", "0"):
+    if os.environ.get("XUCG_SHAREABLE_TORCH", "n")[:1] in ("y", "1"):
         ok, detail = shareable_memory_probe(store, rank, world, local_rank)
         if ok:
             xucg_amd.use_shareable_torch_memory()

@@ -482,6 +482,12 @@ int ucg_builtin_combine_step_on_device(ucg_builtin_combine_t *cmb)
 /* ------------------------------------------------------------------------ */
 /* device-resident buffers (the engine's remote-key steps)                  */
 /* ------------------------------------------------------------------------ */
+static int pool_shareable(void)
+{
+    const char *e = getenv("UCX_BUILTIN_DEV_POOL_MEM");
+    return e != NULL && strcmp(e, "shareable") == 0;
+}
+
 void *ucg_builtin_combine_dev_alloc(ucg_builtin_combine_t *cmb, size_t bytes)
 {
     void *p;
@@ -489,8 +495,14 @@ void *ucg_builtin_combine_dev_alloc(ucg_builtin_combine_t *cmb, size_t bytes)
         return NULL;
     }
     pthread_mutex_lock(&cmb->lock);
-    /* exported to the peers: mapped by its physical allocation */
-    p = ucg_builtin_dev_malloc_shareable(cmb->dev, bytes);
+    /* exported to the peers. hipMalloc memory (hipIpc keys, checked against
+     * the allocation's buffer id) by default: kernels that read peers'
+     * imported virtual-memory allocations ran 5-10x longer on one GPU
+     * (profiles/r04/r04y: 4 KiB allreduce 95 us against 10 us).
+     * UCX_BUILTIN_DEV_POOL_MEM=shareable keeps the pools in shareable
+     * allocations (keys that name the physical allocation). */
+    p = pool_shareable() ? ucg_builtin_dev_malloc_shareable(cmb->dev, bytes)
+                         : ucg_builtin_dev_malloc(cmb->dev, bytes);
     pthread_mutex_unlock(&cmb->lock);
     return p;
 }

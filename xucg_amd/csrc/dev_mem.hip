@@ -76,6 +76,34 @@ struct own_alloc {
 std::mutex g_mu;                                      /* guards everything here */
 std::unordered_map<void*, own_alloc> g_allocs;        /* base -> allocation */
 
+/* Freed plain allocations kept for reuse at the same size (round 4). A
+ * hipFree + hipMalloc can hand out the old address backed by new memory,
+ * and the copy engine can then write through the old translation (DESIGN.md
+ * 7, tools/va_reuse_probe). Reusing the allocation itself - same address,
+ * same memory - never remaps anything. Its keys are retired at free all the
+ * same (a peer's old key is refused), and the device is synchronised before
+ * it is handed out again. Bounded by UCX_BUILTIN_DEV_CACHE_BYTES (default
+ * 1 GiB per process; 0 = free at once); past the bound it is freed. */
+std::multimap<std::pair<int, size_t>, void*> g_plain_cache;   /* (device, bytes) */
+size_t g_plain_cached = 0;
+
+size_t plain_cache_limit()
+{
+    static const size_t lim = [] {
+        const char *e = getenv("UCX_BUILTIN_DEV_CACHE_BYTES");
+        if (e == nullptr || *e == 0) {
+            return (size_t)1 << 30;
+        }
+        char *end = nullptr;
+        double v = strtod(e, &end);
+        if (end && (*end == 'k' || *end == 'K')) v *= 1024.0;
+        else if (end && (*end == 'm' || *end == 'M')) v *= 1048576.0;
+        else if (end && (*end == 'g' || *end == 'G')) v *= 1073741824.0;
+        return v > 0 ? (size_t)v : (size_t)0;
+    }();
+    return lim;
+}
+
 /* The last memory events of the process, for ucg_builtin_dev_debug_ptr: a
  * buffer found to read as zeros is matched against what happened to its
  * address range. */
@@ -803,6 +831,18 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
      * the runtime shares with other allocations, and such memory cannot be
      * exported through hipIpcGetMemHandle (ucg_builtin_dev_ipc_export) */
     bytes = round_gran(bytes);
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto c = g_plain_cache.find({device, bytes});
+        if (c != g_plain_cache.end()) {
+            p = c->second;
+            g_plain_cache.erase(c);
+            g_plain_cached -= bytes;
+            g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0};
+            note_event('R', p, p, bytes, 0);
+            return p;
+        }
+    }
     const hipError_t e = hipMalloc(&p, bytes);
     if (e != hipSuccess) {
         hip_status(e, "hipMalloc");
@@ -920,6 +960,23 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         (void)hipMemUnmap(ptr, a.bytes);
         (void)hipMemRelease(a.handle);
         g_va_retired += a.bytes;           /* the range is never reused */
+    } else if (own && a.kind == KIND_PLAIN) {
+        /* as hipFree does: nothing queued may still use it; then kept for
+         * the next allocation of its size (g_plain_cache) */
+        (void)hipSetDevice(a.device);
+        e = hipDeviceSynchronize();
+        bool kept = false;
+        {
+            std::lock_guard<std::mutex> g(g_mu);
+            if (g_plain_cached + a.bytes <= plain_cache_limit()) {
+                g_plain_cache.emplace(std::make_pair(a.device, a.bytes), ptr);
+                g_plain_cached += a.bytes;
+                kept = true;
+            }
+        }
+        if (!kept) {
+            e = hipFree(ptr);
+        }
     } else {
         e = hipFree(ptr);
     }
