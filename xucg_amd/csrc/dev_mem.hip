@@ -108,7 +108,7 @@ size_t plain_cache_limit()
  * buffer found to read as zeros is matched against what happened to its
  * address range. */
 struct mem_event {
-    char     kind;      /* M malloc, V shareable malloc, F free, X export,
+    char     kind;      /* M malloc, R malloc from the reuse cache, V shareable malloc, F free, X export,
                            I import, C release (close), S stale key refused */
     void    *ptr;
     void    *base;
