@@ -473,6 +473,37 @@ def test_shareable_allocations_never_reuse_an_address(dev_ctx):
 
 
 @pytest.mark.gpu
+def test_plain_allocations_reused_whole(dev_ctx):
+    """Round 4: a freed ucg_builtin_dev_malloc allocation is
+    kept and handed out again, whole, for the next allocation of its size - the
+    same address on the same memory, never a remap - and its old key is
+    refused. 60 rounds of allocate, DMA upload, kernel read-back, free: one
+    address throughout, every read right."""
+    n = (6 << 20) // 4
+    out = dev_ctx.alloc(n * 4)
+    first = None
+    try:
+        for r in range(60):
+            b = dev_ctx.alloc(n * 4)
+            if first is None:
+                first = b.ptr
+                key = dev_ctx.ipc_export(b.ptr)
+            assert b.ptr == first, (r, hex(b.ptr), hex(first))
+            assert " R ptr" in dev_ctx.debug_ptr(b.ptr) or r == 0
+            b.upload(np.full(n, r + 1, np.uint32))                 # DMA write
+            assert dev_ctx.copy_multi([out.ptr], [b.ptr], n * 4) == 0   # kernel read
+            dev_ctx.sync()
+            got = out.download(np.uint32, n)
+            assert (got == r + 1).all(), (r, int((got != r + 1).sum()))
+            b.free()
+        with pytest.raises(xucg_amd.UcsError) as e:
+            dev_ctx.ipc_import(key)
+        assert e.value.status == -2
+    finally:
+        out.free()
+
+
+@pytest.mark.gpu
 def test_ipc_import_rejects_foreign_and_dead_keys(dev_ctx):
     """A blob that is no key, and a key whose exporter's key server is gone,
     fail loudly at import."""

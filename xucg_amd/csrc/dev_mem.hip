@@ -833,8 +833,11 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
     bytes = round_gran(bytes);
     {
         std::lock_guard<std::mutex> g(g_mu);
-        auto c = g_plain_cache.find({device, bytes});
-        if (c != g_plain_cache.end()) {
+        /* the most recently freed one of its size (equal keys keep their
+         * insertion order) */
+        auto c = g_plain_cache.upper_bound({device, bytes});
+        if (c != g_plain_cache.begin() &&
+            (c = std::prev(c))->first == std::make_pair(device, bytes)) {
             p = c->second;
             g_plain_cache.erase(c);
             g_plain_cached -= bytes;
