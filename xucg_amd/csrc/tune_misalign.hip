@@ -289,12 +289,15 @@ k2x(float *dst, const float *src, size_t nvec)
 /* More of the PF idea (2-operand combine, XCD map): the last K lanes each
  * load one line of tile + DIST (lane 63 its first line, lane 62 its second,
  * ...) temporally and discard it; DST also does so for dst. */
-template <int K, int DST, int DIST, unsigned C = kXcdChunk>
+template <int K, int DST, int DIST, unsigned C = kXcdChunk, int EDGE = 1>
 __global__ void __launch_bounds__(kReduceBlock)
 k2p(float *dst, const float *src, size_t nvec)
 {
     const size_t tile = xcd_tile<C>(blockIdx.x, gridDim.x);
     const unsigned lane = threadIdx.x;
+    /* EDGE 0: no prefetch by the last tile of an XCD's chunk (its neighbour
+     * runs on another XCD, which would fetch the lines again) */
+    const bool edge = EDGE == 0 && (tile % C) == C - 1;
     const size_t i = tile * kReduceBlock + lane;
     const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
     u32x4 *d4 = reinterpret_cast<u32x4*>(dst);
@@ -303,7 +306,7 @@ k2p(float *dst, const float *src, size_t nvec)
     const u32x4 b = ld16<1>(d4 + ic);
     const unsigned k = kReduceBlock - 1 - lane;          /* 0 for lane 63 */
     const size_t want = (tile + DIST) * kReduceBlock + (size_t)k * 8;
-    const size_t nx = (k < (unsigned)K && want < nvec) ? want : nvec - 1;
+    const size_t nx = (k < (unsigned)K && want < nvec && !edge) ? want : nvec - 1;
     const u32x4 e0 = ld16<0>(s4 + nx);
     u32x4 e1 = {0, 0, 0, 0};
     if (DST) {
@@ -518,6 +521,18 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k2p<4, 0, 1, 128>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
         {"256 MiB cache-flushed: PF 4 lines", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2p<4, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}, true},
+        {"PF: 3 lines", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<3, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 5 lines", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<5, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 6 lines", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<6, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"PF: 4 lines, none at chunk edges", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1, kXcdChunk, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
+        {"1 GiB: PF 4 lines, none at chunk edges", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2p<4, 0, 1, kXcdChunk, 0>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
+        {"1 GiB: PF 6 lines", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2p<6, 0, 1>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
         {"PF: 1 line (k2p)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k2p<1, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"2-op clamp + barrier", 3.0 * n * 4, [&] {
@@ -581,6 +596,12 @@ int main(int argc, char **argv)
         {"2-op aligned k_reduce (round 3's form)", "PF: src and dst line of the next tile"},
         {"2-op aligned k_reduce (round 3's form)", "PF: first line two tiles ahead"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 1 line (k2p)"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 3 lines"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 5 lines"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 6 lines"},
+        {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines, none at chunk edges"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines, none at chunk edges"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF 6 lines"},
         {"2-op aligned k_reduce (round 3's form)", "2-op product: k_reduce PF=4 (next tile's first 4 lines)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 8 lines (the whole next tile)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of src and of dst"},
