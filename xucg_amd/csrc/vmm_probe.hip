@@ -331,10 +331,81 @@ static int do_export(const char *name, size_t mib)
     return 0;
 }
 
+__global__ void k_nop(unsigned *p)
+{
+    if (p != nullptr && threadIdx.x == 1024) {
+        p[0] = 1;                          /* never: keeps the kernel non-empty */
+    }
+}
+
+__global__ void k_sum(const uint32_t *p, size_t n, unsigned *out)
+{
+    unsigned acc = 0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        acc += p[i];
+    }
+    if (acc == 0x12345678u) {
+        out[0] = acc;                      /* practically never: keeps the loads */
+    }
+}
+
+/* average time per launch of `fn` over `reps` back-to-back launches (us) */
+template <typename F>
+static double per_launch_us(F fn, int reps)
+{
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    fn();
+    CHECK(hipEventRecord(e0, 0));
+    for (int i = 0; i < reps; i++) {
+        fn();
+    }
+    CHECK(hipEventRecord(e1, 0));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    return 1000.0 * ms / reps;
+}
+
+/* round 4: kernels reading imported VMM memory ran 5-10x longer
+ * in the engine. What costs: any kernel once an import is mapped, or only
+ * the ones that read it? An empty kernel, a 4 KiB read and a 64 MiB read, on
+ * the import, on this process's own hipMalloc memory and on its own VMM
+ * memory. */
+static void import_costs(const char *when, const uint32_t *imp, size_t n, const uint32_t *own,
+                         const uint32_t *own_vmm, unsigned *ctr)
+{
+    const int reps = 2000;
+    printf("import cost %s: empty kernel %.2f us", when,
+           per_launch_us([&] { hipLaunchKernelGGL(k_nop, dim3(1), dim3(64), 0, 0, ctr); }, reps));
+    if (imp == nullptr) {
+        printf("\n");
+        return;
+    }
+    auto rd = [&](const uint32_t *p, size_t words, unsigned grid) {
+        return per_launch_us([&] { hipLaunchKernelGGL(k_sum, dim3(grid), dim3(256), 0, 0, p,
+                                                      words, ctr); }, words > 4096 ? 50 : reps);
+    };
+    printf("; 4 KiB read: import %.2f us, own hipMalloc %.2f us, own VMM %.2f us",
+           rd(imp, 1024, 4), rd(own, 1024, 4), rd(own_vmm, 1024, 4));
+    printf("; %zu MiB read: import %.1f us, own hipMalloc %.1f us, own VMM %.1f us\n",
+           n * 4 >> 20, rd(imp, n, 4096), rd(own, n, 4096), rd(own_vmm, n, 4096));
+}
+
 static int do_import(const char *name, size_t mib)
 {
     CHECK(hipSetDevice(0));
     const size_t bytes = mib << 20, n = bytes / 4;
+    unsigned *ctr;
+    uint32_t *own;
+    CHECK(hipMalloc(&ctr, 64));
+    CHECK(hipMalloc(&own, bytes));
+    CHECK(hipMemset(own, 1, bytes));
+    import_costs("before any import", nullptr, 0, nullptr, nullptr, ctr);
     hipMemAllocationProp prop = prop_for(0);
     size_t gran = 0;
     CHECK(hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum));
@@ -385,8 +456,21 @@ static int do_import(const char *name, size_t mib)
                (unsigned long long)m.gen, ms, va, host_bad((uint32_t*)va, n, key),
                kernel_bad((uint32_t*)va, n, key));
         if (round == 0) {
+            hipMemGenericAllocationHandle_t hv;
+            void *ov = nullptr;
+            CHECK(hipMemCreate(&hv, bytes, &prop, 0));
+            CHECK(hipMemAddressReserve(&ov, bytes, gran, nullptr, 0));
+            map_rw(ov, bytes, hv, 0);
+            CHECK(hipMemset(ov, 1, bytes));
+            CHECK(hipDeviceSynchronize());
+            import_costs("with the import mapped", (const uint32_t*)va, n, own,
+                         (const uint32_t*)ov, ctr);
             hipLaunchKernelGGL(k_pattern, dim3(1024), dim3(256), 0, 0, (uint32_t*)va + n / 2,
                                n / 2, 0xB0000000u);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipMemUnmap(ov, bytes));
+            CHECK(hipMemRelease(hv));
+            CHECK(hipMemAddressFree(ov, bytes));
         }
         CHECK(hipDeviceSynchronize());
         CHECK(hipMemUnmap(va, m.size));
@@ -399,6 +483,9 @@ static int do_import(const char *name, size_t mib)
         }
     }
     close(s);
+    import_costs("after the imports were released", nullptr, 0, nullptr, nullptr, ctr);
+    CHECK(hipFree(own));
+    CHECK(hipFree(ctr));
     printf("import: ok\n");
     return 0;
 }
