@@ -531,6 +531,10 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k2p<4, 0, 1, kXcdChunk, 0>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}},
         {"1 GiB: PF 4 lines, none at chunk edges", 3.0 * ng * 4, [&] {
              hipLaunchKernelGGL((k2p<4, 0, 1, kXcdChunk, 0>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
+        {"1 GiB: PF 3 lines", 3.0 * ng * 4, [&] {
+             hipLaunchKernelGGL((k2p<3, 0, 1>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
+        {"256 MiB cache-flushed: PF 3 lines", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2p<3, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0, dst, src, nvec); }, {}, true},
         {"1 GiB: PF 6 lines", 3.0 * ng * 4, [&] {
              hipLaunchKernelGGL((k2p<6, 0, 1>), dim3(gg), dim3(kReduceBlock), 0, 0, dstg, srcg, nvg); }, {}},
         {"PF: 1 line (k2p)", 3.0 * n * 4, [&] {
@@ -602,6 +606,7 @@ int main(int argc, char **argv)
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines, none at chunk edges"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines, none at chunk edges"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 6 lines"},
+        {"1 GiB: round 3's k_reduce", "1 GiB: PF 3 lines"},
         {"2-op aligned k_reduce (round 3's form)", "2-op product: k_reduce PF=4 (next tile's first 4 lines)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 8 lines (the whole next tile)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of src and of dst"},
