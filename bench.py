@@ -1476,7 +1476,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc_traffic(n),
-                "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64, XM=1, PF=4>",
+                "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64, XM=1, PF=3>",
                 "kernel_avg_us": round(avg_us, 3),
                 "kernel_avg_us_batches": [round(b, 2) for b in batch_us],
                 "kernel_median_us_single_launches": round(median_us, 3),

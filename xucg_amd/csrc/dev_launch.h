@@ -78,7 +78,7 @@ inline bool straddles_lines(const void *p)
 
 /* lines of the next tile's src each wave of the 2-operand combine loads
  * ahead (k_reduce's PF form) */
-constexpr int kPrefetchLines = 4;
+constexpr int kPrefetchLines = 3;
 
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)

@@ -386,7 +386,7 @@ int main(int argc, char **argv)
         {"2-op shift, 1 line ahead (round 4 r04l-r04w)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce_shift<float, 0, 1>), dim3(g2), dim3(kReduceBlock), 0, 0,
                                 dst, s4, (size_t)0, nvec, (size_t)0, 0u); }, {}},
-        {"2-op shift, 4 lines ahead (product)", 3.0 * n * 4, [&] {
+        {"2-op shift, 4 lines ahead", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce_shift<float, 0, 1, 4>), dim3(g2), dim3(kReduceBlock), 0, 0,
                                 dst, s4, (size_t)0, nvec, (size_t)0, 0u); }, {}},
         {"2-op plain misaligned", 3.0 * n * 4, [&] {
@@ -458,7 +458,11 @@ int main(int argc, char **argv)
         {"N=8 aligned, + lane-63 next-tile load", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_mx<8, 2>), dim3(gm), dim3(kReduceBlock), 0, 0, dst, sl_al,
                                 nvm); }, {}},
-        {"2-op product: k_reduce PF=4 (next tile's first 4 lines)", 3.0 * n * 4, [&] {
+        {"2-op product: k_reduce PF=3 (next tile's first 3 lines)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 3>), dim3(g2),
+                                dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
+                                nvec, (size_t)0); }, {}},
+        {"2-op k_reduce PF=4 (next tile's first 4 lines)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 4>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
                                 nvec, (size_t)0); }, {}},
@@ -571,7 +575,7 @@ int main(int argc, char **argv)
     };
     const char *pairs[][2] = {
         {"2-op shift, 1 line ahead (round 4 r04l-r04w)", "2-op plain misaligned"},
-        {"2-op shift, 1 line ahead (round 4 r04l-r04w)", "2-op shift, 4 lines ahead (product)"},
+        {"2-op shift, 1 line ahead (round 4 r04l-r04w)", "2-op shift, 4 lines ahead"},
         {"copy shift (product's copy_row)", "copy plain misaligned"},
         {"N=8 shift (product)", "N=8 shift, VGPR-capped"},
         {"N=8 shift (product)", "N=8 plain misaligned (capped)"},
@@ -607,7 +611,8 @@ int main(int argc, char **argv)
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 4 lines, none at chunk edges"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 6 lines"},
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 3 lines"},
-        {"2-op aligned k_reduce (round 3's form)", "2-op product: k_reduce PF=4 (next tile's first 4 lines)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op k_reduce PF=4 (next tile's first 4 lines)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op product: k_reduce PF=3 (next tile's first 3 lines)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 8 lines (the whole next tile)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of src and of dst"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 2 lines, chunk 128"},
