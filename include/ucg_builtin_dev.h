@@ -91,6 +91,7 @@ typedef enum {
     UCS_ERR_CANCELED        = -16,
     UCS_ERR_OUT_OF_RANGE    = -19,
     UCS_ERR_TIMED_OUT       = -20,
+    UCS_ERR_EXCEEDS_LIMIT   = -21,
     UCS_ERR_UNSUPPORTED     = -22
 } ucs_status_t;
 #endif
@@ -348,6 +349,34 @@ ucs_status_t ucg_builtin_dev_memcpy(ucg_builtin_dev_ctx_t *ctx, void *dst,
  * every other pair always runs capped. For A/B runs inside one process
  * (bench.py's one-shot reduce-scatter over xGMI). */
 void         ucg_builtin_dev_set_multi_cap(int capped);
+
+/* Fault injection, for tests: the `after`-th call from now to a device
+ * combine entry point of this process (ucg_builtin_dev_reduce, _reduce_multi,
+ * _reduce_tree, _combine, _combine_host, _profile_reduce) fails with
+ * UCS_ERR_IO_ERROR ("injected device error") and launches nothing; 0 disarms.
+ * Returns how many injected failures have fired in this process so far. It
+ * shows that a device failure on any thread - the resend timer's included -
+ * reaches the operation's completion status (SURVEY.md 8b,
+ * builtin_comp_step.inl:332-333). */
+unsigned     ucg_builtin_dev_inject_failure(unsigned after);
+
+/* Process-wide memory accounting of the shim (round 5):
+ *   [0] bytes of GPU virtual address ranges retired: a shareable allocation
+ *       or an import, once unmapped, leaves its reservation behind so that no
+ *       address is ever mapped to other physical memory;
+ *   [1] how many such ranges;
+ *   [2] the cap on [0]: past it a new shareable allocation or import fails
+ *       with UCS_ERR_EXCEEDS_LIMIT (UCX_BUILTIN_DEV_VA_RETIRED_MAX, default
+ *       64 TiB, or ucg_builtin_dev_set_va_retired_max);
+ *   [3] bytes held by the reuse cache of freed, never-exported
+ *       ucg_builtin_dev_malloc allocations (UCX_BUILTIN_DEV_CACHE_BYTES);
+ *   [4] bytes of live shareable allocations of this process;
+ *   [5] bytes of live shareable imports (peers' allocations mapped here). */
+#define UCG_BUILTIN_DEV_NMEMSTATS 6
+void         ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS]);
+/* Set the cap on retired address ranges for this process (0 = back to
+ * UCX_BUILTIN_DEV_VA_RETIRED_MAX / the default); for tests. */
+void         ucg_builtin_dev_set_va_retired_max(uint64_t bytes);
 
 /* Diagnostics: what the runtime and this shim know about a device address
  * (range, attributes, live or imported allocation) and the process's recent

@@ -1,0 +1,43 @@
+#!/bin/bash
+# Round-5 GPU steps; each under its own time limit, stop at the first failure.
+#   scripts/gpu_r05.sh OUTDIR step [step ...]
+# steps: pf (prefetch A/B, tools/tune_multi_pf), slice (scripts/slice_probe.py),
+#        slice_prof (the same, rank 0 under rocprofv3 --kernel-trace),
+#        va (tools/va_reuse_probe single-process modes), va_ipc (its 12-process mode),
+#        tests:<pytest -k expr> (pytest -m gpu subset)
+OUT=$1; shift
+mkdir -p $OUT
+export TMPDIR=/tmp
+for step in "$@"; do
+    echo "step $step $(date +%T)" >> $OUT/steps.log
+    case $step in
+    pf)
+        for spec in "multi 8 24" "multi 4 24" "multi 16 24" "multi 8 26" "tree 8 24" "tree 3 24" "tree 12 24" "tree 6 24"; do
+            tag=$(echo $spec | tr ' ' '_')
+            timeout -k 10 150 tools/tune_multi_pf $spec 7 > $OUT/pf_$tag.txt 2>&1 || exit 1
+        done ;;
+    slice)
+        timeout -k 10 500 python scripts/slice_probe.py $OUT/slice 4 2000 > $OUT/slice.txt 2>&1 || exit 1 ;;
+    slice_extra)
+        timeout -k 10 200 python scripts/slice_probe.py $OUT/slice 4 2000 mixed:none:all \
+            freed:none:all shareable:none:one > $OUT/slice_extra.txt 2>&1 || exit 1 ;;
+    slice_prof)
+        SLICE_PROF_DIR=$OUT/slice_prof timeout -k 10 300 python scripts/slice_probe.py $OUT/slice_prof 4 2000 \
+            shareable:read:all plain:read:all > $OUT/slice_prof.txt 2>&1 || exit 1 ;;
+    va)
+        timeout -k 10 300 tools/va_reuse_probe 200 6 > $OUT/va_reuse.txt 2>&1 || exit 1 ;;
+    va_ipc)
+        timeout -k 10 560 python scripts/va_reuse_ipc.py $OUT/va_ipc 12 100 6 close hold > $OUT/va_ipc.txt 2>&1 || exit 1 ;;
+    tests:all)
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+            > $OUT/pytest_gpu.log 2>&1 || exit 1 ;;
+    bench)
+        timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1 ;;
+    tests:*)
+        expr=${step#tests:}
+        timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread \
+            -k "$expr" > $OUT/pytest_$(echo "$expr" | tr -c 'a-zA-Z0-9_' '_' | cut -c1-40).log 2>&1 || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
+echo "done $(date +%T)" >> $OUT/steps.log

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""tools/va_reuse_probe's multi-process mode: NP
+processes on the one GPU recycle hipMalloc buffers at the same address every
+round, upload by DMA, and read each other's buffers through hipIpc imports
+(tools/src/va_reuse_probe.hip). This parent never touches the GPU.
+
+    python scripts/va_reuse_ipc.py OUTDIR [NP=12] [ITERS=200] [MiB=6] [mode ...]
+"""
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tools", "va_reuse_probe")
+
+
+def main():
+    out_dir = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/va_ipc"
+    np_ = int(sys.argv[2]) if len(sys.argv) > 2 else 12
+    iters = sys.argv[3] if len(sys.argv) > 3 else "200"
+    mib = sys.argv[4] if len(sys.argv) > 4 else "6"
+    modes = sys.argv[5:] or ["close", "hold"]
+    os.makedirs(out_dir, exist_ok=True)
+    rc = 0
+    for mode in modes:
+        d = tempfile.mkdtemp(prefix="xucg_vaipc_")
+        try:
+            procs = [subprocess.Popen([EXE, "ipc", d, str(r), str(np_), iters, mib, mode],
+                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                     for r in range(np_)]
+            ranks = []
+            for r, p in enumerate(procs):
+                try:
+                    out, _ = p.communicate(timeout=240)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    out = p.communicate()[0] + " <killed: timeout>"
+                js = [ln for ln in out.splitlines() if ln.startswith("{")]
+                try:
+                    ranks.append(json.loads(js[-1]))
+                except (ValueError, IndexError):
+                    ranks.append({"rank": r, "exit": p.returncode, "tail": out[-400:]})
+                    rc = 1
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+        tot = {k: sum(x.get(k, 0) for x in ranks)
+               for k in ("rounds", "same_va", "own_kernel_bad", "own_dma_bad", "peer_kernel_bad",
+                         "peer_dma_bad", "bad_words", "zero_words")}
+        res = {"mode": mode, "np": np_, "iters": int(iters), "mib": int(mib), "total": tot,
+               "ranks": ranks}
+        with open(os.path.join(out_dir, "va_reuse_ipc.jsonl"), "a") as f:
+            f.write(json.dumps(res) + "\n")
+        print(f"{mode}: {tot}", flush=True)
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())

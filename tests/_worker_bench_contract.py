@@ -60,6 +60,27 @@ def main():
     if check(acc):
         fail("a changed element passed the sampled check")
 
+    # the C4 phases' parity without a 4 GiB vendor collective (PlanWindows):
+    # every shard's windows against the oracle's recursive doubling as that
+    # shard's owner evaluates it, and one changed element caught
+    from xucg_amd import group as G
+    n4 = world << 16
+    x4 = [O.fill("float32", "round", 0x5EED4100 + r, n4) for r in range(world)]
+    plan = bench.PlanWindows(dist, torch.from_numpy(x4[rank].copy()), n4, rank, world, "cpu")
+    full = np.empty(n4, np.float32)
+    for r in range(world):
+        lo, hi = G.shard_bounds(n4, 4, world, r)
+        full[lo:hi] = O.reduce_multi("sum", "float32", x4, r)[lo:hi]
+    lo, hi = G.shard_bounds(n4, 4, world, rank)
+    mine = torch.from_numpy(full[lo:hi].copy())
+    if not (plan.rs_ok(mine) and plan.full_ok(torch.from_numpy(full))):
+        fail("the plan's result fails PlanWindows")
+    mine[-1] = float(np.nextafter(mine[-1].item(), np.inf, dtype=np.float32))
+    bad = full.copy()
+    bad[0] = np.nextafter(bad[0], np.float32(np.inf))
+    if plan.rs_ok(mine) or plan.full_ok(torch.from_numpy(bad)):
+        fail("a changed element passed PlanWindows")
+
     # the 1-GPU rehearsal's stand-in for RCCL (bench.HostStagedDist) against
     # gloo's own results, on CPU tensors
     from xucg_amd import group as G

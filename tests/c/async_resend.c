@@ -2,7 +2,8 @@
  * async_resend.c - the resend timer of the group's async context (SURVEY.md
  * 8a row a15; builtin/builtin.c:260-294, 408-413) on two processes.
  *
- *   RANK=r WORLD_SIZE=2 async_resend <shm-name> [host|staged|device]
+ *   RANK=r WORLD_SIZE=2|4 async_resend <shm-name> [host|staged|device] [exact|round]
+ *                                      [fail]
  *
  * The transport has 2 cells per ring, so an allreduce of 133 fragments stops
  * at UCS_ERR_NO_RESOURCE at once on both members. Phases (shm barriers):
@@ -25,6 +26,20 @@
  *           and runs on member 0's timer thread once they go out.
  * Member 0 prints the timer's resend and combine counts and the combine
  * layer's host / device call counts.
+ * Round 5:
+ *   WORLD_SIZE=4  the recursive-doubling plan over 4 members (peers my^1,
+ *           my^2); members 1-3 progress, member 0's timer works alone
+ *   round   rounded fp32 inputs (the oracle's generator, distinct per member):
+ *           every member's result must equal, bit for bit, the oracle's
+ *           simulation of the plan (ucg_oracle_reduce_multi, the association
+ *           of builtin_recursive.c:158-169) - the default "exact" inputs
+ *           (small integers) would hide an association error
+ *   fail    just before member 0 goes to sleep, the next device combine call
+ *           of its process is armed to fail (ucg_builtin_dev_inject_failure):
+ *           the timer thread's combine fails, and member 0's completion
+ *           status must be that error (recv_handle_error,
+ *           builtin_comp_step.inl:332-333); the other members may then end
+ *           with their wait timeout, never with a wrong result
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -35,6 +50,7 @@
 
 #include "ucg_builtin_ops.h"
 #include "ucg_builtin_dev.h"
+#include "combine_ref.h"          /* the checker (oracle/, test infrastructure) */
 
 static int sum_f32(void *op, char *src, char *dst, unsigned count, void *dt)
 {
@@ -63,18 +79,22 @@ static double now_s(void)
     return ts.tv_sec + 1e-9 * ts.tv_nsec;
 }
 
-static int run(char **argv, const char *mode);
+static int run(char **argv, const char *mode, int round_inputs, int fail);
 
 int main(int argc, char **argv)
 {
-    return run(argv, argc > 2 ? argv[2] : "host");
+    return run(argv, argc > 2 ? argv[2] : "host",
+               argc > 3 && strcmp(argv[3], "round") == 0,
+               argc > 4 && strcmp(argv[4], "fail") == 0);
 }
 
-static int run(char **argv, const char *mode)
+static int run(char **argv, const char *mode, int round_inputs, int fail)
 {
     const unsigned rank = (unsigned)atoi(getenv("RANK"));
+    const unsigned world = getenv("WORLD_SIZE") ? (unsigned)atoi(getenv("WORLD_SIZE")) : 2;
     const int count = 8192 * 4 / 4;                /* 32 KiB: 133 fragments of 248 B */
     const int staged = strcmp(mode, "staged") == 0, device = strcmp(mode, "device") == 0;
+    float *want = malloc(count * sizeof(float));
     ucg_builtin_reduce_params_t rp = {sum_f32, yes, no, yes, convert, is_int, is_fp};
     ucg_builtin_combine_config_t cfg;
     ucg_builtin_combine_t *cmb;
@@ -93,8 +113,33 @@ static int run(char **argv, const char *mode)
     if (staged) {
         cfg.dev_min_bytes = 0;                     /* every step on the GPU */
     }
-    for (i = 0; i < count; i++) {
-        in[i] = (float)((int)(rank * 1000 + i) % 4096 - 2048);
+    if (world != 2 && world != 4) {
+        fprintf(stderr, "WORLD_SIZE must be 2 or 4\n");
+        return 2;
+    }
+    if (round_inputs) {
+        /* every member's input from the oracle's generator; the expected
+         * result is the oracle's simulation of the plan over all of them */
+        const void *srcs[4];
+        float *all = malloc((size_t)world * count * sizeof(float));
+        unsigned r;
+        for (r = 0; r < world; r++) {
+            ucg_oracle_fill(ORA_F32, ORA_DIST_ROUND, 0xA5A50000u + r, all + (size_t)r * count,
+                            count);
+            srcs[r] = all + (size_t)r * count;
+        }
+        memcpy(in, all + (size_t)rank * count, count * sizeof(float));
+        ucg_oracle_reduce_multi(ORA_SUM, ORA_F32, want, srcs, world, rank, count);
+        free(all);
+    } else {
+        for (i = 0; i < count; i++) {
+            unsigned r;
+            in[i] = (float)((int)(rank * 1000 + i) % 4096 - 2048);
+            want[i] = 0.0f;
+            for (r = 0; r < world; r++) {             /* exact: any order */
+                want[i] += (float)((int)(r * 1000 + i) % 4096 - 2048);
+            }
+        }
     }
     if (ucg_builtin_combine_create(&rp, &cfg, &cmb) != UCS_OK) {
         fprintf(stderr, "rank %u: combine set-up failed\n", rank);
@@ -120,8 +165,8 @@ static int run(char **argv, const char *mode)
             return 1;
         }
     }
-    if (ucg_builtin_shm_iface_open(argv[1], 2, rank, 256, 2, &iface) != UCS_OK ||
-        ucg_builtin_lgroup_create(iface, 1, 2, rank, cmb, &g) != UCS_OK ||
+    if (ucg_builtin_shm_iface_open(argv[1], world, rank, 256, 2, &iface) != UCS_OK ||
+        ucg_builtin_lgroup_create(iface, 1, world, rank, cmb, &g) != UCS_OK ||
         ucg_builtin_lcoll_allreduce(g, sbuf, rbuf, count, (void*)1, (void*)1, &c) != UCS_OK) {
         fprintf(stderr, "rank %u: set-up failed\n", rank);
         return 1;
@@ -131,7 +176,7 @@ static int run(char **argv, const char *mode)
         return 1;
     }
     ucg_builtin_shm_barrier(iface);
-    if (rank == 1) {
+    if (rank != 0) {
         st = ucg_builtin_lcoll_start(c);                 /* stops at the full ring */
         ucg_builtin_shm_barrier(iface);                  /* B1 */
         ucg_builtin_shm_barrier(iface);                  /* B2 */
@@ -148,19 +193,27 @@ static int run(char **argv, const char *mode)
         }
         ucg_builtin_lgroup_stats(g, st4);
         sent_before = st4[0];
+        if (fail) {
+            /* the next device combine call fails - the owner thread makes
+             * none from here on, so it is the timer thread's */
+            ucg_builtin_dev_inject_failure(1);
+        }
         ucg_builtin_shm_barrier(iface);                  /* B2 */
         usleep(1500 * 1000);                             /* the timer thread works alone */
         ucg_builtin_lgroup_async_stats(g, as);
         ucg_builtin_lgroup_stats(g, st4);
         ucg_builtin_combine_stats(cmb, cs);
-        printf("{\"mode\": \"%s\", \"sent_before_sleep\": %llu, \"sent_after_sleep\": %llu, "
+        printf("{\"mode\": \"%s\", \"world\": %u, \"inputs\": \"%s\", \"fail\": %d, "
+               "\"sent_before_sleep\": %llu, \"sent_after_sleep\": %llu, "
                "\"stashed\": %llu, \"timer_resends\": %llu, \"timer_combines\": %llu, "
                "\"host_calls\": %llu, \"device_calls\": %llu, \"staged_steps\": %llu}\n",
-               mode, (unsigned long long)sent_before, (unsigned long long)st4[0],
+               mode, world, round_inputs ? "round" : "exact", fail,
+               (unsigned long long)sent_before, (unsigned long long)st4[0],
                (unsigned long long)st4[2], (unsigned long long)as[0],
                (unsigned long long)as[1], (unsigned long long)cs[0],
                (unsigned long long)cs[2], (unsigned long long)cs[4]);
-        if (as[0] == 0 || as[1] == 0 || (!device && st4[0] != 133)) {
+        fflush(stdout);
+        if (as[0] == 0 || as[1] == 0 || (!device && !fail && st4[0] < 133)) {
             fprintf(stderr, "rank 0: the timer thread did not resend and combine\n");
             ok = 0;
         }
@@ -176,14 +229,30 @@ static int run(char **argv, const char *mode)
         ok = 0;
     }
     for (i = 0; i < count && st == UCS_OK; i++) {
-        const float want = (float)((int)i % 4096 - 2048) + (float)((int)(1000 + i) % 4096 - 2048);
-        if (out[i] != want) {
-            fprintf(stderr, "rank %u: element %d: %g != %g\n", rank, i, out[i], want);
+        if (memcmp(&out[i], &want[i], sizeof(float)) != 0) {
+            fprintf(stderr, "rank %u: element %d: %a != %a (the plan's association)\n", rank, i,
+                    out[i], want[i]);
             ok = 0;
             break;
         }
     }
-    if (st != UCS_OK) {
+    if (fail) {
+        /* member 0 must report the injected error; the others end cleanly or
+         * by their wait timeout - a wrong result is caught above */
+        /* the error text is the failing thread's (thread-local); the count
+         * of injected failures that fired is process-wide */
+        printf("{\"rank\": %u, \"status\": %d, \"injected_fired\": %u}\n", rank, (int)st,
+               ucg_builtin_dev_inject_failure(0));
+        fflush(stdout);
+        if (rank == 0 && (st != UCS_ERR_IO_ERROR || ucg_builtin_dev_inject_failure(0) != 1)) {
+            fprintf(stderr, "rank 0: status %d, not the injected device error\n", st);
+            ok = 0;
+        }
+        if (rank != 0 && st != UCS_OK && st != UCS_ERR_TIMED_OUT) {
+            fprintf(stderr, "rank %u: status %d\n", rank, st);
+            ok = 0;
+        }
+    } else if (st != UCS_OK) {
         fprintf(stderr, "rank %u: status %d (%s)\n", rank, st,
                 (staged || device) ? ucg_builtin_dev_last_error() : "");
         ok = 0;
@@ -200,6 +269,7 @@ static int run(char **argv, const char *mode)
     }
     free(in);
     free(out);
+    free(want);
     printf("rank %u: %s\n", rank, ok ? "ok" : "FAILED");
     return ok ? 0 : 1;
 }

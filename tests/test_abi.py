@@ -105,7 +105,7 @@ def _kernel_metadata(obj):
 def test_kernel_resources():
     """Round 4: no product kernel allocates LDS, and the
     occupancy cap of the multi-operand kernels is their register allocation:
-    every capped k_reduce_multi / k_reduce_tree (last template argument 1)
+    every capped k_reduce_multi / k_reduce_tree (CAP template argument 1)
     holds at least 168 VGPRs - at most 3 waves per SIMD, 12 per CU (a few
     byte-wide kernels need more registers of their own) - while the uncapped
     fp32 / fp64 SUM forms fit more. Read from the built objects' code-object
@@ -120,9 +120,12 @@ def test_kernel_resources():
     for obj in objs:
         for name, vgpr, lds in _kernel_metadata(obj):
             assert lds == 0, (obj, name, lds)
-            m = re.match(r"_ZN6ucgdev1[34]k_reduce_(multi|tree)I([fd])?.*ELi([01])EEEv", name)
-            if m:
-                if m.group(3) == "1":
+            # template arguments T, OP, N, XM, CAP, PF, PFM: CAP is the
+            # fourth integer (round 5 added the prefetch arguments)
+            m = re.match(r"_ZN6ucgdev1[34]k_reduce_(multi|tree)I([fd])?", name)
+            ints = re.findall(r"Li(\d+)E", name)
+            if m and len(ints) == 6:
+                if ints[3] == "1":
                     capped += 1
                     assert vgpr >= 168, (name, vgpr)
                 elif m.group(2):

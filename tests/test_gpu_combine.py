@@ -473,12 +473,72 @@ def test_shareable_allocations_never_reuse_an_address(dev_ctx):
 
 
 @pytest.mark.gpu
+def test_retired_address_ranges_are_counted_and_capped(dev_ctx):
+    """the ranges that freed shareable allocations leave
+    behind are counted (ucg_builtin_dev_mem_stats) and bounded. Every churned
+    6 MiB allocation retires exactly its bytes; with the cap set just past the
+    current total, the allocation that would cross it fails with
+    UCS_ERR_EXCEEDS_LIMIT and an error that names the knob, and nothing is
+    retired by the failure."""
+    from xucg_amd import _lib
+    nbytes = 6 << 20
+    s0 = _lib.mem_stats()
+    assert s0["va_retired_max"] == 64 << 40            # the default cap, 64 TiB
+    for r in range(5):
+        b = dev_ctx.alloc(nbytes, shareable=True)
+        assert _lib.mem_stats()["shareable_live_bytes"] >= nbytes
+        b.free()
+        s = _lib.mem_stats()
+        assert s["va_retired_bytes"] == s0["va_retired_bytes"] + (r + 1) * nbytes, (r, s)
+        assert s["va_retired_ranges"] == s0["va_retired_ranges"] + r + 1
+    assert dev_ctx.counters()["va_retired_bytes"] == s["va_retired_bytes"]
+    _lib.dev().ucg_builtin_dev_set_va_retired_max(s["va_retired_bytes"] + 2 * nbytes)
+    try:
+        for _ in range(2):                             # two more fit under the cap
+            dev_ctx.alloc(nbytes, shareable=True).free()
+        with pytest.raises(MemoryError) as e:
+            dev_ctx.alloc(nbytes, shareable=True)
+        assert "UCX_BUILTIN_DEV_VA_RETIRED_MAX" in str(e.value), str(e.value)
+        assert _lib.mem_stats()["va_retired_bytes"] == s["va_retired_bytes"] + 2 * nbytes
+    finally:
+        _lib.dev().ucg_builtin_dev_set_va_retired_max(0)
+    assert _lib.mem_stats()["va_retired_max"] == 64 << 40
+    dev_ctx.alloc(nbytes, shareable=True).free()      # room again under the default
+
+
+@pytest.mark.gpu
+def test_exported_plain_memory_is_not_recycled_in_process(dev_ctx):
+    """a freed plain allocation that was exported goes back to the
+    runtime, never to the process's reuse cache, so memory a peer may still
+    read through its mapping is never handed out again here; one that was
+    never exported is kept for the next allocation of its size."""
+    from xucg_amd import _lib
+    nbytes = 6 << 20
+    a = dev_ctx.alloc(nbytes)
+    dev_ctx.ipc_export(a.ptr)
+    c0 = _lib.mem_stats()["plain_cache_bytes"]
+    a.free()
+    assert _lib.mem_stats()["plain_cache_bytes"] == c0
+    b = dev_ctx.alloc(nbytes)
+    bp = b.ptr
+    c1 = _lib.mem_stats()["plain_cache_bytes"]
+    b.free()
+    assert _lib.mem_stats()["plain_cache_bytes"] == c1 + nbytes
+    c = dev_ctx.alloc(nbytes)                          # the cached one, handed back
+    assert c.ptr == bp and _lib.mem_stats()["plain_cache_bytes"] == c1
+    c.free()
+
+
+@pytest.mark.gpu
 def test_plain_allocations_reused_whole(dev_ctx):
-    """Round 4: a freed ucg_builtin_dev_malloc allocation is
-    kept and handed out again, whole, for the next allocation of its size - the
-    same address on the same memory, never a remap - and its old key is
-    refused. 60 rounds of allocate, DMA upload, kernel read-back, free: one
-    address throughout, every read right."""
+    """Round 4: a freed ucg_builtin_dev_malloc allocation that
+    was never exported is kept and handed out again, whole, for the next
+    allocation of its size - the same address on the same memory, never a
+    remap. 60 rounds of allocate, DMA upload, kernel read-back, free: one
+    address throughout, every read right. Round 5: an exported
+    one goes back to the runtime instead (a peer may still read it), and its
+    key is refused after the free even when the runtime hands the address
+    out again."""
     n = (6 << 20) // 4
     out = dev_ctx.alloc(n * 4)
     first = None
@@ -487,7 +547,6 @@ def test_plain_allocations_reused_whole(dev_ctx):
             b = dev_ctx.alloc(n * 4)
             if first is None:
                 first = b.ptr
-                key = dev_ctx.ipc_export(b.ptr)
             assert b.ptr == first, (r, hex(b.ptr), hex(first))
             assert " R ptr" in dev_ctx.debug_ptr(b.ptr) or r == 0
             b.upload(np.full(n, r + 1, np.uint32))                 # DMA write
@@ -496,9 +555,18 @@ def test_plain_allocations_reused_whole(dev_ctx):
             got = out.download(np.uint32, n)
             assert (got == r + 1).all(), (r, int((got != r + 1).sum()))
             b.free()
+        b = dev_ctx.alloc(n * 4)
+        key = dev_ctx.ipc_export(b.ptr)
+        pb = b.ptr
+        b.free()
+        assert f" F ptr 0x{pb:x}" in dev_ctx.debug_ptr(pb)
+        c = dev_ctx.alloc(n * 4)          # never the exported one, from the cache
+        after_free = dev_ctx.debug_ptr(pb).split(f" F ptr 0x{pb:x}")[-1]
+        assert f" R ptr 0x{pb:x}" not in after_free, after_free
         with pytest.raises(xucg_amd.UcsError) as e:
             dev_ctx.ipc_import(key)
         assert e.value.status == -2
+        c.free()
     finally:
         out.free()
 

@@ -306,6 +306,46 @@ def test_bench_collective_phases_rehearsal_on_one_gpu(world):
 
 
 @pytest.mark.gpu
+def test_c4_full_size_8_ranks_on_one_gpu():
+    """BASELINE config 4 at full size with 8 members: the
+    one-shot pull and push reduce-scatter, all-gather and allreduce of a 4 GiB
+    fp32 buffer per member (8 x 4 GiB plus stages and outputs, about 104 GiB
+    of the one GPU's 288 GB), through the IPC peer mappings, every result
+    bit-exact against the plan's association on sampled windows of every
+    shard (bench.PlanWindows; builtin_recursive.c:158-169), exact and rounded
+    inputs. The gloo stand-in's 4 GiB vendor legs are skipped (they do not
+    fit its host staging); the phase's wall time is recorded."""
+    import importlib
+    import json
+    import tempfile
+    import uuid
+    bench = importlib.import_module("bench")
+    out = os.path.join(tempfile.gettempdir(), f"xucg_c4full_{uuid.uuid4().hex}.json")
+    phase = "c4_oneshot_xgmi_rs_4gib_fp32"
+    codes, outs = launch("../bench.py", 8, args=("--collective-child",), timeout=280,
+                         env_extra={"LOCAL_RANK": "0", "XUCG_COLLECTIVE_BACKEND": "gloo",
+                                    "XUCG_COLLECTIVE_SCALE": "1", "XUCG_COLLECTIVE_OUT": out,
+                                    "XUCG_COLLECTIVE_PHASES": phase})
+    assert codes == [0] * 8, "\n".join(o[-3000:] for o in outs)
+    with open(out) as f:
+        res = json.load(f)
+    os.unlink(out)
+    print(json.dumps({"phase_wall_s": res["phase_wall_s"], "wall_s": res["wall_s"]}))
+    assert res["rehearsal"]["size_divisor"] == 1 and res["rehearsal"]["vendor_legs"] is False
+    assert bench.collective_failures(res) == [], json.dumps(res)[:3000]
+    c4 = res[phase]
+    assert c4["bytes"] == 4 << 30
+    for k in ("oneshot_rs_bit_exact_vs_host_plan_sampled_exact",
+              "oneshot_ag_bit_exact_vs_host_plan_sampled",
+              "oneshot_allreduce_bit_exact_vs_host_plan_sampled",
+              "push_rs_bit_exact_vs_host_plan_sampled",
+              "push_allreduce_bit_exact_vs_host_plan_sampled",
+              "oneshot_rs_bit_exact_vs_host_plan_sampled_rounded"):
+        assert c4[k] is True, (k, c4)
+    assert res["phase_wall_s"][phase] < 240, res["phase_wall_s"]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mode", ["oneshot", "steps"])
 def test_c5_engine_512mib_fp64_sampled_oracle(mode):
     """BASELINE config 5 at full size per member (512 MiB fp64), 8 members on

@@ -143,9 +143,26 @@ def test_async_resend_timer_combines_on_its_thread():
     assert stats["timer_resends"] > 0 and stats["timer_combines"] > 0
 
 
+def test_async_resend_timer_four_members_rounded_inputs():
+    """Row a15 at 4 members with rounded fp32 inputs: the
+    timer thread sends member 0's step-1 fragments and combines the stash;
+    every member's result equals, bit for bit, the oracle's simulation of the
+    recursive-doubling plan (ucg_oracle_reduce_multi; builtin_recursive.c:
+    158-169) - exact small-integer inputs could not tell an association
+    error apart."""
+    exe = os.path.join(ROOT, "tests", "c", "_build", "async_resend")
+    codes, outs = launch_exe(exe, 4, (shm_name(), "host", "round"), timeout=60)
+    assert codes == [0] * 4, "\n".join(outs)
+    import json
+    stats = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][0])
+    assert stats["world"] == 4 and stats["inputs"] == "round"
+    assert stats["sent_after_sleep"] >= 133 and stats["timer_combines"] > 0, stats
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["staged", "device"])
-def test_async_resend_timer_device_combines(mode):
+@pytest.mark.parametrize("mode,world,inputs", [("staged", 2, "exact"), ("device", 2, "exact"),
+                                               ("staged", 4, "round"), ("device", 4, "round")])
+def test_async_resend_timer_device_combines(mode, world, inputs):
     """Row a15 on the GPU: the resend timer's thread makes
     the combine's HIP calls. staged: host buffers with every step staged on
     the device, so the fragments the timer thread drains are device combines
@@ -153,13 +170,35 @@ def test_async_resend_timer_device_combines(mode):
     steps, member 0's fold launched from its timer thread once its stuck
     messages go out. Results bit-exact, no host combine, no device error."""
     exe = os.path.join(ROOT, "tests", "c", "_build", "async_resend")
-    codes, outs = launch_exe(exe, 2, (shm_name(), mode), timeout=90)
-    assert codes == [0, 0], "\n".join(outs)
+    codes, outs = launch_exe(exe, world, (shm_name(), mode, inputs), timeout=90)
+    assert codes == [0] * world, "\n".join(outs)
     import json
     stats = json.loads([ln for ln in outs[0].splitlines() if ln.startswith("{")][0])
-    assert stats["mode"] == mode
+    assert stats["mode"] == mode and stats["world"] == world and stats["inputs"] == inputs
     assert stats["timer_resends"] > 0 and stats["timer_combines"] > 0, stats
     assert stats["host_calls"] == 0 and stats["device_calls"] > 0, stats
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["staged", "device"])
+def test_async_resend_timer_device_failure_reaches_completion(monkeypatch, mode):
+    """the timer thread's device combine fails (the next
+    device call of member 0's process armed with
+    ucg_builtin_dev_inject_failure just before its owner thread goes quiet):
+    member 0's operation completes with that error, UCS_ERR_IO_ERROR, as the
+    reference's recv_handle_error path ends an op (builtin_comp_step.inl:
+    332-333, builtin.c:260-294); member 1 ends cleanly or by its wait
+    timeout, never with a wrong result."""
+    # member 1 may wait for fragments member 0 dropped with its op: its wait
+    # gives up after 20 s (its start-up, HIP init included, fits well inside)
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "20")
+    exe = os.path.join(ROOT, "tests", "c", "_build", "async_resend")
+    codes, outs = launch_exe(exe, 2, (shm_name(), mode, "round", "fail"), timeout=120)
+    assert codes == [0, 0], "\n".join(outs)
+    import json
+    lines = [json.loads(ln) for ln in outs[0].splitlines() if ln.startswith("{")]
+    st0 = [x for x in lines if "status" in x][0]
+    assert st0["rank"] == 0 and st0["status"] == -3 and st0["injected_fired"] == 1, st0
 
 
 @pytest.mark.parametrize("exe,world,args", [("component_test", 4, ("host",)),

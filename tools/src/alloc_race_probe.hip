@@ -21,7 +21,7 @@
  *
  * Prints one line: iterations, buffers whose content changed after the
  * verified upload (and how many of those read as all zeros).
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

@@ -6,7 +6,7 @@
  *
  *   tune_alloc [trials = 4]
  *
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

@@ -17,7 +17,7 @@
  * `joint`: operands and output carved out of one allocation, back to back
  * (bench.py's one_shot_shape layout) instead of one allocation each.
  *
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

@@ -7,7 +7,7 @@
  *
  *   tune_copy [log2 bytes = 28] [rounds = 5]
  *
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

@@ -10,7 +10,7 @@
  *
  *   tune_misalign [rounds = 5]
  *
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

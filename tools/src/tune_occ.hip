@@ -8,7 +8,7 @@
  *
  *   tune_occ [log2 elements per operand = 24] [rounds = 5]
  *
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

@@ -16,7 +16,7 @@
  * Also reported: what the runtime says about a VMM pointer (address range,
  * buffer id, legacy IPC handle), and the 2 x 256 MiB fp32 combine
  * (k_reduce) on hipMalloc memory vs VMM memory, one and two allocations.
- * Built by `make -C xucg_amd/csrc tune` into tools/ (not part of the product).
+ * Built by `make -C tools/src` into tools/ (not part of the product).
  */
 #include <hip/hip_runtime.h>
 

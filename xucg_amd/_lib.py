@@ -34,6 +34,7 @@ UCS_ERR_BUSY = -15
 UCS_ERR_CANCELED = -16
 UCS_ERR_OUT_OF_RANGE = -19
 UCS_ERR_TIMED_OUT = -20
+UCS_ERR_EXCEEDS_LIMIT = -21
 UCS_ERR_UNSUPPORTED = -22
 IPC_HANDLE_BYTES = 96  # UCG_BUILTIN_DEV_IPC_HANDLE_BYTES
 
@@ -54,6 +55,9 @@ class DevCtxParams(ctypes.Structure):
 
 ZCOPY_NEVER = (1 << 64) - 1   # UCG_BUILTIN_DEV_ZCOPY_NEVER
 NCOUNTERS = 6                 # UCG_BUILTIN_DEV_NCOUNTERS
+NMEMSTATS = 6                 # UCG_BUILTIN_DEV_NMEMSTATS
+MEMSTATS = ["va_retired_bytes", "va_retired_ranges", "va_retired_max",
+            "plain_cache_bytes", "shareable_live_bytes", "shareable_import_bytes"]
 COMPLETION = {"signal": 1, "sync": 2}   # UCG_BUILTIN_DEV_COMPLETION_*
 
 
@@ -104,7 +108,19 @@ DEV_API = {
     "ucg_builtin_dev_profile_stream": (_st, [_vp, _int, _vp, _vp, _sz, _u,
                                              ctypes.POINTER(ctypes.c_double)]),
     "ucg_builtin_dev_counters": (None, [_vp, ctypes.POINTER(_u64)]),
+    "ucg_builtin_dev_mem_stats": (None, [ctypes.POINTER(_u64)]),
+    "ucg_builtin_dev_set_va_retired_max": (None, [_u64]),
+    "ucg_builtin_dev_inject_failure": (_u, [_u]),
 }
+
+
+def mem_stats():
+    """The shim's process-wide memory accounting (ucg_builtin_dev_mem_stats):
+    retired address ranges and their cap, the reuse cache, live shareable
+    allocations and imports, as a dict of MEMSTATS."""
+    out = (_u64 * NMEMSTATS)()
+    dev().ucg_builtin_dev_mem_stats(out)
+    return dict(zip(MEMSTATS, list(out)))
 
 _dev = None
 _host = None

@@ -175,18 +175,17 @@ static size_t shm_key_bytes(const void *key)
 }
 
 /* UCX_BUILTIN_DEV_POOL_BYTES (default 32 MiB, 0 = none): the device arena
- * made with a group that has a device, out of which its registered buffers
- * are carved while it lasts */
+ * out of which a group's registered buffers are carved while it lasts. It is
+ * made on the group's first device-buffer (remote-key) buffer, not with the
+ * group: a group that never runs a device-buffer step costs no HBM (ADVICE
+ * r04). arena_bytes holds the size still to make while arena is NULL. */
 UCG_INTERNAL void rma_group_init(ucg_builtin_lgroup_t *g)
 {
     const size_t bytes = parse_memunits(getenv("UCX_BUILTIN_DEV_POOL_BYTES"),
                                         (size_t)32 << 20);
     g->arena = NULL;
-    g->arena_bytes = g->arena_used = 0;
-    if (bytes && ucg_builtin_combine_has_device(g->cmb)) {
-        g->arena = ucg_builtin_combine_dev_alloc(g->cmb, bytes);
-        g->arena_bytes = g->arena ? bytes : 0;
-    }
+    g->arena_used = 0;
+    g->arena_bytes = (bytes && ucg_builtin_combine_has_device(g->cmb)) ? bytes : 0;
 }
 
 /* registered buffers come in size classes - at least 64 KiB, eight per
@@ -239,10 +238,17 @@ static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
         p->ptr = shm_seg_alloc(bytes, p->key);
         return p->ptr ? (int)g->npool++ : -1;
     }
+    if (g->arena == NULL && g->arena_bytes) {
+        /* the group's first device buffer: make the arena now (once; a
+         * failure leaves the group without one) */
+        g->arena = ucg_builtin_combine_dev_alloc(g->cmb, g->arena_bytes);
+        if (g->arena == NULL) {
+            g->arena_bytes = 0;
+        }
+    }
     if (g->arena && g->arena_used + bytes <= g->arena_bytes) {
-        /* from the arena made with the group: no allocation on the op path
-         * (the zeroed fresh allocations), and the peers map the
-         * whole arena once (one key, offsets) */
+        /* from the group's arena: one allocation per group, not one per
+         * buffer, and the peers map the whole arena once (one key, offsets) */
         p->ptr = (char*)g->arena + g->arena_used;
         p->in_arena = 1;
         g->arena_used += bytes;
@@ -303,10 +309,15 @@ static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
 }
 
 /* Group destroy is collective but not synchronised: a peer may still map this
- * member's pool buffers when they are given back here. Pool buffers are
- * shareable allocations (ucg_builtin_dev_malloc_shareable): a peer's mapping
- * holds the physical memory until the peer releases it, and the free retires
- * the buffers' keys, so a later group can never map them by an old key.
+ * member's pool buffers when they are given back here, and a buffer rma_free
+ * left taken (a timeout, an error, a destroy while running) may still be read.
+ * Pool buffers and the arena are exported device memory - hipMalloc memory
+ * with hipIpc keys by default, shareable allocations with
+ * UCX_BUILTIN_DEV_POOL_MEM=shareable - and ucg_builtin_dev_free gives exported
+ * memory back to the runtime, never to the process's reuse cache: a peer's
+ * mapping holds the physical memory until the peer releases it, so nothing of
+ * this process can be handed that memory while the peer still reads it, and
+ * the free retires the keys, so a later group can never map it by an old key.
  * Shared-memory segments stay alive for the peers that map them. */
 UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
 {

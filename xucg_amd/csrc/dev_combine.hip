@@ -106,6 +106,17 @@ bool multi_capped()
 }
 }  // namespace ucgdev
 
+/* ucg_builtin_dev_inject_failure: device calls left before the injected
+ * failure (0 = none armed). Test-only; one relaxed load per call otherwise. */
+static std::atomic<int64_t> g_inject_after{0};
+static std::atomic<unsigned> g_inject_fired{0};
+
+unsigned ucg_builtin_dev_inject_failure(unsigned after)
+{
+    g_inject_after.store((int64_t)after);
+    return g_inject_fired.load();
+}
+
 void ucg_builtin_dev_set_multi_cap(int capped)
 {
     g_multi_cap_override.store(capped < 0 ? -1 : (capped != 0), std::memory_order_relaxed);
@@ -582,11 +593,27 @@ ucs_status_t ucg_builtin_dev_complete(ucg_builtin_dev_ctx_t *ctx)
     return stream_complete(ctx, true);
 }
 
+static bool injected_failure()
+{
+    if (g_inject_after.load(std::memory_order_relaxed) <= 0) {
+        return false;
+    }
+    if (g_inject_after.fetch_sub(1) != 1) {
+        return false;
+    }
+    g_inject_fired++;
+    return true;
+}
+
 static ucs_status_t check_args(ucg_builtin_dev_ctx_t *ctx, ucg_dev_op_t op,
                                ucg_dev_dtype_t dt, const char *what)
 {
     if (ctx == nullptr) {
         return set_error(UCS_ERR_INVALID_PARAM, what, "ctx is NULL");
+    }
+    if (injected_failure()) {
+        return set_error(UCS_ERR_IO_ERROR, what,
+                         "injected device error (ucg_builtin_dev_inject_failure)");
     }
     if (!ucg_builtin_dev_is_supported(dt, op)) {
         return set_error(UCS_ERR_UNSUPPORTED, what,

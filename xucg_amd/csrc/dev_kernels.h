@@ -324,7 +324,37 @@ __device__ __forceinline__ E rd_tree(E (&val)[N], F f)
     return val[0];
 }
 
-template <typename T, int OP, int N, int XM = 0, int CAP = 0>
+/* The next-tile prefetch of k_reduce's PF form, for the in-phase multi-operand
+ * kernels (k_reduce_multi, k_reduce_tree): with the XCD-aware tile map, the
+ * last PF lanes of a wave load the first PF 128-B lines of the next tile of
+ * each of the operands `ops[0 .. PFM)` with temporal loads and discard them;
+ * every other lane reloads the operand's last vector (one line, an L2 hit),
+ * so no branch separates the loads. The loads are issued with the tile's own
+ * and kept alive by an empty asm after the sched barrier. */
+template <int PF, int PFM>
+__device__ __forceinline__ void next_tile_lines(const u32x4 *const (&ops)[PFM > 0 ? PFM : 1],
+                                                size_t i, size_t nvec)
+{
+    if constexpr (PF > 0 && PFM > 0) {
+        const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+        const size_t want = (i - threadIdx.x + kReduceBlock) + (size_t)k * 8;
+        const size_t at   = (k < (unsigned)PF && want < nvec) ? want : nvec - 1;
+        u32x4 pf[PFM];
+#pragma unroll
+        for (int m = 0; m < PFM; m++) {
+            pf[m] = ld16<0>(ops[m] + at);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < PFM; m++) {
+            asm volatile("" :: "v"(pf[m][0]));    /* the load stays; its value is unused */
+        }
+    } else {
+        (void)ops; (void)i; (void)nvec;
+    }
+}
+
+template <typename T, int OP, int N, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                size_t tail)
@@ -358,6 +388,34 @@ k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
     }
 
     u32x4 *d4 = reinterpret_cast<u32x4*>(dst + head);
+    if constexpr (PF > 0) {
+        /* PF form: always on the XCD tile map, loads clamped and unmasked
+         * (one tile of one vector per lane, kMultiU == 1) */
+        static_assert(kMultiU == 1 && PFM <= N, "one vector per lane; prefetch operands <= N");
+        if (nvec == 0) {
+            return;
+        }
+        const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                          threadIdx.x;
+        const size_t ic = i < nvec ? i : nvec - 1;
+        const u32x4 *op[N];
+        u32x4 val[N];
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            op[m]  = reinterpret_cast<const u32x4*>(static_cast<const T*>(srcs.p[self ^ m]) + head);
+            val[m] = ld16<1>(op[m] + ic);
+        }
+        const u32x4 *pops[PFM > 0 ? PFM : 1];
+#pragma unroll
+        for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
+            pops[m] = op[m];
+        }
+        next_tile_lines<PF, PFM>(pops, i, nvec);
+        if (i < nvec) {
+            st16<1>(d4 + i, rd_tree<N>(val, fv));
+        }
+        return;
+    }
     const size_t tile = XM ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x;
     const size_t base = tile * (kReduceBlock * kMultiU) + threadIdx.x;
 #pragma unroll
@@ -488,7 +546,7 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
  * two, and for MPI_Reduce). Operands past n load srcs[0] again (an L2 hit,
  * no branch between the loads) and are not combined.
  */
-template <typename T, int OP, int NMAX, int XM = 0, int CAP = 0>
+template <typename T, int OP, int NMAX, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
 {
@@ -515,6 +573,43 @@ k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t
             }
             dst[j] = acc;
         }
+    }
+
+    if constexpr (PF > 0) {
+        /* PF form (see k_reduce_multi): XCD tile map, clamped unmasked loads,
+         * the first PFM operands' next-tile lines loaded ahead */
+        static_assert(PFM <= NMAX, "prefetch operands <= NMAX");
+        if (nvec == 0) {
+            return;
+        }
+        const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                          threadIdx.x;
+        const size_t ic = i < nvec ? i : nvec - 1;
+        const u32x4 *op[NMAX];
+        u32x4 val[NMAX];
+#pragma unroll
+        for (int m = 0; m < NMAX; m++) {
+            op[m]  = reinterpret_cast<const u32x4*>(
+                static_cast<const T*>(srcs.p[(unsigned)m < n ? m : 0]) + head);
+            val[m] = ld16<1>(op[m] + ic);
+        }
+        const u32x4 *pops[PFM > 0 ? PFM : 1];
+#pragma unroll
+        for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
+            pops[m] = op[m];
+        }
+        next_tile_lines<PF, PFM>(pops, i, nvec);
+        if (i < nvec) {
+            u32x4 acc = val[0];
+#pragma unroll
+            for (int m = 1; m < NMAX; m++) {
+                if ((unsigned)m < n) {
+                    acc = vapply<T, OP>(val[m], acc);
+                }
+            }
+            st16<1>(reinterpret_cast<u32x4*>(dst + head) + i, acc);
+        }
+        return;
     }
 
     const size_t i = (XM ? xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) : blockIdx.x) *

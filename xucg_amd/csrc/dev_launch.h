@@ -80,6 +80,18 @@ inline bool straddles_lines(const void *p)
  * ahead (k_reduce's PF form) */
 constexpr int kPrefetchLines = 3;
 
+/* The in-phase multi-operand kernels' PF form (round 5):
+ * one line of the next tile per prefetched operand (tools/tune_multi_pf,
+ * profiles/r05/pf, 64 MiB per operand, A/B in one process): N = 8 and 16,
+ * every operand: 82.3 / 81.2 % of 8 TB/s against 79.7 / 80.5 % for round
+ * 4's form (three lines: 82.5 % at 64 MiB but 74.3 % at 256 MiB); N = 4
+ * lost 5 points with any prefetch and keeps round 4's form. Tree fan-in:
+ * n = NMAX (8, 16) every operand, 85.0 % against 80.5 % at n = 8; otherwise
+ * the root's operand only, 83.0 % against 77.7 % at n = 3 and 82.4 against
+ * 80.5 % at n = 12 (operands past n reload the root's, so prefetching them
+ * fetches its lines again: n = 6 read 78.4 % with every operand). */
+constexpr int kMultiPrefetchLines = 1;
+
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
@@ -241,7 +253,20 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
             const dim3 g(grid), b(kReduceBlock);
-            if (cap) {
+            if constexpr (N >= 8) {
+                if (cap) {
+                    /* the PF form: XCD map, the next tile's line of every operand */
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N>),
+                                       g, b, 0, st, d + off, sl, self, h, chunk, t);
+                } else if constexpr (uncapped_ab<T, OP>()) {
+                    if (xm)
+                        hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 0>), g, b, 0, st,
+                                           d + off, sl, self, h, chunk, t);
+                    else
+                        hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 0, 0>), g, b, 0, st,
+                                           d + off, sl, self, h, chunk, t);
+                }
+            } else if (cap) {
                 if (xm)
                     hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, can_cap>), g, b, 0, st,
                                        d + off, sl, self, h, chunk, t);
@@ -353,14 +378,21 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
             const dim3 g(grid), b(kReduceBlock);
-            if (cap) {
-                if (xm)
-                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, can_cap>), g, b, 0, st,
+            constexpr int L = kMultiPrefetchLines;
+            if constexpr (!can_cap) {
+                /* the PF form: the root's next line */
+                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 0, L, 1>), g, b, 0, st,
+                                   d + off, sl, n, h, chunk, t);
+            } else if (cap) {
+                /* the PF form, capped: every operand's next line when n fills
+                 * NMAX, else the root's only */
+                if (n == (unsigned)NMAX)
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);
                 else
-                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 0, can_cap>), g, b, 0, st,
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, 1>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);
-            } else if constexpr (!can_cap || uncapped_ab<T, OP>()) {
+            } else if constexpr (uncapped_ab<T, OP>()) {
                 if (xm)
                     hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 0>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);

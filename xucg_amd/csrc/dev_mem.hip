@@ -104,6 +104,24 @@ size_t plain_cache_limit()
     return lim;
 }
 
+/* give every cached allocation back to the runtime (hipMalloc ran out of
+ * memory: the cache may hold what it needs, at other sizes); returns how
+ * many. Caller does not hold g_mu. */
+size_t plain_cache_drain()
+{
+    std::multimap<std::pair<int, size_t>, void*> all;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        all.swap(g_plain_cache);
+        g_plain_cached = 0;
+    }
+    for (auto &kv : all) {
+        (void)hipSetDevice(kv.first.first);
+        (void)hipFree(kv.second);
+    }
+    return all.size();
+}
+
 /* The last memory events of the process, for ucg_builtin_dev_debug_ptr: a
  * buffer found to read as zeros is matched against what happened to its
  * address range. */
@@ -503,8 +521,14 @@ hipError_t import_fd(hipMemGenericAllocationHandle_t *h, int fd, int device)
 }
 
 /* map an imported VMM allocation (fd) at a new reservation of this process */
+ucs_status_t va_room(size_t bytes, const char *what);
+
 ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
 {
+    const ucs_status_t room = va_room(size, "ipc_import");
+    if (room != UCS_OK) {
+        return room;
+    }
     hipMemGenericAllocationHandle_t h;
     HIP_TRY(import_fd(&h, fd, device));
     void *va = nullptr;
@@ -538,16 +562,74 @@ ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
  * translations: peers read the previous allocation's data, or zeros, through
  * a fresh mapping of a new allocation at an old address
  * (tools/va_reuse_probe). So an allocation or import, once
- * unmapped, leaves its reservation behind: the process's virtual address
- * space (128 TiB) absorbs that, physical memory goes back at once. */
+ * unmapped, leaves its reservation behind; physical memory goes back at once.
+ * The retired ranges are counted (ucg_builtin_dev_mem_stats) and bounded
+ * (round 5): past UCX_BUILTIN_DEV_VA_RETIRED_MAX (default
+ * 64 TiB, half of the 128 TiB a process's GPU virtual address space spans)
+ * a new shareable allocation or import fails with UCS_ERR_EXCEEDS_LIMIT
+ * instead of running the address space out; half-way there a warning is
+ * printed once. */
 std::atomic<uint64_t> g_va_retired{0};
+std::atomic<uint64_t> g_va_retired_ranges{0};
+std::atomic<uint64_t> g_va_retired_max_set{0};        /* 0: the environment's */
+std::atomic<bool>     g_va_warned{false};
+
+uint64_t va_retired_max()
+{
+    const uint64_t set = g_va_retired_max_set.load(std::memory_order_relaxed);
+    if (set) {
+        return set;
+    }
+    static const uint64_t lim = [] {
+        const char *e = getenv("UCX_BUILTIN_DEV_VA_RETIRED_MAX");
+        const uint64_t dflt = (uint64_t)64 << 40;
+        if (e == nullptr || *e == 0) {
+            return dflt;
+        }
+        char *end = nullptr;
+        double v = strtod(e, &end);
+        if (end && (*end == 'k' || *end == 'K')) v *= 1024.0;
+        else if (end && (*end == 'm' || *end == 'M')) v *= 1048576.0;
+        else if (end && (*end == 'g' || *end == 'G')) v *= 1073741824.0;
+        else if (end && (*end == 't' || *end == 'T')) v *= 1099511627776.0;
+        return v > 0 ? (uint64_t)v : dflt;
+    }();
+    return lim;
+}
+
+/* may a new range of `bytes` be reserved? (UCS_ERR_EXCEEDS_LIMIT, named, if
+ * the retired ranges are past the cap) */
+ucs_status_t va_room(size_t bytes, const char *what)
+{
+    const uint64_t r = g_va_retired.load(std::memory_order_relaxed), cap = va_retired_max();
+    if (r + bytes > cap) {
+        char b[200];
+        snprintf(b, sizeof(b), "retired address ranges %llu B + %zu B past "
+                 "UCX_BUILTIN_DEV_VA_RETIRED_MAX %llu B (never-remapped ranges, DESIGN.md 6)",
+                 (unsigned long long)r, bytes, (unsigned long long)cap);
+        return set_error(UCS_ERR_EXCEEDS_LIMIT, what, b);
+    }
+    return UCS_OK;
+}
+
+void va_retire(size_t bytes)
+{
+    const uint64_t r = g_va_retired.fetch_add(bytes) + bytes;
+    g_va_retired_ranges++;
+    if (r > va_retired_max() / 2 && !g_va_warned.exchange(true)) {
+        fprintf(stderr, "xucg: %llu B of GPU virtual address space retired by unmapped "
+                "shareable allocations and imports, past half of "
+                "UCX_BUILTIN_DEV_VA_RETIRED_MAX (%llu B)\n", (unsigned long long)r,
+                (unsigned long long)va_retired_max());
+    }
+}
 
 void unmap_import(import_rec &m)
 {
     if (m.kind == KIND_VMM) {
         (void)hipMemUnmap(m.base, m.size);
         (void)hipMemRelease(m.handle);
-        g_va_retired += m.size;
+        va_retire(m.size);
     } else if (m.kind == KIND_PLAIN) {
         (void)hipIpcCloseMemHandle(m.base);
     }
@@ -846,7 +928,12 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
             return p;
         }
     }
-    const hipError_t e = hipMalloc(&p, bytes);
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e == hipErrorOutOfMemory && plain_cache_drain() > 0) {
+        /* the reuse cache held memory of other sizes: given back, once more */
+        (void)hipGetLastError();
+        e = hipMalloc(&p, bytes);
+    }
     if (e != hipSuccess) {
         hip_status(e, "hipMalloc");
         return nullptr;
@@ -874,6 +961,9 @@ void *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         (void)hipGetDevice(&device);
     }
     bytes = round_gran(bytes);
+    if (va_room(bytes, "malloc_shareable") != UCS_OK) {
+        return nullptr;
+    }
     hipMemAllocationProp prop;
     memset(&prop, 0, sizeof(prop));
     prop.type = hipMemAllocationTypePinned;
@@ -930,7 +1020,7 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         return;
     }
     own_alloc a;
-    bool own = false;
+    bool own = false, exported = false;
     int fd = -1;
     {
         std::lock_guard<std::mutex> g(g_mu);
@@ -943,6 +1033,7 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         /* retire its key: a peer's import of it is refused from now on */
         auto ex = g_export_of.find(ptr);
         if (ex != g_export_of.end()) {
+            exported = true;
             fd = g_exports[ex->second].fd;
             g_exports.erase(ex->second);
             g_export_of.erase(ex);
@@ -962,14 +1053,19 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         e = hipDeviceSynchronize();
         (void)hipMemUnmap(ptr, a.bytes);
         (void)hipMemRelease(a.handle);
-        g_va_retired += a.bytes;           /* the range is never reused */
+        va_retire(a.bytes);                /* the range is never reused */
     } else if (own && a.kind == KIND_PLAIN) {
         /* as hipFree does: nothing queued may still use it; then kept for
-         * the next allocation of its size (g_plain_cache) */
+         * the next allocation of its size (g_plain_cache) - unless it was
+         * exported: a peer may still map it (a group destroyed while a peer
+         * reads, a buffer left taken after a timeout), and memory handed out
+         * again here would change under that reader. Given back to the
+         * runtime instead, the peer's mapping keeps the old physical memory
+         * (ADVICE r04). */
         (void)hipSetDevice(a.device);
         e = hipDeviceSynchronize();
         bool kept = false;
-        {
+        if (!exported) {
             std::lock_guard<std::mutex> g(g_mu);
             if (g_plain_cached + a.bytes <= plain_cache_limit()) {
                 g_plain_cache.emplace(std::make_pair(a.device, a.bytes), ptr);
@@ -985,6 +1081,37 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
     }
     std::lock_guard<std::mutex> g(g_mu);
     note_event('F', ptr, ptr, own ? a.bytes : 0, (int)e);
+}
+
+void ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS])
+{
+    if (out == nullptr) {
+        return;
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    uint64_t live_vmm = 0, live_imp = 0;
+    for (const auto &kv : g_allocs) {
+        if (kv.second.kind == KIND_VMM) {
+            live_vmm += kv.second.bytes;
+        }
+    }
+    for (const auto &kv : g_imports) {
+        if (kv.second.kind == KIND_VMM) {
+            live_imp += kv.second.size;
+        }
+    }
+    out[0] = g_va_retired.load();
+    out[1] = g_va_retired_ranges.load();
+    out[2] = va_retired_max();
+    out[3] = g_plain_cached;
+    out[4] = live_vmm;
+    out[5] = live_imp;
+}
+
+void ucg_builtin_dev_set_va_retired_max(uint64_t bytes)
+{
+    g_va_retired_max_set.store(bytes);
+    g_va_warned.store(false);
 }
 
 /* torch.cuda.memory.CUDAPluggableAllocator entry points: every tensor of a

@@ -285,8 +285,12 @@ class DevContext:
     def counters(self):
         out = (ctypes.c_uint64 * _lib.NCOUNTERS)()
         _lib.dev().ucg_builtin_dev_counters(self.handle, out)
-        return {"launches": out[0], "combined_bytes": out[1], "h2d_bytes": out[2],
-                "d2h_bytes": out[3], "zcopy_bytes": out[4], "signal_waits": out[5]}
+        c = {"launches": out[0], "combined_bytes": out[1], "h2d_bytes": out[2],
+             "d2h_bytes": out[3], "zcopy_bytes": out[4], "signal_waits": out[5]}
+        # the process-wide accounting beside the context's own (retired
+        # address ranges and their cap: ucg_builtin_dev_mem_stats)
+        c.update(_lib.mem_stats())
+        return c
 
 
 def use_shareable_torch_memory():
