@@ -36,16 +36,38 @@ def load_baseline_metric():
         return json.load(f)["metric"]
 
 
+def lib_sha16(path):
+    """first 16 hex digits of the sha256 of a file (None if unreadable)"""
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
 def pmc_traffic(count):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary (or None)."""
+    """HBM bytes per launch from the committed rocprofv3 PMC summary
+    (profiles/pmc_traffic.json), and where it comes from: the profile, the
+    library it was measured on and whether that is the library loaded now
+    (stale when they differ: the figure is then an older library's). Not a
+    measurement of this run - PMC counters need their own profiler passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    from xucg_amd import _lib
+    loaded = lib_sha16(_lib.DEV_LIB)
     try:
         with open(path) as f:
-            d = json.load(f)
-        e = d.get(str(count))
-        return None if e is None else e.get("hbm_bytes_per_launch")
+            e = json.load(f).get(str(count))
     except (OSError, ValueError):
-        return None
+        e = None
+    if e is None:
+        return None, {"profile": None, "stale": True, "lib_sha16_loaded": loaded}
+    measured = e.get("lib_sha16")
+    return e.get("hbm_bytes_per_launch"), {
+        "profile": "profiles/pmc_traffic.json <- " + str(e.get("source")),
+        "kind": "committed rocprofv3 PMC summary (FETCH_SIZE x 2 + WRITE_SIZE), not this run",
+        "lib_sha16_profiled": measured, "lib_sha16_loaded": loaded,
+        "stale": measured is None or measured != loaded}
 
 
 def cpu_baseline(count, budget_s=10.0):
@@ -1492,6 +1514,7 @@ def main():
     sa.free()
     sd.free()
 
+    traffic, traffic_source = pmc_traffic(n)
     extra = {}
     if not args.no_extra and rank == 0:
         # north-star: 1 GiB fp32 combine, device-resident
@@ -1573,7 +1596,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(n),
+                "traffic": traffic,
+                "traffic_source": traffic_source,
                 "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64, XM=1, PF=3>",
                 "kernel_avg_us": round(avg_us, 3),
                 "kernel_avg_us_batches": [round(b, 2) for b in batch_us],
@@ -1590,6 +1614,10 @@ def main():
                             "stores / src copied to dst (ucg_builtin_dev_profile_stream)"},
             },
             "cpu_baseline": cpu,
+            # the shim's process-wide memory accounting at the end of the run:
+            # retired address ranges and their cap, the reuse cache
+            # (ucg_builtin_dev_mem_stats)
+            "shim_memory": xucg_amd._lib.mem_stats(),
             "extra": extra,
             "collective": collective,
         }

@@ -157,6 +157,9 @@ int          ucg_builtin_combine_step_on_device(ucg_builtin_combine_t *cmb);
  * the combine's lock and returns once the device work is complete. */
 void        *ucg_builtin_combine_dev_alloc(ucg_builtin_combine_t *cmb, size_t bytes);
 void         ucg_builtin_combine_dev_free(ucg_builtin_combine_t *cmb, void *ptr);
+/* keep an exported buffer a peer may still read: keys retired, memory never
+ * reused (ucg_builtin_dev_park) */
+void         ucg_builtin_combine_dev_park(ucg_builtin_combine_t *cmb, void *ptr);
 ucs_status_t ucg_builtin_combine_dev_export(ucg_builtin_combine_t *cmb,
                                             const void *dev_ptr, void *handle);
 ucs_status_t ucg_builtin_combine_dev_import(ucg_builtin_combine_t *cmb,

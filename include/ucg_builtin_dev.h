@@ -323,8 +323,17 @@ void        *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t
 /* 1 when ptr lies in a live allocation of ucg_builtin_dev_malloc_shareable */
 int          ucg_builtin_dev_is_shareable(const void *ptr);
 /* Frees either kind (waits for the device first, as hipFree does) and
- * retires the allocation's keys; a pointer of neither is hipFree'd. */
+ * retires the allocation's keys; a pointer of neither is hipFree'd. A freed
+ * ucg_builtin_dev_malloc allocation is kept for the next allocation of its
+ * size (UCX_BUILTIN_DEV_CACHE_BYTES), so its address never comes back from
+ * the runtime with other memory behind it. */
 void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);
+/* For an allocation of this shim that a peer may still be reading (an op
+ * that ended before every peer was done: a timeout, an error, a destroy
+ * while running): retires its keys and keeps the memory allocated, never
+ * handed out again, for the life of the process (ucg_builtin_dev_mem_stats
+ * [6] counts it). */
+void         ucg_builtin_dev_park(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 /* torch.cuda.memory.CUDAPluggableAllocator entry points over
  * ucg_builtin_dev_malloc_shareable / ucg_builtin_dev_free, so that every
  * tensor of a process can be exported by its physical allocation. */
@@ -368,11 +377,12 @@ unsigned     ucg_builtin_dev_inject_failure(unsigned after);
  *   [2] the cap on [0]: past it a new shareable allocation or import fails
  *       with UCS_ERR_EXCEEDS_LIMIT (UCX_BUILTIN_DEV_VA_RETIRED_MAX, default
  *       64 TiB, or ucg_builtin_dev_set_va_retired_max);
- *   [3] bytes held by the reuse cache of freed, never-exported
- *       ucg_builtin_dev_malloc allocations (UCX_BUILTIN_DEV_CACHE_BYTES);
+ *   [3] bytes held by the reuse cache of freed ucg_builtin_dev_malloc
+ *       allocations (UCX_BUILTIN_DEV_CACHE_BYTES);
  *   [4] bytes of live shareable allocations of this process;
- *   [5] bytes of live shareable imports (peers' allocations mapped here). */
-#define UCG_BUILTIN_DEV_NMEMSTATS 6
+ *   [5] bytes of live shareable imports (peers' allocations mapped here);
+ *   [6] bytes parked (ucg_builtin_dev_park). */
+#define UCG_BUILTIN_DEV_NMEMSTATS 7
 void         ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS]);
 /* Set the cap on retired address ranges for this process (0 = back to
  * UCX_BUILTIN_DEV_VA_RETIRED_MAX / the default); for tests. */

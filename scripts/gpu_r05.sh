@@ -24,6 +24,30 @@ for step in "$@"; do
     slice_prof)
         SLICE_PROF_DIR=$OUT/slice_prof timeout -k 10 300 python scripts/slice_probe.py $OUT/slice_prof 4 2000 \
             shareable:read:all plain:read:all > $OUT/slice_prof.txt 2>&1 || exit 1 ;;
+    slice_hsa)
+        SLICE_PROF_DIR=$OUT/slice_hsa SLICE_PROF_TRACE=--hsa-trace timeout -k 10 300 \
+            python scripts/slice_probe.py $OUT/slice_hsa 1 200 shareable:none:one plain:none:one \
+            > $OUT/slice_hsa.txt 2>&1 || exit 1 ;;
+    c4full)
+        timeout -k 10 400 python -u -m pytest tests/test_group.py -m gpu -x -v -s --timeout 320 \
+            --timeout-method thread -k c4_full_size > $OUT/c4full.log 2>&1 || exit 1 ;;
+    pf_pmc)
+        # one rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE cannot share one)
+        for spec in "multi 8 24" "tree 8 24" "tree 3 24"; do
+            tag=$(echo $spec | tr ' ' '_')
+            for c in FETCH_SIZE WRITE_SIZE; do
+                timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv \
+                    -d $OUT/pf_pmc_$tag/pmc_$c -o s -- tools/tune_multi_pf $spec 1 \
+                    > $OUT/pf_pmc_${tag}_$c.txt 2>&1 || exit 1
+            done
+            python3 scripts/pmc_kernels.py $OUT/pf_pmc_$tag > $OUT/pf_pmc_${tag}_by_kernel.txt 2>&1
+        done ;;
+    gather_pmc)
+        timeout -s KILL 120 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --output-format csv \
+            -d $OUT/gather_pmc/pmc_hit -o s -- tools/tune_misalign 1 > $OUT/gather_pmc_hit.txt 2>&1 || exit 1
+        timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+            -d $OUT/gather_pmc/pmc_fetch -o s -- tools/tune_misalign 1 > $OUT/gather_pmc_fetch.txt 2>&1 || exit 1
+        python3 scripts/pmc_kernels.py $OUT/gather_pmc > $OUT/gather_pmc_by_kernel.txt 2>&1 ;;
     va)
         timeout -k 10 300 tools/va_reuse_probe 200 6 > $OUT/va_reuse.txt 2>&1 || exit 1 ;;
     va_ipc)
@@ -31,6 +55,10 @@ for step in "$@"; do
     tests:all)
         timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
             > $OUT/pytest_gpu.log 2>&1 || exit 1 ;;
+    c3i)
+        timeout -k 10 300 python scripts/c3_interleaved.py $OUT/c3_interleaved.json > $OUT/c3_interleaved.txt 2>&1 || exit 1 ;;
+    prof)
+        timeout -k 10 1000 scripts/profile_round.sh ${OUT#gpurun_out/}/prof > $OUT/profile_round.txt 2>&1 || exit 1 ;;
     bench)
         timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1 ;;
     tests:*)

@@ -20,6 +20,10 @@ run() { # name, limit, args...
     if [ "$rc" -ne 0 ]; then tail -5 "$OUT/$name.err"; exit "$rc"; fi
 }
 
+# the library every pass below runs (bench.py compares it with the one it
+# loads: roofline.traffic_source.stale)
+sha256sum "$ROOT/xucg_amd/lib/libucg_builtin_dev.so" > "$OUT/lib_sha.txt"
+
 # the same command as the driver's bench minus the CPU leg and the extra
 # sizes, so every k_reduce launch in the trace is the headline 2^26 combine
 run trace 600 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench \

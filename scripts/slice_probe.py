@@ -40,8 +40,13 @@ def run_case(case, np_default, iters):
         for r in range(np_):
             cmd = [EXE, d, str(r), str(np_), mem, imp, act, str(iters)]
             if prof and r == 0:
-                cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", prof, "-o",
-                       case.replace(":", "_"), "--output-format", "csv", "--"] + cmd
+                # SLICE_PROF_TRACE: the rocprofv3 trace options (default the
+                # kernel trace; "--hsa-trace" lists the runtime's HSA calls,
+                # queue creation included)
+                opts = os.environ.get("SLICE_PROF_TRACE", "--kernel-trace").split()
+                cmd = ["rocprofv3"] + opts + ["--stats", "-d", prof, "-o",
+                                              case.replace(":", "_"), "--output-format",
+                                              "csv", "--"] + cmd
             procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE,
                                           stderr=subprocess.STDOUT, text=True))
         ranks = []

@@ -48,7 +48,8 @@ def main():
             shutil.rmtree(d, ignore_errors=True)
         tot = {k: sum(x.get(k, 0) for x in ranks)
                for k in ("rounds", "same_va", "own_kernel_bad", "own_dma_bad", "peer_kernel_bad",
-                         "peer_dma_bad", "bad_words", "zero_words")}
+                         "peer_dma_bad", "bad_words", "zero_words", "export_fail",
+                         "import_fail", "peer_checked")}
         res = {"mode": mode, "np": np_, "iters": int(iters), "mib": int(mib), "total": tot,
                "ranks": ranks}
         with open(os.path.join(out_dir, "va_reuse_ipc.jsonl"), "a") as f:

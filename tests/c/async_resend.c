@@ -223,6 +223,11 @@ static int run(char **argv, const char *mode, int round_inputs, int fail)
         }
         st = (st == UCS_INPROGRESS) ? ucg_builtin_lcoll_wait(c) : st;
     }
+    if (fail && rank == 0 && getenv("UCX_BUILTIN_WAIT_TIMEOUT")) {
+        /* member 1 may be waiting for the rest of this member's step until
+         * its wait times out: meet it at the last barrier well after that */
+        usleep((useconds_t)(atof(getenv("UCX_BUILTIN_WAIT_TIMEOUT")) * 0.5e6));
+    }
     if (device && st == UCS_OK &&
         ucg_builtin_dev_memcpy(dctx, out, rbuf, count * sizeof(float)) != UCS_OK) {
         fprintf(stderr, "rank %u: download: %s\n", rank, ucg_builtin_dev_last_error());

@@ -507,38 +507,51 @@ def test_retired_address_ranges_are_counted_and_capped(dev_ctx):
 
 
 @pytest.mark.gpu
-def test_exported_plain_memory_is_not_recycled_in_process(dev_ctx):
-    """a freed plain allocation that was exported goes back to the
-    runtime, never to the process's reuse cache, so memory a peer may still
-    read through its mapping is never handed out again here; one that was
-    never exported is kept for the next allocation of its size."""
+def test_parked_memory_is_never_handed_out_again(dev_ctx):
+    """an exported buffer a peer may still read (an op that ended
+    before every peer was done) is parked, not freed: its key is refused from
+    then on, and its memory is never handed out again - not by the reuse
+    cache, which takes every other freed allocation (exported or not: the
+    same memory at the same address keeps the runtime's hipIpc mappings of
+    it right)."""
     from xucg_amd import _lib
     nbytes = 6 << 20
     a = dev_ctx.alloc(nbytes)
-    dev_ctx.ipc_export(a.ptr)
-    c0 = _lib.mem_stats()["plain_cache_bytes"]
-    a.free()
-    assert _lib.mem_stats()["plain_cache_bytes"] == c0
+    key = dev_ctx.ipc_export(a.ptr)
+    pa = a.ptr
+    p0 = _lib.mem_stats()["parked_bytes"]
+    _lib.dev().ucg_builtin_dev_park(dev_ctx.handle, pa)
+    a.ptr = None                                      # parked: not ours to free
+    assert _lib.mem_stats()["parked_bytes"] == p0 + nbytes
+    with pytest.raises(xucg_amd.UcsError) as e:
+        dev_ctx.ipc_import(key)
+    assert e.value.status == -2
+    got = [dev_ctx.alloc(nbytes) for _ in range(3)]
+    assert pa not in [b.ptr for b in got]
+    for b in got:
+        b.free()
+    # an exported allocation freed the normal way is reused whole
     b = dev_ctx.alloc(nbytes)
+    dev_ctx.ipc_export(b.ptr)
     bp = b.ptr
     c1 = _lib.mem_stats()["plain_cache_bytes"]
     b.free()
     assert _lib.mem_stats()["plain_cache_bytes"] == c1 + nbytes
-    c = dev_ctx.alloc(nbytes)                          # the cached one, handed back
+    c = dev_ctx.alloc(nbytes)
     assert c.ptr == bp and _lib.mem_stats()["plain_cache_bytes"] == c1
     c.free()
 
 
 @pytest.mark.gpu
 def test_plain_allocations_reused_whole(dev_ctx):
-    """Round 4: a freed ucg_builtin_dev_malloc allocation that
-    was never exported is kept and handed out again, whole, for the next
-    allocation of its size - the same address on the same memory, never a
-    remap. 60 rounds of allocate, DMA upload, kernel read-back, free: one
-    address throughout, every read right. Round 5: an exported
-    one goes back to the runtime instead (a peer may still read it), and its
-    key is refused after the free even when the runtime hands the address
-    out again."""
+    """Round 4: a freed ucg_builtin_dev_malloc allocation is
+    kept and handed out again, whole, for the next allocation of its size - the
+    same address on the same memory, never a remap - and its old key is
+    refused. 60 rounds of allocate, DMA upload, kernel read-back, free: one
+    address throughout, every read right. Round 5: exported allocations
+    included - given back to the runtime, the address would return with other
+    memory, and peers' new imports of it could map the old memory
+    (tools/va_reuse_probe ipc)."""
     n = (6 << 20) // 4
     out = dev_ctx.alloc(n * 4)
     first = None
@@ -547,6 +560,7 @@ def test_plain_allocations_reused_whole(dev_ctx):
             b = dev_ctx.alloc(n * 4)
             if first is None:
                 first = b.ptr
+                key = dev_ctx.ipc_export(b.ptr)
             assert b.ptr == first, (r, hex(b.ptr), hex(first))
             assert " R ptr" in dev_ctx.debug_ptr(b.ptr) or r == 0
             b.upload(np.full(n, r + 1, np.uint32))                 # DMA write
@@ -555,18 +569,9 @@ def test_plain_allocations_reused_whole(dev_ctx):
             got = out.download(np.uint32, n)
             assert (got == r + 1).all(), (r, int((got != r + 1).sum()))
             b.free()
-        b = dev_ctx.alloc(n * 4)
-        key = dev_ctx.ipc_export(b.ptr)
-        pb = b.ptr
-        b.free()
-        assert f" F ptr 0x{pb:x}" in dev_ctx.debug_ptr(pb)
-        c = dev_ctx.alloc(n * 4)          # never the exported one, from the cache
-        after_free = dev_ctx.debug_ptr(pb).split(f" F ptr 0x{pb:x}")[-1]
-        assert f" R ptr 0x{pb:x}" not in after_free, after_free
         with pytest.raises(xucg_amd.UcsError) as e:
             dev_ctx.ipc_import(key)
         assert e.value.status == -2
-        c.free()
     finally:
         out.free()
 

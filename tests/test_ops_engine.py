@@ -630,6 +630,96 @@ def test_shm_iface_refuses_a_live_jobs_object():
         os.unlink(path)
 
 
+def _fnv1a64(text):
+    """builtin_shm.c job_token(): FNV-1a of the token text"""
+    h = 0xcbf29ce484222325
+    for c in text.encode():
+        h = ((h ^ c) * 0x100000001b3) & ((1 << 64) - 1)
+    return h or 1
+
+
+def _stamp_extra(path, pidns, job):
+    """the round-5 header fields after members: pid namespace, job token"""
+    import struct
+    with open(path, "r+b") as f:
+        f.seek(104)
+        f.write(struct.pack("<QQ", pidns, job))
+
+
+def test_shm_iface_peer_refuses_another_jobs_live_object(monkeypatch):
+    """member 1 of a second job that shares the first job's name
+    and layout no longer maps the first job's live object (its barrier would
+    have thrown that job's barriers out of step): the object carries the
+    creating job's token, and a member of another job is refused with
+    UCS_ERR_BUSY at once."""
+    import subprocess
+    import sys
+    import time
+    import struct
+    import xucg_amd
+    name = shm_name()
+    env = dict(os.environ, UCX_BUILTIN_JOB_TOKEN="job-A", UCX_BUILTIN_WAIT_TIMEOUT="20",
+               PYTHONPATH=ROOT)
+    # job A's member 0: creates and stamps the object, then waits for member 1
+    a = subprocess.Popen([sys.executable, "-c",
+                          "from xucg_amd import ops; ops.ShmIface(%r, 2, 0)" % name],
+                         env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        path = "/dev/shm/" + name
+        t0 = time.time()
+        while time.time() - t0 < 30:
+            try:
+                with open(path, "rb") as f:
+                    f.seek(64)
+                    if struct.unpack("<Q", f.read(8))[0] == 0x58554347534d3031:
+                        break
+            except (OSError, struct.error):
+                pass
+            time.sleep(0.01)
+        else:
+            pytest.fail("job A's object never stamped")
+        monkeypatch.setenv("UCX_BUILTIN_JOB_TOKEN", "job-B")
+        t1 = time.time()
+        with pytest.raises(xucg_amd.UcsError) as e:
+            ops.ShmIface(name, 2, 1)
+        assert e.value.status == -15 and time.time() - t1 < 5
+    finally:
+        a.kill()
+        a.wait()
+        try:
+            os.unlink("/dev/shm/" + name)
+        except OSError:
+            pass
+
+
+@pytest.mark.parametrize("ours", [False, True])
+def test_shm_iface_creator_in_another_pid_namespace(monkeypatch, ours):
+    """a creator pid of another pid namespace (containers sharing
+    /dev/shm) means nothing to kill() here. Member 0 treats such an object as
+    live - UCS_ERR_BUSY - unless it carries this job's own token, which makes
+    it an earlier incarnation of this job to recycle; it is never judged by
+    a pid that happens to be free (or taken) in this namespace."""
+    import subprocess
+    import xucg_amd
+    monkeypatch.setenv("UCX_BUILTIN_JOB_TOKEN", "job-ns")
+    dead = subprocess.Popen(["true"])
+    dead.wait()
+    name = shm_name()
+    path = _stamped_object(name, dead.pid)
+    _stamp_extra(path, 0x7fffffff12345, _fnv1a64("job-ns") if ours else 0x1234)
+    try:
+        if ours:
+            it = ops.ShmIface(name, 1, 0)
+            it.close()
+        else:
+            with pytest.raises(xucg_amd.UcsError) as e:
+                ops.ShmIface(name, 1, 0)
+            assert e.value.status == -15
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+
+
 def test_shm_iface_reopened_at_once_by_every_member():
     """Close and reopen of one name in a loop by 4 members: a member that
     reopens before member 0 unlinked the closed object waits for the new

@@ -209,6 +209,7 @@ static int ipc_mode(int argc, char **argv)
     std::vector<uint32_t> host(n);
     auto val = [](int r, int i) { return 0x01000000u * (uint32_t)(r + 1) + (uint32_t)i + 1; };
     long own_bad = 0, own_dma_bad = 0, peer_kernel_bad = 0, peer_dma_bad = 0, same_va = 0;
+    long export_fail = 0, import_fail = 0, peer_checked = 0;
     unsigned long long bad_words = 0, zero_words = 0;
     std::vector<std::string> first_bad;
     std::vector<void*> held;                      /* hold: last round's imports */
@@ -230,8 +231,14 @@ static int ipc_mode(int argc, char **argv)
         CHECK(hipMemcpy(&h2[0], p, 4, hipMemcpyDeviceToHost));
         CHECK(hipMemcpy(&h2[1], (uint32_t*)p + n - 1, 4, hipMemcpyDeviceToHost));
         own_dma_bad += (h2[0] != val(rank, i) || h2[1] != val(rank, i));
+        /* a handle of all zero bytes tells the peers this round has no key:
+         * the runtime refused the export (counted, not fatal) */
         hipIpcMemHandle_t ih;
-        CHECK(hipIpcGetMemHandle(&ih, p));
+        if (hipIpcGetMemHandle(&ih, p) != hipSuccess) {
+            (void)hipGetLastError();
+            memset(&ih, 0, sizeof(ih));
+            export_fail++;
+        }
         put_file(dir, "key_" + std::to_string(rank) + "_" + std::to_string(i), &ih, sizeof(ih));
         barrier(dir, "a" + std::to_string(i), rank, np);
         std::vector<void*> maps;
@@ -243,8 +250,17 @@ static int ipc_mode(int argc, char **argv)
                 printf("FAIL key of %d round %d\n", q, i);
                 return 1;
             }
+            static const hipIpcMemHandle_t none = {};
+            if (memcmp(&qh, &none, sizeof(qh)) == 0) {
+                continue;                               /* the peer could not export */
+            }
             void *m = nullptr;
-            CHECK(hipIpcOpenMemHandle(&m, qh, hipIpcMemLazyEnablePeerAccess));
+            if (hipIpcOpenMemHandle(&m, qh, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+                (void)hipGetLastError();
+                import_fail++;
+                continue;
+            }
+            peer_checked++;
             maps.push_back(m);
             CHECK(hipMemset(ctr, 0, 8));
             hipLaunchKernelGGL(k_count, dim3(1024), dim3(256), 0, 0, (const uint32_t*)m, n,
@@ -279,9 +295,11 @@ static int ipc_mode(int argc, char **argv)
     barrier(dir, "end", rank, np);
     printf("{\"rank\": %d, \"np\": %d, \"mode\": \"%s\", \"rounds\": %d, \"same_va\": %ld, "
            "\"own_kernel_bad\": %ld, \"own_dma_bad\": %ld, \"peer_kernel_bad\": %ld, "
-           "\"peer_dma_bad\": %ld, \"bad_words\": %llu, \"zero_words\": %llu, \"first_bad\": [",
+           "\"peer_dma_bad\": %ld, \"bad_words\": %llu, \"zero_words\": %llu, "
+           "\"export_fail\": %ld, \"import_fail\": %ld, \"peer_checked\": %ld, \"first_bad\": [",
            rank, np, hold ? "hold" : "close", iters, same_va, own_bad, own_dma_bad,
-           peer_kernel_bad, peer_dma_bad, bad_words, zero_words);
+           peer_kernel_bad, peer_dma_bad, bad_words, zero_words, export_fail, import_fail,
+           peer_checked);
     for (size_t k = 0; k < first_bad.size(); k++) {
         printf("%s\"%s\"", k ? ", " : "", first_bad[k].c_str());
     }

@@ -55,9 +55,10 @@ class DevCtxParams(ctypes.Structure):
 
 ZCOPY_NEVER = (1 << 64) - 1   # UCG_BUILTIN_DEV_ZCOPY_NEVER
 NCOUNTERS = 6                 # UCG_BUILTIN_DEV_NCOUNTERS
-NMEMSTATS = 6                 # UCG_BUILTIN_DEV_NMEMSTATS
+NMEMSTATS = 7                 # UCG_BUILTIN_DEV_NMEMSTATS
 MEMSTATS = ["va_retired_bytes", "va_retired_ranges", "va_retired_max",
-            "plain_cache_bytes", "shareable_live_bytes", "shareable_import_bytes"]
+            "plain_cache_bytes", "shareable_live_bytes", "shareable_import_bytes",
+            "parked_bytes"]
 COMPLETION = {"signal": 1, "sync": 2}   # UCG_BUILTIN_DEV_COMPLETION_*
 
 
@@ -95,6 +96,7 @@ DEV_API = {
     "ucg_builtin_dev_torch_alloc": (_vp, [_sz, _int, _vp]),
     "ucg_builtin_dev_torch_free": (None, [_vp, _sz, _int, _vp]),
     "ucg_builtin_dev_free": (None, [_vp, _vp]),
+    "ucg_builtin_dev_park": (None, [_vp, _vp]),
     "ucg_builtin_dev_host_alloc": (_vp, [_sz]),
     "ucg_builtin_dev_host_free": (None, [_vp]),
     "ucg_builtin_dev_host_register": (_int, [_vp, _vp, _sz]),

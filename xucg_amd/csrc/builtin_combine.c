@@ -517,6 +517,16 @@ void ucg_builtin_combine_dev_free(ucg_builtin_combine_t *cmb, void *ptr)
     pthread_mutex_unlock(&cmb->lock);
 }
 
+void ucg_builtin_combine_dev_park(ucg_builtin_combine_t *cmb, void *ptr)
+{
+    if (cmb == NULL || cmb->dev == NULL || ptr == NULL) {
+        return;
+    }
+    pthread_mutex_lock(&cmb->lock);
+    ucg_builtin_dev_park(cmb->dev, ptr);
+    pthread_mutex_unlock(&cmb->lock);
+}
+
 ucs_status_t ucg_builtin_combine_dev_export(ucg_builtin_combine_t *cmb,
                                             const void *dev_ptr, void *handle)
 {

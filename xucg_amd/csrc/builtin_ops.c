@@ -1118,7 +1118,7 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
 {
     static double lim = -1.0;
     static long spin = -1;
-    unsigned idle = 0;
+    unsigned idle = 0, busy = 0;
     double t0 = now_s();
     if (lim < 0.0) {
         const char *e = getenv("UCX_BUILTIN_WAIT_SPIN");
@@ -1128,7 +1128,14 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
     while (!c->done) {
         if (ucg_builtin_lgroup_progress(c->g) != 0) {
             idle = 0;
-            continue;
+            /* progress counts resend attempts too: a peer that stopped
+             * taking messages (its op ended with an error) keeps it
+             * non-zero, so the time limit is checked here as well */
+            if ((++busy & 4095) == 0 && now_s() - t0 > lim) {
+                idle = (unsigned)spin;
+            } else {
+                continue;
+            }
         }
         /* a peer's message is usually a few hundred ns away: spin first,
          * give the core away only when the wait gets long */

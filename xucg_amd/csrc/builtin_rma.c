@@ -309,19 +309,22 @@ static ucs_status_t rma_import(ucg_builtin_lgroup_t *g, unsigned peer, int kind,
 }
 
 /* Group destroy is collective but not synchronised: a peer may still map this
- * member's pool buffers when they are given back here, and a buffer rma_free
- * left taken (a timeout, an error, a destroy while running) may still be read.
- * Pool buffers and the arena are exported device memory - hipMalloc memory
- * with hipIpc keys by default, shareable allocations with
- * UCX_BUILTIN_DEV_POOL_MEM=shareable - and ucg_builtin_dev_free gives exported
- * memory back to the runtime, never to the process's reuse cache: a peer's
- * mapping holds the physical memory until the peer releases it, so nothing of
- * this process can be handed that memory while the peer still reads it, and
- * the free retires the keys, so a later group can never map it by an old key.
- * Shared-memory segments stay alive for the peers that map them. */
+ * member's pool buffers when they are given back here. Pool buffers and the
+ * arena are exported device memory - hipMalloc memory with hipIpc keys by
+ * default, shareable allocations with UCX_BUILTIN_DEV_POOL_MEM=shareable. A
+ * free retires their keys, so a later group can never map them by an old key.
+ * Plain memory then goes to the process's reuse cache (the same memory at the
+ * same address, which keeps the runtime's hipIpc mappings right, DESIGN.md
+ * 7), shareable memory back to the device (a peer's mapping holds it). A
+ * buffer rma_free left taken - an op that ended before every peer was done
+ * (a timeout, an error, a destroy while running) - may still be read by a
+ * peer: it is parked instead, never handed out again, and so is the arena
+ * when such a buffer lies in it. Shared-memory segments stay
+ * alive for the peers that map them. */
 UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
 {
     unsigned i;
+    int park_arena = 0;
     for (i = 0; i < g->nimp; i++) {
         if (g->imp[i].kind == RMA_SHM) {
             munmap(g->imp[i].ptr, shm_key_bytes(g->imp[i].key));
@@ -335,12 +338,24 @@ UCG_INTERNAL void rma_group_free(ucg_builtin_lgroup_t *g)
             memcpy(&k, g->pool[i].key, sizeof(k));
             munmap(g->pool[i].ptr, g->pool[i].bytes);
             shm_unlink(k.name);
-        } else if (!g->pool[i].in_arena) {
-            ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
+        } else {
+            /* taken by an op (rma_free keeps a buffer with readers taken) */
+            const int readers = g->pool[i].busy && !g->pool[i].user;
+            if (g->pool[i].in_arena) {
+                park_arena |= readers;
+            } else if (readers) {
+                ucg_builtin_combine_dev_park(g->cmb, g->pool[i].ptr);
+            } else {
+                ucg_builtin_combine_dev_free(g->cmb, g->pool[i].ptr);
+            }
         }
     }
     if (g->arena) {
-        ucg_builtin_combine_dev_free(g->cmb, g->arena);
+        if (park_arena) {
+            ucg_builtin_combine_dev_park(g->cmb, g->arena);
+        } else {
+            ucg_builtin_combine_dev_free(g->cmb, g->arena);
+        }
         g->arena = NULL;
     }
     free(g->imp);

@@ -43,11 +43,16 @@ static incast_cell_t *incast_cell(ucg_builtin_shm_iface_t *it, unsigned member,
 
 /* The object's header (the first SEG_CTL_BYTES): the barrier counter at 0,
  * then who made it. Member 0 creates the object (O_EXCL) and stamps it with
- * its pid and a random instance; the others map it once it is stamped by a
- * live creator and the name still refers to that instance. An object left
- * behind by a dead creator (a crashed job) is unlinked and made anew; one
- * whose creator is alive belongs to another job with the same name and is
- * refused (UCS_ERR_BUSY: set a job uid). Closing marks the object closed
+ * its pid, its pid namespace, the job's token and a random instance; the
+ * others map it once it is stamped by a live creator of their own job and the
+ * name still refers to that instance. An object left behind by a dead
+ * creator (a crashed job) is unlinked and made anew; one whose creator is
+ * alive belongs to another job with the same name and is refused
+ * (UCS_ERR_BUSY: set a job uid) - by member 0, and (round 5) by
+ * every other member too when both jobs carry a token (job_token). A creator
+ * in another pid namespace (containers sharing /dev/shm) cannot be probed
+ * with kill(): its object is taken as live, and recycled by member 0 only
+ * when it carries this job's own token. Closing marks the object closed
  * before the last barrier, so a member that reopens the name at once waits
  * for the next instance. ADVICE r03: two jobs without a job uid, or a new job
  * over a crashed one's object, shared rings and the barrier counter. */
@@ -59,6 +64,8 @@ typedef struct {
     uint64_t         instance;          /* random, per creation */
     uint64_t         seg_bytes;
     uint64_t         members;
+    uint64_t         pidns;             /* the creator's pid namespace (0: unknown) */
+    uint64_t         job;               /* the creator's job token (0: none) */
 } seg_hdr_t;
 _Static_assert(sizeof(seg_hdr_t) <= SEG_CTL_BYTES, "segment header size");
 #define SHM_STAMP  0x58554347534d3031ull         /* "XUCGSM01" */
@@ -67,6 +74,67 @@ _Static_assert(sizeof(seg_hdr_t) <= SEG_CTL_BYTES, "segment header size");
 static int pid_alive(uint64_t pid)
 {
     return pid != 0 && (kill((pid_t)pid, 0) == 0 || errno != ESRCH);
+}
+
+/* this process's pid namespace: the inode of /proc/self/ns/pid (0: unknown) */
+static uint64_t pid_ns(void)
+{
+    struct stat sb;
+    return stat("/proc/self/ns/pid", &sb) == 0 ? (uint64_t)sb.st_ino : 0;
+}
+
+/* the creator `pid` of namespace `ns`: 1 alive, 0 gone, -1 cannot tell (a
+ * pid of another namespace means nothing to kill() here) */
+static int owner_state(uint64_t pid, uint64_t ns)
+{
+    const uint64_t mine = pid_ns();
+    if (ns != 0 && mine != 0 && ns != mine) {
+        return -1;
+    }
+    return pid_alive(pid);
+}
+
+/* This job's token, the same in every member of one launch: FNV-1a of
+ * UCX_BUILTIN_JOB_TOKEN, else of the launcher's job id (PMIx namespace, Open
+ * MPI's job id, Slurm's job.step, torchrun's run id, the rendezvous
+ * MASTER_ADDR:MASTER_PORT); 0 when there is none (a peer can then not tell
+ * another job's object from its own: set a job uid). */
+static uint64_t job_token(void)
+{
+    static const char *vars[][2] = {{"UCX_BUILTIN_JOB_TOKEN", NULL},
+                                    {"PMIX_NAMESPACE", NULL},
+                                    {"OMPI_MCA_ess_base_jobid", NULL},
+                                    {"SLURM_JOB_ID", "SLURM_STEP_ID"},
+                                    {"TORCHELASTIC_RUN_ID", NULL},
+                                    {"MASTER_ADDR", "MASTER_PORT"}};
+    unsigned i;
+    for (i = 0; i < sizeof(vars) / sizeof(vars[0]); i++) {
+        const char *a = getenv(vars[i][0]), *b = vars[i][1] ? getenv(vars[i][1]) : "";
+        const char *parts[3];
+        uint64_t h = 0xcbf29ce484222325ull;
+        unsigned k;
+        if (a == NULL || *a == 0 || b == NULL) {
+            continue;
+        }
+        parts[0] = a;
+        parts[1] = *b ? ":" : "";
+        parts[2] = b;
+        for (k = 0; k < 3; k++) {
+            const unsigned char *c;
+            for (c = (const unsigned char*)parts[k]; *c; c++) {
+                h = (h ^ *c) * 0x100000001b3ull;
+            }
+        }
+        return h ? h : 1;
+    }
+    return 0;
+}
+
+/* an object of another job: both sides carry a token and they differ */
+static int foreign_job(uint64_t job)
+{
+    const uint64_t mine = job_token();
+    return job != 0 && mine != 0 && job != mine;
 }
 
 /* the header of the object the name refers to now (zeros if none) */
@@ -87,6 +155,8 @@ static void peek_hdr(const char *name, seg_hdr_t *out)
             out->instance  = h->instance;
             out->seg_bytes = h->seg_bytes;
             out->members   = h->members;
+            out->pidns     = h->pidns;
+            out->job       = h->job;
             munmap(h, sizeof(seg_hdr_t));
         }
     }
@@ -117,12 +187,18 @@ static int iface_create(ucg_builtin_shm_iface_t *it, double t0)
             break;
         }
         peek_hdr(it->name, &ph);
-        if (ph.stamp == SHM_STAMP && pid_alive(ph.owner)) {
-            fprintf(stderr, "ucg_builtin_shm_iface_open(%s): in use by live process %llu "
-                    "(another job with this name: set a job uid)\n", it->name,
-                    (unsigned long long)ph.owner);
-            it->open_status = UCS_ERR_BUSY;
-            return -1;
+        if (ph.stamp == SHM_STAMP) {
+            /* live, or in another pid namespace and not provably this job's
+             * (an earlier incarnation of this very job is recycled) */
+            const int state = owner_state(ph.owner, ph.pidns);
+            if (state == 1 || (state < 0 && !(ph.job != 0 && ph.job == job_token()))) {
+                fprintf(stderr, "ucg_builtin_shm_iface_open(%s): in use by %s process %llu "
+                        "(another job with this name: set a job uid)\n", it->name,
+                        state == 1 ? "live" : "another pid namespace's",
+                        (unsigned long long)ph.owner);
+                it->open_status = UCS_ERR_BUSY;
+                return -1;
+            }
         }
         /* a dead creator's object, a closed one, or one never set up */
         if (ph.stamp != 0 || now_s() - t0 > 1.0) {
@@ -186,6 +262,8 @@ static ucs_status_t iface_map(ucg_builtin_shm_iface_t *it)
             h->instance  = random_u64();
             h->seg_bytes = it->seg_bytes;
             h->members   = it->members;
+            h->pidns     = pid_ns();
+            h->job       = job_token();
             atomic_store_explicit(&h->stamp, SHM_STAMP, memory_order_release);
             return UCS_OK;
         }
@@ -200,14 +278,24 @@ static ucs_status_t iface_map(ucg_builtin_shm_iface_t *it)
             }
         }
         if (atomic_load_explicit(&h->stamp, memory_order_acquire) == SHM_STAMP &&
-            pid_alive(h->owner) && h->seg_bytes == it->seg_bytes &&
+            owner_state(h->owner, h->pidns) != 0 && foreign_job(h->job)) {
+            fprintf(stderr, "ucg_builtin_shm_iface_open(%s): the object of another job "
+                    "(creator %llu; set a job uid)\n", it->name,
+                    (unsigned long long)h->owner);
+            munmap(it->seg, it->seg_bytes);
+            it->seg = NULL;
+            it->open_status = UCS_ERR_BUSY;
+            return it->open_status;
+        }
+        if (atomic_load_explicit(&h->stamp, memory_order_acquire) == SHM_STAMP &&
+            owner_state(h->owner, h->pidns) != 0 && h->seg_bytes == it->seg_bytes &&
             h->members == it->members) {
             peek_hdr(it->name, &ph);
             if (ph.instance == h->instance) {
                 return UCS_OK;                      /* still the named object */
             }
         } else if (atomic_load_explicit(&h->stamp, memory_order_acquire) == SHM_STAMP &&
-                   pid_alive(h->owner)) {
+                   owner_state(h->owner, h->pidns) != 0) {
             fprintf(stderr, "ucg_builtin_shm_iface_open(%s): a live object of another "
                     "layout (%llu members, %llu B; here %u, %zu)\n", it->name,
                     (unsigned long long)h->members, (unsigned long long)h->seg_bytes,

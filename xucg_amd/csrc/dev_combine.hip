@@ -231,11 +231,15 @@ static ucs_status_t ring_init(ucg_builtin_dev_ctx_t *ctx)
     const size_t total = ctx->slot_bytes * ctx->nslots;
     HIP_TRY(hipHostMalloc((void**)&ctx->h_ring, total, hipHostMallocDefault));
     HIP_TRY(hipHostGetDevicePointer((void**)&ctx->h_ring_dev, ctx->h_ring, 0));
-    /* device slots at addresses never used before: the copy engine writes
-     * them, and a recycled address can take a DMA write into the previous
-     * allocation's pages (tools/va_reuse_probe) */
-    ctx->d_ring  = static_cast<char*>(ucg_builtin_dev_malloc_shareable(ctx, total));
-    ctx->d_ring2 = static_cast<char*>(ucg_builtin_dev_malloc_shareable(ctx, total));
+    /* plain hipMalloc memory (round 5): never exported, so it needs no
+     * shareable allocation, and a virtual-memory allocation makes the HIP
+     * runtime create one more hardware queue in the process, after which
+     * every process sharing the GPU is time-sliced (DESIGN.md 6,
+     * tools/src/slice_probe.c). A DMA write into this process's own
+     * hipMalloc memory at a recycled address read right in every round
+     * measured (tools/va_reuse_probe, one and 12 processes). */
+    ctx->d_ring  = static_cast<char*>(ucg_builtin_dev_malloc(ctx, total));
+    ctx->d_ring2 = static_cast<char*>(ucg_builtin_dev_malloc(ctx, total));
     if (ctx->d_ring == nullptr || ctx->d_ring2 == nullptr) {
         return UCS_ERR_NO_MEMORY;          /* the reason is in the last error */
     }
@@ -1088,8 +1092,8 @@ ucs_status_t ucg_builtin_dev_stage_begin(ucg_builtin_dev_ctx_t *ctx,
         HIP_TRY(hipStreamSynchronize(ctx->stream));
         ucg_builtin_dev_free(ctx, ctx->d_acc);     /* NULL is a no-op */
         ctx->d_acc_cap = 0;
-        /* a fresh address, as the ring's (the H2D mirror copy writes it) */
-        ctx->d_acc = static_cast<char*>(ucg_builtin_dev_malloc_shareable(ctx, bytes));
+        /* plain memory, as the ring's */
+        ctx->d_acc = static_cast<char*>(ucg_builtin_dev_malloc(ctx, bytes));
         if (ctx->d_acc == nullptr) {
             return UCS_ERR_NO_MEMORY;
         }

@@ -86,6 +86,7 @@ std::unordered_map<void*, own_alloc> g_allocs;        /* base -> allocation */
  * 1 GiB per process; 0 = free at once); past the bound it is freed. */
 std::multimap<std::pair<int, size_t>, void*> g_plain_cache;   /* (device, bytes) */
 size_t g_plain_cached = 0;
+uint64_t g_parked = 0;           /* bytes parked by ucg_builtin_dev_park */
 
 size_t plain_cache_limit()
 {
@@ -127,7 +128,7 @@ size_t plain_cache_drain()
  * address range. */
 struct mem_event {
     char     kind;      /* M malloc, R malloc from the reuse cache, V shareable malloc, F free, X export,
-                           I import, C release (close), S stale key refused */
+                           I import, C release (close), S stale key refused, P parked */
     void    *ptr;
     void    *base;
     size_t   bytes;
@@ -1020,7 +1021,7 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         return;
     }
     own_alloc a;
-    bool own = false, exported = false;
+    bool own = false;
     int fd = -1;
     {
         std::lock_guard<std::mutex> g(g_mu);
@@ -1033,7 +1034,6 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         /* retire its key: a peer's import of it is refused from now on */
         auto ex = g_export_of.find(ptr);
         if (ex != g_export_of.end()) {
-            exported = true;
             fd = g_exports[ex->second].fd;
             g_exports.erase(ex->second);
             g_export_of.erase(ex);
@@ -1056,16 +1056,20 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         va_retire(a.bytes);                /* the range is never reused */
     } else if (own && a.kind == KIND_PLAIN) {
         /* as hipFree does: nothing queued may still use it; then kept for
-         * the next allocation of its size (g_plain_cache) - unless it was
-         * exported: a peer may still map it (a group destroyed while a peer
-         * reads, a buffer left taken after a timeout), and memory handed out
-         * again here would change under that reader. Given back to the
-         * runtime instead, the peer's mapping keeps the old physical memory
-         * (ADVICE r04). */
+         * the next allocation of its size (g_plain_cache), exported or not.
+         * An exported allocation must not go back to the runtime: the next
+         * hipMalloc hands its address out again with other memory, and a
+         * peer's hipIpcOpenMemHandle of the new allocation's handle can
+         * return a mapping of the old memory - 3,608 of 6,974 peer reads in
+         * 12 processes recycling hipMalloc buffers read the previous
+         * round's data (tools/va_reuse_probe ipc). Reused here
+         * it is the same memory, so such a mapping still reads right. A
+         * buffer that a peer may still be reading is parked instead
+         * (ucg_builtin_dev_park: ADVICE r04). */
         (void)hipSetDevice(a.device);
         e = hipDeviceSynchronize();
         bool kept = false;
-        if (!exported) {
+        {
             std::lock_guard<std::mutex> g(g_mu);
             if (g_plain_cached + a.bytes <= plain_cache_limit()) {
                 g_plain_cache.emplace(std::make_pair(a.device, a.bytes), ptr);
@@ -1081,6 +1085,32 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
     }
     std::lock_guard<std::mutex> g(g_mu);
     note_event('F', ptr, ptr, own ? a.bytes : 0, (int)e);
+}
+
+void ucg_builtin_dev_park(ucg_builtin_dev_ctx_t *ctx, void *ptr)
+{
+    if (ptr == nullptr) {
+        return;
+    }
+    (void)ctx;
+    int fd = -1;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_allocs.find(ptr);
+    if (it == g_allocs.end()) {
+        return;                                  /* not this shim's: left alone */
+    }
+    g_parked += it->second.bytes;
+    g_allocs.erase(it);                          /* never freed, never handed out */
+    auto ex = g_export_of.find(ptr);
+    if (ex != g_export_of.end()) {               /* its keys retire all the same */
+        fd = g_exports[ex->second].fd;
+        g_exports.erase(ex->second);
+        g_export_of.erase(ex);
+    }
+    if (fd >= 0) {
+        close(fd);
+    }
+    note_event('P', ptr, ptr, 0, 0);
 }
 
 void ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS])
@@ -1106,6 +1136,7 @@ void ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS])
     out[3] = g_plain_cached;
     out[4] = live_vmm;
     out[5] = live_imp;
+    out[6] = g_parked;
 }
 
 void ucg_builtin_dev_set_va_retired_max(uint64_t bytes)

@@ -66,6 +66,7 @@ HOST_API = {
     "ucg_builtin_combine_check_reduction": (_int, [_vp, _vp]),
     "ucg_builtin_combine_dev_alloc": (_vp, [_vp, _sz]),
     "ucg_builtin_combine_dev_free": (None, [_vp, _vp]),
+    "ucg_builtin_combine_dev_park": (None, [_vp, _vp]),
     "ucg_builtin_combine_dev_export": (_int, [_vp, _vp, _vp]),
     "ucg_builtin_combine_dev_import": (_int, [_vp, _vp, ctypes.POINTER(_vp)]),
     "ucg_builtin_combine_dev_release": (None, [_vp, _vp]),
