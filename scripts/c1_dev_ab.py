@@ -3,7 +3,7 @@
 same command as bench.py's extra.c1_loopback_allreduce_4kib_fp32
 .device_buffers_* legs, alternating settings over several repetitions.
 
-    python scripts/c1_dev_ab.py OUT.json [reps] [r03|r04]
+    python scripts/c1_dev_ab.py OUT.json [reps] [r03|r04|r05]
 
 r03 settings: the default library (the context's second stream created with
 it), UCX_BUILTIN_DEV_D2H_STREAM=lazy (created on first use, round 2's
@@ -14,6 +14,9 @@ r04 settings (the device-buffer latency went from 12 to 95 us between the
 rounds): the default; hipMalloc memory and hipIpc keys instead of shareable
 memory (UCX_BUILTIN_DEV_SHAREABLE=n); no pool arena
 (UCX_BUILTIN_DEV_POOL_BYTES=0); both; the send buffer not registered.
+r05 settings (the default): the default (plain pools and staging ring), the
+pools in shareable memory, host buffers with every step staged on the GPU
+(C1_DEVICE_STAGING), the send buffer not registered.
 The parent never touches the GPU: ranks are child processes."""
 import json
 import os
@@ -54,7 +57,16 @@ def run(world, count, iters, env_extra, prof=None):
 
 def main():
     out, reps = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 3
-    if (sys.argv[3] if len(sys.argv) > 3 else "r04") == "r03":
+    which = sys.argv[3] if len(sys.argv) > 3 else "r05"
+    if which == "r05":
+        # round 5: pools and staging in plain memory; a process
+        # owning virtual memory time-slices every process on the GPU
+        settings = {"default": {},
+                    "pools_shareable": {"UCX_BUILTIN_DEV_POOL_MEM": "shareable"},
+                    "host_buffers_staged": {"C1_DEVICE_BUFFERS": None, "C1_REGISTERED": None,
+                                            "C1_DEVICE_STAGING": "1"},
+                    "send_not_registered": {"C1_REGISTERED": None}}
+    elif which == "r03":
         settings = {"default": {}, "d2h_lazy": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy"},
                     "d2h_lazy_hwq2": {"UCX_BUILTIN_DEV_D2H_STREAM": "lazy",
                                       "GPU_MAX_HW_QUEUES": "2"},

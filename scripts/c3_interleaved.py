@@ -3,13 +3,14 @@
 timed interleaved with the fp32 SUM reference on the same buffers? The five
 lowest 1 GiB pairs of round 4's sweep (profiles/r04/c3/c3_sweep.json) and
 fp32 MIN / MAX, each alternated with fp32 SUM over rounds in one process:
-per round, 20 back-to-back launches of the pair, then 20 of fp32 SUM (HIP
-events on the context stream, ucg_builtin_dev_profile_reduce). Reported per
+per round, 20 back-to-back launches of the pair and 20 of fp32 SUM, in
+alternating order (HIP events on the context stream,
+ucg_builtin_dev_profile_reduce). Reported per
 pair: its median % of 8 TB/s, the interleaved fp32 SUM's, and the median of
 the per-round ratios - a ratio near 1 means the sweep's gap was the box's
 phase, not the dtype.
 
-    python scripts/c3_interleaved.py [out.json] [rounds = 7]
+    python scripts/c3_interleaved.py [out.json] [rounds = 8]
 """
 import json
 import os
@@ -30,7 +31,7 @@ BYTES = 1 << 30             # per operand, the north-star size
 
 def main():
     out_path = sys.argv[1] if len(sys.argv) > 1 else None
-    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 7
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     ctx = xucg_amd.DevContext(device=0)
     pair = ctx.alloc(2 * BYTES)            # one allocation, the bench's layout
     src, dst = pair.ptr, pair.ptr + BYTES
@@ -45,9 +46,14 @@ def main():
         ctx.profile_reduce(op, dt, dst, src, n, 5)
         ctx.profile_reduce("sum", "float32", dst, src, nf, 5)
         p_us, f_us = [], []
-        for _ in range(rounds):
-            p_us.append(ctx.profile_reduce(op, dt, dst, src, n, 20))
-            f_us.append(ctx.profile_reduce("sum", "float32", dst, src, nf, 20))
+        for r in range(rounds):
+            # the order alternates, so neither side always runs second
+            if r % 2:
+                f_us.append(ctx.profile_reduce("sum", "float32", dst, src, nf, 20))
+                p_us.append(ctx.profile_reduce(op, dt, dst, src, n, 20))
+            else:
+                p_us.append(ctx.profile_reduce(op, dt, dst, src, n, 20))
+                f_us.append(ctx.profile_reduce("sum", "float32", dst, src, nf, 20))
         frac = [3 * BYTES / (u * 1e-6) / 1e9 / PEAK for u in p_us]
         ffrac = [3 * BYTES / (u * 1e-6) / 1e9 / PEAK for u in f_us]
         row = {"dtype": dt, "op": op,

@@ -31,6 +31,11 @@ for step in "$@"; do
     c4full)
         timeout -k 10 400 python -u -m pytest tests/test_group.py -m gpu -x -v -s --timeout 320 \
             --timeout-method thread -k c4_full_size > $OUT/c4full.log 2>&1 || exit 1 ;;
+    pf2)
+        for spec in "multi 8 24" "multi 8 26" "multi 16 24" "tree 8 24"; do
+            tag=$(echo $spec | tr ' ' '_')
+            timeout -k 10 200 tools/tune_multi_pf $spec 9 > $OUT/pf2_$tag.txt 2>&1 || exit 1
+        done ;;
     pf_pmc)
         # one rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE cannot share one)
         for spec in "multi 8 24" "tree 8 24" "tree 3 24"; do
@@ -59,6 +64,10 @@ for step in "$@"; do
         timeout -k 10 300 python scripts/c3_interleaved.py $OUT/c3_interleaved.json > $OUT/c3_interleaved.txt 2>&1 || exit 1 ;;
     prof)
         timeout -k 10 1000 scripts/profile_round.sh ${OUT#gpurun_out/}/prof > $OUT/profile_round.txt 2>&1 || exit 1 ;;
+    smoke)
+        timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1 ;;
+    c1ab)
+        timeout -k 10 700 python scripts/c1_dev_ab.py $OUT/c1_dev_ab.json 2 r05 > $OUT/c1_dev_ab.log 2>&1 || exit 1 ;;
     bench)
         timeout -k 10 400 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 1 ;;
     tests:*)

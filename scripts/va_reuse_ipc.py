@@ -44,17 +44,36 @@ def main():
                 except (ValueError, IndexError):
                     ranks.append({"rank": r, "exit": p.returncode, "tail": out[-400:]})
                     rc = 1
+            # handles of different members in one round with equal bytes
+            # (a handle naming (address, size) alone would collide between
+            # processes whose allocations sit at the same address)
+            same_bytes = rounds_with_same = 0
+            for i in range(int(iters)):
+                seen = {}
+                for r in range(np_):
+                    try:
+                        with open(os.path.join(d, f"key_{r}_{i}"), "rb") as f:
+                            b = f.read()
+                    except OSError:
+                        continue
+                    if b.strip(b"\0"):
+                        seen.setdefault(b, []).append(r)
+                dups = [v for v in seen.values() if len(v) > 1]
+                same_bytes += sum(len(v) for v in dups)
+                rounds_with_same += bool(dups)
+            handle_bytes = {"members_sharing_handle_bytes": same_bytes,
+                            "rounds_with_shared_handle_bytes": rounds_with_same}
         finally:
             shutil.rmtree(d, ignore_errors=True)
         tot = {k: sum(x.get(k, 0) for x in ranks)
                for k in ("rounds", "same_va", "own_kernel_bad", "own_dma_bad", "peer_kernel_bad",
                          "peer_dma_bad", "bad_words", "zero_words", "export_fail",
-                         "import_fail", "peer_checked")}
+                         "import_fail", "peer_checked", "dup_ptr", "bad_and_dup")}
         res = {"mode": mode, "np": np_, "iters": int(iters), "mib": int(mib), "total": tot,
-               "ranks": ranks}
+               "handles": handle_bytes, "ranks": ranks}
         with open(os.path.join(out_dir, "va_reuse_ipc.jsonl"), "a") as f:
             f.write(json.dumps(res) + "\n")
-        print(f"{mode}: {tot}", flush=True)
+        print(f"{mode}: {tot} {handle_bytes}", flush=True)
     return rc
 
 

@@ -77,6 +77,8 @@ static void add_multi(std::vector<Variant> &vs)
     MV("PF3, half the operands", 1, 1, 3, (N / 2 > 0 ? N / 2 : 1), true);
     MV("PF3, operand 0 only", 1, 1, 3, 1, true);
     MV("PF1, operand 0 only", 1, 1, 1, 1, true);
+    MV("PF1, half the operands", 1, 1, 1, (N / 2 > 0 ? N / 2 : 1), true);
+    MV("PF1, two operands", 1, 1, 1, (N >= 2 ? 2 : 1), true);
     MV("PF3, all operands, uncapped", 1, 0, 3, N, true);
     MV("PF1, all operands, uncapped", 1, 0, 1, N, true);
 #undef MV
@@ -102,6 +104,7 @@ static void add_tree(std::vector<Variant> &vs, unsigned n)
     TV("PF3, first half", 1, C, 3, NMAX / 2);
     TV("PF3, operand 0 only", 1, C, 3, 1);
     TV("PF1, operand 0 only", 1, C, 1, 1);
+    TV("PF1, first half", 1, C, 1, NMAX / 2);
 #undef TV
 }
 

@@ -209,7 +209,7 @@ static int ipc_mode(int argc, char **argv)
     std::vector<uint32_t> host(n);
     auto val = [](int r, int i) { return 0x01000000u * (uint32_t)(r + 1) + (uint32_t)i + 1; };
     long own_bad = 0, own_dma_bad = 0, peer_kernel_bad = 0, peer_dma_bad = 0, same_va = 0;
-    long export_fail = 0, import_fail = 0, peer_checked = 0;
+    long export_fail = 0, import_fail = 0, peer_checked = 0, dup_ptr = 0, bad_and_dup = 0;
     unsigned long long bad_words = 0, zero_words = 0;
     std::vector<std::string> first_bad;
     std::vector<void*> held;                      /* hold: last round's imports */
@@ -261,6 +261,13 @@ static int ipc_mode(int argc, char **argv)
                 continue;
             }
             peer_checked++;
+            /* the runtime handed out a mapping this round already has for
+             * another peer's handle: the same pointer twice */
+            bool dup = false;
+            for (void *o : maps) {
+                dup = dup || o == m;
+            }
+            dup_ptr += dup;
             maps.push_back(m);
             CHECK(hipMemset(ctr, 0, 8));
             hipLaunchKernelGGL(k_count, dim3(1024), dim3(256), 0, 0, (const uint32_t*)m, n,
@@ -269,6 +276,7 @@ static int ipc_mode(int argc, char **argv)
             CHECK(hipMemcpy(&h2[0], m, 4, hipMemcpyDeviceToHost));
             CHECK(hipMemcpy(&h2[1], (uint32_t*)m + n - 1, 4, hipMemcpyDeviceToHost));
             const bool kb = c[0] != 0, db = (h2[0] != val(q, i) || h2[1] != val(q, i));
+            bad_and_dup += (kb || db) && dup;
             peer_kernel_bad += kb;
             peer_dma_bad += db;
             bad_words += c[0];
@@ -296,10 +304,11 @@ static int ipc_mode(int argc, char **argv)
     printf("{\"rank\": %d, \"np\": %d, \"mode\": \"%s\", \"rounds\": %d, \"same_va\": %ld, "
            "\"own_kernel_bad\": %ld, \"own_dma_bad\": %ld, \"peer_kernel_bad\": %ld, "
            "\"peer_dma_bad\": %ld, \"bad_words\": %llu, \"zero_words\": %llu, "
-           "\"export_fail\": %ld, \"import_fail\": %ld, \"peer_checked\": %ld, \"first_bad\": [",
+           "\"export_fail\": %ld, \"import_fail\": %ld, \"peer_checked\": %ld, "
+           "\"dup_ptr\": %ld, \"bad_and_dup\": %ld, \"first_bad\": [",
            rank, np, hold ? "hold" : "close", iters, same_va, own_bad, own_dma_bad,
            peer_kernel_bad, peer_dma_bad, bad_words, zero_words, export_fail, import_fail,
-           peer_checked);
+           peer_checked, dup_ptr, bad_and_dup);
     for (size_t k = 0; k < first_bad.size(); k++) {
         printf("%s\"%s\"", k ? ", " : "", first_bad[k].c_str());
     }
