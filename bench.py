@@ -402,6 +402,41 @@ PHASE_MIN_S = {"c4_rccl_rs_ag_4gib_fp32": 30, "c4_oneshot_xgmi_rs_4gib_fp32": 60
                "c5_builtin_engine_device_buffers_512mib_fp64": 45}
 
 
+def phase_budget_skip(dist, dev, t_start, limit, name):
+    """None when phase `name` may start, else its "skipped" entry: it needs
+    PHASE_MIN_S[name] seconds of the child's `limit` left. The elapsed time
+    is max-reduced over the ranks first, so every rank decides alike."""
+    import torch
+    el = torch.tensor([time.perf_counter() - t_start], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    left, need = limit - el.item(), PHASE_MIN_S.get(name, 30)
+    if left < need:
+        return {"skipped": f"budget: {left:.0f} s left of the child's {limit:.0f} s, "
+                           f"the phase needs {need} s"}
+    return None
+
+
+def read_child_result(path, rc, tail):
+    """Rank 0's view of the collective child: the phases it saved (path), the
+    one running when it was stopped marked as failed, and the child's exit
+    status as an error entry when it did not end cleanly."""
+    res = None
+    try:
+        with open(path) as f:
+            res = json.load(f)
+        os.unlink(path)
+    except (OSError, ValueError):
+        pass
+    running = (res or {}).pop("running", None)
+    if running:
+        # killed inside a phase: that phase's entry says so, the finished
+        # ones stand
+        res[running] = {"error": f"the collective child was stopped inside this phase ({rc})"}
+    if rc != 0 or res is None:
+        res = dict(res or {}, error=f"collective child exited with {rc}", tail=tail)
+    return res
+
+
 def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2, save=None):
     """BASELINE configs 4 and 5 across the N GPUs of the node (N > 1 only).
 
@@ -439,13 +474,9 @@ def collective_phases(ctx, dist, rank, world, local_rank, steps=5, warmup=2, sav
         if only and name not in only:
             out[name] = {"skipped": "not in XUCG_COLLECTIVE_PHASES"}
             return
-        import torch
-        el = torch.tensor([time.perf_counter() - t_start], dtype=torch.float64, device=dev)
-        dist.all_reduce(el, op=dist.ReduceOp.MAX)          # every rank decides alike
-        left = limit - el.item()
-        if left < PHASE_MIN_S.get(name, 30):
-            out[name] = {"skipped": f"budget: {left:.0f} s left of the child's {limit:.0f} s, "
-                                    f"the phase needs {PHASE_MIN_S.get(name, 30)} s"}
+        skip = phase_budget_skip(dist, dev, t_start, limit, name)
+        if skip:
+            out[name] = skip
             return
         if save:
             save(out, running=name)
@@ -1073,21 +1104,7 @@ def run_collective_children(dist, rank, world, timeout_s=300):
         rc, tail = "timeout", str(e)[-300:]
     if rank != 0:
         return None, rc == 0
-    res = None
-    try:
-        with open(obj[0]["out"]) as f:
-            res = json.load(f)
-        os.unlink(obj[0]["out"])
-    except (OSError, ValueError):
-        pass
-    running = (res or {}).pop("running", None)
-    if running:
-        # killed inside a phase: that phase's entry says so, the finished
-        # ones stand
-        res[running] = {"error": f"the collective child was stopped inside this phase ({rc})"}
-    if rc != 0 or res is None:
-        res = dict(res or {}, error=f"collective child exited with {rc}", tail=tail)
-    return res, rc == 0
+    return read_child_result(obj[0]["out"], rc, tail), rc == 0
 
 
 class HostStagedDist:

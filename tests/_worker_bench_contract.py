@@ -6,6 +6,7 @@ association evaluated on the host over windows of every rank's input -
 agreeing with the oracle and catching a changed element."""
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -59,6 +60,16 @@ def main():
     acc[n - 1] = np.nextafter(acc[n - 1].item(), np.inf)       # the tail window
     if check(acc):
         fail("a changed element passed the sampled check")
+
+    # phase budgets: every rank takes the slowest rank's elapsed time, so all
+    # skip or all run (rank r pretends to have run r x 10 s)
+    t_start = time.perf_counter() - 10.0 * rank
+    need = bench.PHASE_MIN_S["c4_oneshot_xgmi_rs_4gib_fp32"]
+    for limit, want_skip in ((need + 10.0 * (world - 1) + 5, False),
+                             (need + 10.0 * (world - 1) - 5, True)):
+        sk = bench.phase_budget_skip(dist, "cpu", t_start, limit, "c4_oneshot_xgmi_rs_4gib_fp32")
+        if (sk is not None) != want_skip or (sk and "budget" not in sk["skipped"]):
+            fail(f"phase_budget_skip({limit}) = {sk}")
 
     # the C4 phases' parity without a 4 GiB vendor collective (PlanWindows):
     # every shard's windows against the oracle's recursive doubling as that

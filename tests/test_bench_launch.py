@@ -48,3 +48,29 @@ def test_bench_gpus_one_stays_one_process():
     assert p.returncode == 0, p.stderr[-2000:]
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1, line
+
+
+def test_collective_child_result_keeps_finished_phases(tmp_path):
+    """An overrun costs the running phase's entry, never the line (VERDICT r04
+    #1): the parent reads back the phases the child saved, marks the one it was
+    stopped in as failed, and adds the child's exit status as an error."""
+    import json
+    import bench
+    path = tmp_path / "child.json"
+    path.write_text(json.dumps({"c4_rccl_rs_ag_4gib_fp32": {"rs_ms": 1.0},
+                                "phase_wall_s": {"c4_rccl_rs_ag_4gib_fp32": 3.0},
+                                "running": "c4_oneshot_xgmi_rs_4gib_fp32"}))
+    res = bench.read_child_result(str(path), "timeout", "tail")
+    assert res["c4_rccl_rs_ag_4gib_fp32"] == {"rs_ms": 1.0}
+    assert "stopped inside this phase" in res["c4_oneshot_xgmi_rs_4gib_fp32"]["error"]
+    assert res["error"].startswith("collective child exited with timeout")
+    assert not path.exists()
+    fails = bench.collective_failures(res)
+    assert any(f.startswith("c4_oneshot_xgmi_rs_4gib_fp32") for f in fails), fails
+    # a clean child: its final file, no error entries
+    path.write_text(json.dumps({"c4_rccl_rs_ag_4gib_fp32": {"rs_ms": 1.0}}))
+    res = bench.read_child_result(str(path), 0, "")
+    assert bench.collective_failures(res) == [] and "running" not in res
+    # no file at all
+    res = bench.read_child_result(str(tmp_path / "none.json"), 1, "boom")
+    assert res["error"] == "collective child exited with 1" and res["tail"] == "boom"

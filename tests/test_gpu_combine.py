@@ -543,6 +543,38 @@ def test_parked_memory_is_never_handed_out_again(dev_ctx):
 
 
 @pytest.mark.gpu
+def test_exported_allocations_kept_past_the_cache_bound():
+    """With the reuse cache's bound at 0 (UCX_BUILTIN_DEV_CACHE_BYTES=0, read
+    once per process: a child process), a never-exported allocation is freed
+    at once, and one that was ever exported is kept all the same - given back
+    to the runtime, its address could come back with other memory and peers'
+    fresh hipIpc imports of it map another process's buffer.
+    The oom drain gives back only the never-exported ones."""
+    import subprocess
+    import sys
+    code = r"""
+import xucg_amd
+from xucg_amd import _lib
+ctx = xucg_amd.DevContext(device=0)
+n = 6 << 20
+a = ctx.alloc(n); a.free()
+assert _lib.mem_stats()["plain_cache_bytes"] == 0, _lib.mem_stats()
+b = ctx.alloc(n); ctx.ipc_export(b.ptr); pb = b.ptr; b.free()
+assert _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
+c = ctx.alloc(n)
+assert c.ptr == pb and _lib.mem_stats()["plain_cache_bytes"] == 0
+c.free()                        # still the ever-exported allocation: kept again
+assert _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
+ctx.close()
+print("OK")
+"""
+    env = dict(os.environ, UCX_BUILTIN_DEV_CACHE_BYTES="0")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+
+
+@pytest.mark.gpu
 def test_plain_allocations_reused_whole(dev_ctx):
     """Round 4: a freed ucg_builtin_dev_malloc allocation is
     kept and handed out again, whole, for the next allocation of its size - the

@@ -50,6 +50,7 @@
 #include <thread>
 #include <tuple>
 #include <unordered_map>
+#include <vector>
 
 #include "dev_internal.h"
 
@@ -71,6 +72,7 @@ struct own_alloc {
     size_t   bytes;
     hipMemGenericAllocationHandle_t handle;   /* KIND_VMM */
     uint64_t key_id;                          /* 0: never exported */
+    bool     exported;                        /* KIND_PLAIN: ever exported */
 };
 
 std::mutex g_mu;                                      /* guards everything here */
@@ -82,9 +84,13 @@ std::unordered_map<void*, own_alloc> g_allocs;        /* base -> allocation */
  * 7, tools/va_reuse_probe). Reusing the allocation itself - same address,
  * same memory - never remaps anything. Its keys are retired at free all the
  * same (a peer's old key is refused), and the device is synchronised before
- * it is handed out again. Bounded by UCX_BUILTIN_DEV_CACHE_BYTES (default
- * 1 GiB per process; 0 = free at once); past the bound it is freed. */
-std::multimap<std::pair<int, size_t>, void*> g_plain_cache;   /* (device, bytes) */
+ * it is handed out again. Never-exported allocations are bounded by
+ * UCX_BUILTIN_DEV_CACHE_BYTES (default 1 GiB per process; 0 = free at once)
+ * and freed past the bound; an allocation that was ever exported is always
+ * kept (round 5: given back to the runtime, its address returns with other
+ * memory, and peers' fresh hipIpc imports of it can map another process's
+ * memory). The value is (pointer, ever exported). */
+std::multimap<std::pair<int, size_t>, std::pair<void*, bool>> g_plain_cache;  /* (device, bytes) */
 size_t g_plain_cached = 0;
 uint64_t g_parked = 0;           /* bytes parked by ucg_builtin_dev_park */
 
@@ -105,22 +111,29 @@ size_t plain_cache_limit()
     return lim;
 }
 
-/* give every cached allocation back to the runtime (hipMalloc ran out of
- * memory: the cache may hold what it needs, at other sizes); returns how
- * many. Caller does not hold g_mu. */
+/* give the never-exported cached allocations back to the runtime (hipMalloc
+ * ran out of memory: the cache may hold what it needs, at other sizes);
+ * returns how many. Caller does not hold g_mu. */
 size_t plain_cache_drain()
 {
-    std::multimap<std::pair<int, size_t>, void*> all;
+    std::vector<std::pair<int, void*>> out;
     {
         std::lock_guard<std::mutex> g(g_mu);
-        all.swap(g_plain_cache);
-        g_plain_cached = 0;
+        for (auto it = g_plain_cache.begin(); it != g_plain_cache.end();) {
+            if (!it->second.second) {
+                out.emplace_back(it->first.first, it->second.first);
+                g_plain_cached -= it->first.second;
+                it = g_plain_cache.erase(it);
+            } else {
+                ++it;
+            }
+        }
     }
-    for (auto &kv : all) {
-        (void)hipSetDevice(kv.first.first);
-        (void)hipFree(kv.second);
+    for (auto &d : out) {
+        (void)hipSetDevice(d.first);
+        (void)hipFree(d.second);
     }
-    return all.size();
+    return out.size();
 }
 
 /* The last memory events of the process, for ucg_builtin_dev_debug_ptr: a
@@ -733,6 +746,7 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
         g_export_of[(void*)base] = id;
         if (own != g_allocs.end()) {
             own->second.key_id = id;
+            own->second.exported = true;
         }
     }
     note_event('X', (void*)dev_ptr, (void*)base, size, 0);
@@ -921,10 +935,11 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         auto c = g_plain_cache.upper_bound({device, bytes});
         if (c != g_plain_cache.begin() &&
             (c = std::prev(c))->first == std::make_pair(device, bytes)) {
-            p = c->second;
+            p = c->second.first;
+            const bool was_exported = c->second.second;
             g_plain_cache.erase(c);
             g_plain_cached -= bytes;
-            g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0};
+            g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0, was_exported};
             note_event('R', p, p, bytes, 0);
             return p;
         }
@@ -940,7 +955,7 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         return nullptr;
     }
     std::lock_guard<std::mutex> g(g_mu);
-    g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0};
+    g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0, false};
     note_event('M', p, p, bytes, 0);
     return p;
 }
@@ -998,7 +1013,7 @@ void *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         return nullptr;
     }
     std::lock_guard<std::mutex> g(g_mu);
-    g_allocs[va] = own_alloc{KIND_VMM, device, bytes, h, 0};
+    g_allocs[va] = own_alloc{KIND_VMM, device, bytes, h, 0, false};
     note_event('V', va, va, bytes, 0);
     return va;
 }
@@ -1057,22 +1072,22 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
     } else if (own && a.kind == KIND_PLAIN) {
         /* as hipFree does: nothing queued may still use it; then kept for
          * the next allocation of its size (g_plain_cache), exported or not.
-         * An exported allocation must not go back to the runtime: the next
-         * hipMalloc hands its address out again with other memory, and a
-         * peer's hipIpcOpenMemHandle of the new allocation's handle can
-         * return a mapping of the old memory - 3,608 of 6,974 peer reads in
-         * 12 processes recycling hipMalloc buffers read the previous
-         * round's data (tools/va_reuse_probe ipc). Reused here
-         * it is the same memory, so such a mapping still reads right. A
-         * buffer that a peer may still be reading is parked instead
-         * (ucg_builtin_dev_park: ADVICE r04). */
+         * An allocation that was ever exported must not go back to the
+         * runtime, so it is kept whatever the bound: the next hipMalloc
+         * hands its address out again with other memory, and peers' fresh
+         * hipIpcOpenMemHandle of a recycled address read another process's
+         * buffer in 3,608 of 6,974 checks (12 processes,
+         * tools/va_reuse_probe ipc). Reused here it is the same
+         * memory. A buffer that a peer may still be reading is parked
+         * instead (ucg_builtin_dev_park: ADVICE r04). */
         (void)hipSetDevice(a.device);
         e = hipDeviceSynchronize();
         bool kept = false;
         {
             std::lock_guard<std::mutex> g(g_mu);
-            if (g_plain_cached + a.bytes <= plain_cache_limit()) {
-                g_plain_cache.emplace(std::make_pair(a.device, a.bytes), ptr);
+            if (a.exported || g_plain_cached + a.bytes <= plain_cache_limit()) {
+                g_plain_cache.emplace(std::make_pair(a.device, a.bytes),
+                                      std::make_pair(ptr, a.exported));
                 g_plain_cached += a.bytes;
                 kept = true;
             }
