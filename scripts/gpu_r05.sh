@@ -36,6 +36,23 @@ for step in "$@"; do
             tag=$(echo $spec | tr ' ' '_')
             timeout -k 10 200 tools/tune_multi_pf $spec 9 > $OUT/pf2_$tag.txt 2>&1 || exit 1
         done ;;
+    pf3)
+        for spec in "multi 8 24" "multi 8 26" "multi 16 24"; do
+            tag=$(echo $spec | tr ' ' '_')
+            timeout -k 10 200 tools/tune_multi_pf $spec 9 > $OUT/pf3_$tag.txt 2>&1 || exit 1
+        done
+        for c in FETCH_SIZE WRITE_SIZE; do
+            timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv \
+                -d $OUT/pf3_pmc/pmc_$c -o s -- tools/tune_multi_pf multi 8 24 1 \
+                > $OUT/pf3_pmc_$c.txt 2>&1 || exit 1
+        done
+        python3 scripts/pmc_kernels.py $OUT/pf3_pmc > $OUT/pf3_pmc_by_kernel.txt 2>&1 ;;
+    pf4)
+        # prefetch distance: the tree fan-in's A/B, and the multi product at two tiles
+        for spec in "tree 8 24" "tree 16 24" "tree 3 24" "tree 12 24" "tree 8 26" "multi 8 24" "multi 16 24"; do
+            tag=$(echo $spec | tr ' ' '_')
+            timeout -k 10 200 tools/tune_multi_pf $spec 9 > $OUT/pf4_$tag.txt 2>&1 || exit 1
+        done ;;
     pf_pmc)
         # one rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE cannot share one)
         for spec in "multi 8 24" "tree 8 24" "tree 3 24"; do

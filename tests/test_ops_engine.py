@@ -726,3 +726,16 @@ def test_shm_iface_reopened_at_once_by_every_member():
     instance (the barrier of each instance would hang otherwise)."""
     codes, outs = launch("_worker_reopen.py", 4, args=(shm_name(), 30), timeout=120)
     assert codes == [0] * 4, "\n".join(outs)
+
+
+@pytest.mark.gpu
+def test_group_destroy_parks_buffers_a_peer_may_read(monkeypatch):
+    """an op on device buffers that ends before every peer is done
+    (here: a timeout, member 1 never starting) leaves its exposed buffer taken,
+    and destroying the group parks it (ucg_builtin_dev_park) rather than
+    returning it to the reuse cache, where the next allocation of its size
+    would change it under the reader."""
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
+    codes, outs = launch("_worker_park.py", 2, args=(shm_name(),), timeout=150)
+    assert codes == [0, 0], "\n".join(outs)
+    assert "parked" in outs[0], outs[0]

@@ -64,9 +64,10 @@ k_read_only(float *dst, SrcList srcs, size_t nvec)
 template <int N>
 static void add_multi(std::vector<Variant> &vs)
 {
-#define MV(label, XM, CAP, PF, PFM, CHK)                                               \
+#define MV(label, XM, CAP, PF, PFM, CHK, ...)                                          \
     vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {           \
-        hipLaunchKernelGGL((k_reduce_multi<float, 0, N, XM, CAP, PF, PFM>), dim3(tiles(nv)), \
+        hipLaunchKernelGGL((k_reduce_multi<float, 0, N, XM, CAP, PF, PFM __VA_OPT__(,) __VA_ARGS__>), \
+                           dim3(tiles(nv)), \
                            dim3(kReduceBlock), 0, q, d, s, 0u, (size_t)0, nv, (size_t)0); \
     }, CHK, {}})
     MV("round-4 product (capped, identity map)", 0, 1, 0, 0, true);
@@ -79,6 +80,9 @@ static void add_multi(std::vector<Variant> &vs)
     MV("PF1, operand 0 only", 1, 1, 1, 1, true);
     MV("PF1, half the operands", 1, 1, 1, (N / 2 > 0 ? N / 2 : 1), true);
     MV("PF1, two operands", 1, 1, 1, (N >= 2 ? 2 : 1), true);
+    MV("PF1, all operands, 2 tiles ahead", 1, 1, 1, N, true, 2);
+    MV("PF1, all operands, 4 tiles ahead", 1, 1, 1, N, true, 4);
+    MV("PF1, operand 0 only, 2 tiles ahead", 1, 1, 1, 1, true, 2);
     MV("PF3, all operands, uncapped", 1, 0, 3, N, true);
     MV("PF1, all operands, uncapped", 1, 0, 1, N, true);
 #undef MV
@@ -91,9 +95,10 @@ static void add_multi(std::vector<Variant> &vs)
 template <int NMAX>
 static void add_tree(std::vector<Variant> &vs, unsigned n)
 {
-#define TV(label, XM, CAP, PF, PFM)                                                     \
+#define TV(label, XM, CAP, PF, PFM, ...)                                                \
     vs.push_back({label, [n](float *d, SrcList s, size_t nv, hipStream_t q) {           \
-        hipLaunchKernelGGL((k_reduce_tree<float, 0, NMAX, XM, CAP, PF, PFM>), dim3(tiles(nv)), \
+        hipLaunchKernelGGL((k_reduce_tree<float, 0, NMAX, XM, CAP, PF, PFM __VA_OPT__(,) __VA_ARGS__>), \
+                           dim3(tiles(nv)), \
                            dim3(kReduceBlock), 0, q, d, s, n, (size_t)0, nv, (size_t)0); \
     }, true, {}})
     constexpr int C = NMAX >= 8;    /* the product caps NMAX 8 and 16 */
@@ -105,6 +110,9 @@ static void add_tree(std::vector<Variant> &vs, unsigned n)
     TV("PF3, operand 0 only", 1, C, 3, 1);
     TV("PF1, operand 0 only", 1, C, 1, 1);
     TV("PF1, first half", 1, C, 1, NMAX / 2);
+    TV("PF1, all operands, 2 tiles ahead", 1, C, 1, NMAX, 2);
+    TV("PF1, all operands, 4 tiles ahead", 1, C, 1, NMAX, 4);
+    TV("PF1, operand 0 only, 2 tiles ahead", 1, C, 1, 1, 2);
 #undef TV
 }
 

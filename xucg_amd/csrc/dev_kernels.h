@@ -326,18 +326,19 @@ __device__ __forceinline__ E rd_tree(E (&val)[N], F f)
 
 /* The next-tile prefetch of k_reduce's PF form, for the in-phase multi-operand
  * kernels (k_reduce_multi, k_reduce_tree): with the XCD-aware tile map, the
- * last PF lanes of a wave load the first PF 128-B lines of the next tile of
- * each of the operands `ops[0 .. PFM)` with temporal loads and discard them;
+ * last PF lanes of a wave load the first PF 128-B lines of the tile D tiles
+ * ahead of each of the operands `ops[0 .. PFM)` with temporal loads and
+ * discard them;
  * every other lane reloads the operand's last vector (one line, an L2 hit),
  * so no branch separates the loads. The loads are issued with the tile's own
  * and kept alive by an empty asm after the sched barrier. */
-template <int PF, int PFM>
+template <int PF, int PFM, int D>
 __device__ __forceinline__ void next_tile_lines(const u32x4 *const (&ops)[PFM > 0 ? PFM : 1],
                                                 size_t i, size_t nvec)
 {
     if constexpr (PF > 0 && PFM > 0) {
         const unsigned k  = kReduceBlock - 1 - threadIdx.x;
-        const size_t want = (i - threadIdx.x + kReduceBlock) + (size_t)k * 8;
+        const size_t want = (i - threadIdx.x + (size_t)D * kReduceBlock) + (size_t)k * 8;
         const size_t at   = (k < (unsigned)PF && want < nvec) ? want : nvec - 1;
         u32x4 pf[PFM];
 #pragma unroll
@@ -354,7 +355,8 @@ __device__ __forceinline__ void next_tile_lines(const u32x4 *const (&ops)[PFM > 
     }
 }
 
-template <typename T, int OP, int N, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0>
+template <typename T, int OP, int N, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0,
+          int PFD = 1>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                size_t tail)
@@ -410,7 +412,7 @@ k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
         for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
             pops[m] = op[m];
         }
-        next_tile_lines<PF, PFM>(pops, i, nvec);
+        next_tile_lines<PF, PFM, PFD>(pops, i, nvec);
         if (i < nvec) {
             st16<1>(d4 + i, rd_tree<N>(val, fv));
         }
@@ -546,7 +548,8 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
  * two, and for MPI_Reduce). Operands past n load srcs[0] again (an L2 hit,
  * no branch between the loads) and are not combined.
  */
-template <typename T, int OP, int NMAX, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0>
+template <typename T, int OP, int NMAX, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0,
+          int PFD = 1>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
 {
@@ -598,7 +601,7 @@ k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t
         for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
             pops[m] = op[m];
         }
-        next_tile_lines<PF, PFM>(pops, i, nvec);
+        next_tile_lines<PF, PFM, PFD>(pops, i, nvec);
         if (i < nvec) {
             u32x4 acc = val[0];
 #pragma unroll

@@ -92,6 +92,15 @@ constexpr int kPrefetchLines = 3;
  * fetches its lines again: n = 6 read 78.4 % with every operand). */
 constexpr int kMultiPrefetchLines = 1;
 
+/* How far ahead that line lies, in tiles (tools/tune_multi_pf, profiles/r05/
+ * pf3, A/B in one process, every operand): k_reduce_multi two tiles ahead,
+ * N = 8 at 64 MiB per operand 84.3 % of 8 TB/s against 82.2 % one tile
+ * ahead, 80.0 against 78.6 % at 256 MiB, N = 16 81.7 against 81.4 %; four
+ * and eight tiles are no better. The tree fan-in keeps one tile until its
+ * own A/B (profiles/r05/pf4). */
+constexpr int kMultiPrefetchTiles = 2;
+constexpr int kTreePrefetchTiles  = 1;
+
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
@@ -256,7 +265,8 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             if constexpr (N >= 8) {
                 if (cap) {
                     /* the PF form: XCD map, the next tile's line of every operand */
-                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N>),
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N,
+                                                       kMultiPrefetchTiles>),
                                        g, b, 0, st, d + off, sl, self, h, chunk, t);
                 } else if constexpr (uncapped_ab<T, OP>()) {
                     if (xm)
@@ -378,19 +388,19 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
             const dim3 g(grid), b(kReduceBlock);
-            constexpr int L = kMultiPrefetchLines;
+            constexpr int L = kMultiPrefetchLines, D = kTreePrefetchTiles;
             if constexpr (!can_cap) {
                 /* the PF form: the root's next line */
-                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 0, L, 1>), g, b, 0, st,
+                hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 0, L, 1, D>), g, b, 0, st,
                                    d + off, sl, n, h, chunk, t);
             } else if (cap) {
                 /* the PF form, capped: every operand's next line when n fills
                  * NMAX, else the root's only */
                 if (n == (unsigned)NMAX)
-                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX>), g, b, 0, st,
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX, D>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);
                 else
-                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, 1>), g, b, 0, st,
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, 1, D>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);
             } else if constexpr (uncapped_ab<T, OP>()) {
                 if (xm)
