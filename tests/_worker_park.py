@@ -43,7 +43,7 @@ def main():
         group.close()
         parked = _lib.mem_stats()["parked_bytes"] - p0
         print(f"rank 0: status {st} parked {parked}", flush=True)
-        if st != xucg_amd.UCS_ERR_TIMED_OUT or parked <= 0:
+        if st != _lib.UCS_ERR_TIMED_OUT or parked <= 0:
             print("rank 0: FAIL: the op did not time out, or nothing was parked", flush=True)
             rc = 1
         s.free()

@@ -93,13 +93,15 @@ constexpr int kPrefetchLines = 3;
 constexpr int kMultiPrefetchLines = 1;
 
 /* How far ahead that line lies, in tiles (tools/tune_multi_pf, profiles/r05/
- * pf3, A/B in one process, every operand): k_reduce_multi two tiles ahead,
- * N = 8 at 64 MiB per operand 84.3 % of 8 TB/s against 82.2 % one tile
- * ahead, 80.0 against 78.6 % at 256 MiB, N = 16 81.7 against 81.4 %; four
- * and eight tiles are no better. The tree fan-in keeps one tile until its
- * own A/B (profiles/r05/pf4). */
-constexpr int kMultiPrefetchTiles = 2;
-constexpr int kTreePrefetchTiles  = 1;
+ * pf3 and pf4, A/B in one process). Every operand prefetched: two tiles
+ * ahead; k_reduce_multi N = 8 at 64 MiB per operand 84.3 / 85.4 % of 8 TB/s
+ * (two runs) against 82.2 / 84.4 % one tile ahead, 80.0 against 78.6 % at
+ * 256 MiB, N = 16 81.7 / 81.5 against 81.4 / 81.2 %; the tree fan-in at
+ * n = NMAX = 8 85.1 against 83.8 %, equal at 256 MiB and at NMAX = 16. Four
+ * and eight tiles are no better. The root's operand alone (tree, n < NMAX):
+ * one tile ahead; two lost 1.1 points at n = 3 and were equal at n = 12. */
+constexpr int kFullPrefetchTiles = 2;
+constexpr int kRootPrefetchTiles = 1;
 
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
@@ -266,7 +268,7 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
                 if (cap) {
                     /* the PF form: XCD map, the next tile's line of every operand */
                     hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N,
-                                                       kMultiPrefetchTiles>),
+                                                       kFullPrefetchTiles>),
                                        g, b, 0, st, d + off, sl, self, h, chunk, t);
                 } else if constexpr (uncapped_ab<T, OP>()) {
                     if (xm)
@@ -388,7 +390,8 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
                 grid = (unsigned)div_up(head, kReduceBlock);
             }
             const dim3 g(grid), b(kReduceBlock);
-            constexpr int L = kMultiPrefetchLines, D = kTreePrefetchTiles;
+            constexpr int L = kMultiPrefetchLines;
+            constexpr int D = kRootPrefetchTiles, DF = kFullPrefetchTiles;
             if constexpr (!can_cap) {
                 /* the PF form: the root's next line */
                 hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 0, L, 1, D>), g, b, 0, st,
@@ -397,7 +400,7 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
                 /* the PF form, capped: every operand's next line when n fills
                  * NMAX, else the root's only */
                 if (n == (unsigned)NMAX)
-                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX, D>), g, b, 0, st,
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX, DF>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);
                 else
                     hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, 1, D>), g, b, 0, st,
