@@ -53,6 +53,14 @@ for step in "$@"; do
             tag=$(echo $spec | tr ' ' '_')
             timeout -k 10 200 tools/tune_multi_pf $spec 9 > $OUT/pf4_$tag.txt 2>&1 || exit 1
         done ;;
+    stagger)
+        # do operands a power of two apart lose to HBM channel conflicts?
+        for spec in "multi 8 26" "multi 8 24" "tree 8 26"; do
+            for sg in 0 4352 2105600; do
+                tag=$(echo $spec $sg | tr ' ' '_')
+                timeout -k 10 200 tools/tune_multi_pf $spec 5 $sg > $OUT/stagger_$tag.txt 2>&1 || exit 1
+            done
+        done ;;
     pf_pmc)
         # one rocprofv3 pass per counter (FETCH_SIZE and WRITE_SIZE cannot share one)
         for spec in "multi 8 24" "tree 8 24" "tree 3 24"; do

@@ -119,13 +119,16 @@ static void add_tree(std::vector<Variant> &vs, unsigned n)
 int main(int argc, char **argv)
 {
     if (argc < 3 || (strcmp(argv[1], "multi") && strcmp(argv[1], "tree"))) {
-        fprintf(stderr, "usage: tune_multi_pf multi|tree N [lg=24] [rounds=5]\n");
+        fprintf(stderr, "usage: tune_multi_pf multi|tree N [lg=24] [rounds=5] [stagger=0]\n");
         return 2;
     }
     const bool tree  = !strcmp(argv[1], "tree");
     const unsigned N = (unsigned)atoi(argv[2]);
     const int lg     = argc > 3 ? atoi(argv[3]) : 24;
     const int rounds = argc > 4 ? atoi(argv[4]) : 5;
+    /* operand m starts m * stagger bytes past m * S (a multiple of 256 B):
+     * do operands a power of two apart meet in the same HBM channels? */
+    const size_t stagger = argc > 5 ? (size_t)atol(argv[5]) & ~(size_t)255 : 0;
     const int iters  = 10;
     if ((!tree && (N != 2 && N != 4 && N != 8 && N != 16)) || (tree && (N < 2 || N > 16))) {
         fprintf(stderr, "N: multi 2/4/8/16, tree 2..16\n");
@@ -133,10 +136,11 @@ int main(int argc, char **argv)
     }
     const size_t n = (size_t)1 << lg, nvec = n / 4, S = n * 4;
     char *arena;
-    CHECK(hipMalloc(&arena, (N + 2) * S));
+    const size_t slot = S + stagger;
+    CHECK(hipMalloc(&arena, (N + 2) * slot));
     SrcList srcs;
     for (unsigned m = 0; m < (unsigned)kMaxMulti; m++) {
-        srcs.p[m] = m < N ? arena + m * S : nullptr;
+        srcs.p[m] = m < N ? arena + m * slot : nullptr;
     }
     {
         std::vector<float> h(n);
@@ -148,8 +152,8 @@ int main(int argc, char **argv)
             CHECK(hipMemcpy(const_cast<void*>(srcs.p[m]), h.data(), S, hipMemcpyHostToDevice));
         }
     }
-    float *out = reinterpret_cast<float*>(arena + N * S);
-    float *ref = reinterpret_cast<float*>(arena + (N + 1) * S);
+    float *out = reinterpret_cast<float*>(arena + N * slot);
+    float *ref = reinterpret_cast<float*>(arena + (N + 1) * slot);
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
 
@@ -209,8 +213,9 @@ int main(int argc, char **argv)
         }
     }
     const double bytes = (double)(N + 1) * S;
-    printf("%s %u, %zu MiB per operand, (N+1)*S = %.0f MiB per launch, %d rounds x %d\n",
-           tree ? "tree n =" : "multi N =", N, S >> 20, bytes / 1048576.0, rounds, iters);
+    printf("%s %u, %zu MiB per operand, (N+1)*S = %.0f MiB per launch, %d rounds x %d, "
+           "stagger %zu B\n", tree ? "tree n =" : "multi N =", N, S >> 20, bytes / 1048576.0,
+           rounds, iters, stagger);
     for (auto &v : vs) {
         std::sort(v.ms.begin(), v.ms.end());
         const float med = v.ms[v.ms.size() / 2];
