@@ -325,7 +325,8 @@ int          ucg_builtin_dev_is_shareable(const void *ptr);
 /* Frees either kind (waits for the device first, as hipFree does) and
  * retires the allocation's keys; a pointer of neither is hipFree'd. A freed
  * ucg_builtin_dev_malloc allocation is kept for the next allocation of its
- * size - one that was ever exported always, others up to
+ * size - one that was ever exported always (and also handed out whole for
+ * a request of at least half its size), others up to
  * UCX_BUILTIN_DEV_CACHE_BYTES - so an exported address never comes back from
  * the runtime with other memory behind it. */
 void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);

@@ -549,7 +549,9 @@ def test_exported_allocations_kept_past_the_cache_bound():
     at once, and one that was ever exported is kept all the same - given back
     to the runtime, its address could come back with other memory and peers'
     fresh hipIpc imports of it map another process's buffer.
-    The oom drain gives back only the never-exported ones."""
+    The oom drain gives back only the never-exported ones. A smaller request,
+    at least half the size, takes the kept allocation whole, so a caller whose
+    sizes vary does not add one kept allocation per size."""
     import subprocess
     import sys
     code = r"""
@@ -564,6 +566,14 @@ assert _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
 c = ctx.alloc(n)
 assert c.ptr == pb and _lib.mem_stats()["plain_cache_bytes"] == 0
 c.free()                        # still the ever-exported allocation: kept again
+assert _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
+d = ctx.alloc(4 << 20)          # smaller, at least half its size: the same memory
+assert d.ptr == pb and _lib.mem_stats()["plain_cache_bytes"] == 0, _lib.mem_stats()
+d.free()                        # back whole, at its own size
+assert _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
+e = ctx.alloc(2 << 20)          # under half: a new allocation, freed at once
+assert e.ptr != pb and _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
+e.free()
 assert _lib.mem_stats()["plain_cache_bytes"] == n, _lib.mem_stats()
 ctx.close()
 print("OK")

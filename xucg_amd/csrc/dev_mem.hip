@@ -943,6 +943,22 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
             note_event('R', p, p, bytes, 0);
             return p;
         }
+        /* else the smallest ever-exported one up to twice the size: those are
+         * never given back, so a caller whose sizes vary reuses them rather
+         * than adding one per size */
+        for (auto x = g_plain_cache.lower_bound({device, bytes});
+             x != g_plain_cache.end() && x->first.first == device &&
+             x->first.second <= 2 * bytes; ++x) {
+            if (x->second.second) {
+                const size_t have = x->first.second;
+                p = x->second.first;
+                g_plain_cache.erase(x);
+                g_plain_cached -= have;
+                g_allocs[p] = own_alloc{KIND_PLAIN, device, have, {}, 0, true};
+                note_event('R', p, p, have, 0);
+                return p;
+            }
+        }
     }
     hipError_t e = hipMalloc(&p, bytes);
     if (e == hipErrorOutOfMemory && plain_cache_drain() > 0) {
