@@ -1,5 +1,5 @@
 #!/bin/bash
-# Allocation race probe (xucg_amd/csrc/alloc_race_probe.hip): NP processes on
+# Allocation race probe (tools/src/alloc_race_probe.hip): NP processes on
 # the one GPU allocate, upload, verify, use and free 2 MiB buffers with no
 # engine code; then the same with every process exporting a buffer and
 # importing every peer's.   usage: scripts/alloc_race.sh OUTDIR [NP] [ITERS]
