@@ -24,6 +24,13 @@ extern "C" {
 void ucg_builtin_component_set_classifier(ucg_builtin_op_classifier_f op_cls,
                                           ucg_builtin_dt_classifier_f dt_cls);
 
+/* The vtable's destroy returns nothing (api/ucg_plan_component.h:161-162),
+ * yet a group's tear-down can fail: a member's process gone
+ * (UCS_ERR_CONNECTION_RESET) or its last barrier timed out. destroy then
+ * still frees everything, warns on stderr and keeps the status here: the
+ * status of the last group destroy of this process (UCS_OK if none failed). */
+ucs_status_t ucg_builtin_component_last_destroy_status(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,7 +92,8 @@ typedef enum {
     UCS_ERR_OUT_OF_RANGE    = -19,
     UCS_ERR_TIMED_OUT       = -20,
     UCS_ERR_EXCEEDS_LIMIT   = -21,
-    UCS_ERR_UNSUPPORTED     = -22
+    UCS_ERR_UNSUPPORTED     = -22,
+    UCS_ERR_CONNECTION_RESET = -25
 } ucs_status_t;
 #endif
 #endif

@@ -60,8 +60,16 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
                                         unsigned my_index, size_t max_short,
                                         unsigned ring_cells,
                                         ucg_builtin_shm_iface_t **iface_p);
-void         ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *iface);
+/* UCS_OK, or - a member's process gone, or the last barrier timed out - the
+ * failure; the object is unmapped either way (never aborts the process) */
+ucs_status_t ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *iface);
 size_t       ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *iface);
+/* The job token this process stamps into the objects it creates (the first
+ * of UCX_BUILTIN_JOB_TOKEN, PMIX_NAMESPACE, OMPI_MCA_ess_base_jobid,
+ * SLURM_JOB_ID:SLURM_STEP_ID, TORCHELASTIC_RUN_ID unless "none",
+ * MASTER_ADDR:MASTER_PORT; 0 = none): a member refuses a live object of
+ * another token. */
+uint64_t     ucg_builtin_shm_job_token(void);
 /* uct_ep_am_short: UCS_ERR_NO_RESOURCE when the peer's ring is full */
 ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *iface,
                                       unsigned peer, uint64_t header,
@@ -96,8 +104,11 @@ ucs_status_t ucg_builtin_shm_am_incast_batched(ucg_builtin_shm_iface_t *iface,
                                                unsigned root, uint64_t header,
                                                unsigned expected, const void *payload,
                                                size_t length);
-/* Blocking barrier of all members (set-up / tear-down only). */
-void         ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *iface);
+/* Blocking barrier of all members (set-up / tear-down only): UCS_OK,
+ * UCS_ERR_CONNECTION_RESET when a member's process is gone, UCS_ERR_TIMED_OUT
+ * after UCX_BUILTIN_WAIT_TIMEOUT seconds; after a failure every later
+ * barrier returns it at once. */
+ucs_status_t ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *iface);
 
 /* ---- f1: group and collective engine ------------------------------------ */
 typedef struct ucg_builtin_lgroup ucg_builtin_lgroup_t;

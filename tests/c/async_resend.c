@@ -38,8 +38,9 @@
  *           of its process is armed to fail (ucg_builtin_dev_inject_failure):
  *           the timer thread's combine fails, and member 0's completion
  *           status must be that error (recv_handle_error,
- *           builtin_comp_step.inl:332-333); the other members may then end
- *           with their wait timeout, never with a wrong result
+ *           builtin_comp_step.inl:332-333); the other members end with
+ *           UCS_ERR_CANCELED as soon as they see member 0 gave up on the op
+ *           (round 6), never with a wrong result or a wait timeout
  */
 #define _GNU_SOURCE
 #include <stdio.h>
@@ -223,11 +224,6 @@ static int run(char **argv, const char *mode, int round_inputs, int fail)
         }
         st = (st == UCS_INPROGRESS) ? ucg_builtin_lcoll_wait(c) : st;
     }
-    if (fail && rank == 0 && getenv("UCX_BUILTIN_WAIT_TIMEOUT")) {
-        /* member 1 may be waiting for the rest of this member's step until
-         * its wait times out: meet it at the last barrier well after that */
-        usleep((useconds_t)(atof(getenv("UCX_BUILTIN_WAIT_TIMEOUT")) * 0.5e6));
-    }
     if (device && st == UCS_OK &&
         ucg_builtin_dev_memcpy(dctx, out, rbuf, count * sizeof(float)) != UCS_OK) {
         fprintf(stderr, "rank %u: download: %s\n", rank, ucg_builtin_dev_last_error());
@@ -253,8 +249,13 @@ static int run(char **argv, const char *mode, int round_inputs, int fail)
             fprintf(stderr, "rank 0: status %d, not the injected device error\n", st);
             ok = 0;
         }
-        if (rank != 0 && st != UCS_OK && st != UCS_ERR_TIMED_OUT) {
-            fprintf(stderr, "rank %u: status %d\n", rank, st);
+        /* member 0 published that it gave up on the op (finish ->
+         * shm_abandon): a member still waiting for its fragments ends with
+         * UCS_ERR_CANCELED at once, not with its wait timeout - no member
+         * has to be timed to meet the others at the last barrier */
+        if (rank != 0 && st != UCS_OK && st != UCS_ERR_CANCELED) {
+            fprintf(stderr, "rank %u: status %d, not OK or the peer's cancellation\n",
+                    rank, st);
             ok = 0;
         }
     } else if (st != UCS_OK) {
@@ -262,10 +263,16 @@ static int run(char **argv, const char *mode, int round_inputs, int fail)
                 (staged || device) ? ucg_builtin_dev_last_error() : "");
         ok = 0;
     }
-    ucg_builtin_shm_barrier(iface);
+    if ((st = ucg_builtin_shm_barrier(iface)) != UCS_OK) {
+        fprintf(stderr, "rank %u: last barrier: status %d\n", rank, st);
+        ok = 0;
+    }
     ucg_builtin_lcoll_destroy(c);
     ucg_builtin_lgroup_destroy(g);
-    ucg_builtin_shm_iface_close(iface);
+    if ((st = ucg_builtin_shm_iface_close(iface)) != UCS_OK) {
+        fprintf(stderr, "rank %u: close: status %d\n", rank, st);
+        ok = 0;
+    }
     ucg_builtin_combine_destroy(cmb);
     if (dctx) {
         ucg_builtin_dev_free(dctx, sbuf);

@@ -187,11 +187,11 @@ def test_async_resend_timer_device_failure_reaches_completion(monkeypatch, mode)
     ucg_builtin_dev_inject_failure just before its owner thread goes quiet):
     member 0's operation completes with that error, UCS_ERR_IO_ERROR, as the
     reference's recv_handle_error path ends an op (builtin_comp_step.inl:
-    332-333, builtin.c:260-294); member 1 ends cleanly or by its wait
-    timeout, never with a wrong result."""
-    # member 1 may wait for fragments member 0 dropped with its op: its wait
-    # gives up after 20 s (its start-up, HIP init included, fits well inside)
-    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "20")
+    332-333, builtin.c:260-294); member 1 ends cleanly or, seeing that
+    member 0 gave up on the op, with UCS_ERR_CANCELED - never with a wrong
+    result, and without any member timed to meet the other (round 6: no
+    sleep before the last barrier, whose status must be UCS_OK)."""
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
     exe = os.path.join(ROOT, "tests", "c", "_build", "async_resend")
     codes, outs = launch_exe(exe, 2, (shm_name(), mode, "round", "fail"), timeout=120)
     assert codes == [0, 0], "\n".join(outs)
@@ -199,6 +199,67 @@ def test_async_resend_timer_device_failure_reaches_completion(monkeypatch, mode)
     lines = [json.loads(ln) for ln in outs[0].splitlines() if ln.startswith("{")]
     st0 = [x for x in lines if "status" in x][0]
     assert st0["rank"] == 0 and st0["status"] == -3 and st0["injected_fired"] == 1, st0
+    st1 = [json.loads(ln) for ln in outs[1].splitlines() if ln.startswith("{")][-1]
+    assert st1["status"] in (0, -16), st1          # UCS_OK or UCS_ERR_CANCELED
+
+
+@pytest.mark.parametrize("mode,world,victim", [("exit-before", 3, 1), ("exit-before", 4, 0),
+                                               ("exit-during", 4, 2), ("exit-during", 2, 0),
+                                               ("cancel", 4, 3), ("cancel", 3, 0)])
+def test_peer_failure_ends_ops_with_status_not_abort(monkeypatch, mode, world, victim):
+    """a member that fails never takes its peers down. Its
+    process gone (before or during the op): every survivor's op ends with
+    UCS_ERR_CONNECTION_RESET and its close returns that status, within a
+    fraction of the wait timeout, and the survivor exits 0 (no abort() in the
+    barrier, the incast lock or close). A member that gives up on the op
+    (destroys it while it runs): the others end it with UCS_ERR_CANCELED as
+    soon as they see it published, and the last barrier and close succeed.
+    The reference ends ops with a status (recv_handle_error,
+    builtin_comp_step.inl:332-333)."""
+    import json
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "60")
+    codes, outs = launch("_worker_fail.py", world, args=(shm_name(), mode, victim),
+                         timeout=120)
+    for r in range(world):
+        if r == victim and mode != "cancel":
+            continue
+        assert codes[r] == 0, "\n".join(outs)
+        line = json.loads([ln for ln in outs[r].splitlines() if ln.startswith("{")][-1])
+        if r == victim:
+            assert line["close"] == 0, line
+            continue
+        want = _lib_status("UCS_ERR_CANCELED" if mode == "cancel" else
+                           "UCS_ERR_CONNECTION_RESET")
+        assert line["status"] == want and line["took_s"] < 20, (line, outs)
+        assert line["close"] == (0 if mode == "cancel" else want), line
+        assert "Aborted" not in outs[r] and "Fatal" not in outs[r], outs[r]
+
+
+def _lib_status(name):
+    from xucg_amd import _lib
+    return getattr(_lib, name)
+
+
+def test_job_token_skips_torchrun_none_run_id(monkeypatch):
+    """torchrun sets TORCHELASTIC_RUN_ID=none for every
+    static-rendezvous job; two such jobs must still get different tokens
+    (from MASTER_ADDR:MASTER_PORT), and a real run id still decides."""
+    from xucg_amd import _lib
+    lib = _lib.host()
+    for v in ("UCX_BUILTIN_JOB_TOKEN", "PMIX_NAMESPACE", "OMPI_MCA_ess_base_jobid",
+              "SLURM_JOB_ID"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    a = lib.ucg_builtin_shm_job_token()
+    monkeypatch.setenv("MASTER_PORT", "29501")
+    b = lib.ucg_builtin_shm_job_token()
+    assert a != 0 and b != 0 and a != b
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "f3a1c0de")
+    c = lib.ucg_builtin_shm_job_token()
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    assert lib.ucg_builtin_shm_job_token() == c and c not in (a, b)
 
 
 @pytest.mark.parametrize("exe,world,args", [("component_test", 4, ("host",)),

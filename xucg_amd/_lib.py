@@ -36,6 +36,7 @@ UCS_ERR_OUT_OF_RANGE = -19
 UCS_ERR_TIMED_OUT = -20
 UCS_ERR_EXCEEDS_LIMIT = -21
 UCS_ERR_UNSUPPORTED = -22
+UCS_ERR_CONNECTION_RESET = -25
 IPC_HANDLE_BYTES = 96  # UCG_BUILTIN_DEV_IPC_HANDLE_BYTES
 
 # every exported C-ABI function: name -> (restype, argtypes)

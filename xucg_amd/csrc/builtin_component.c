@@ -47,6 +47,7 @@
 #include "ucg_builtin_component.h"
 #include "ucg_builtin_ops.h"
 
+#include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -323,7 +324,7 @@ static ucs_status_t ucg_builtin_create(ucg_plan_ctx_h pctx, ucg_group_ctx_h ctx,
 err_group:
     ucg_builtin_lgroup_destroy(gctx->lgroup);
 err_iface:
-    ucg_builtin_shm_iface_close(gctx->iface);
+    (void)ucg_builtin_shm_iface_close(gctx->iface);
 err_cmb:
     ucg_builtin_combine_destroy(gctx->cmb);
     return st;
@@ -341,14 +342,28 @@ static void destroy_plan(ucg_builtin_plan_t *plan)
     free(plan);
 }
 
+static _Atomic int g_destroy_status = UCS_OK;
+
+ucs_status_t ucg_builtin_component_last_destroy_status(void)
+{
+    return (ucs_status_t)atomic_load(&g_destroy_status);
+}
+
 static void ucg_builtin_destroy(ucg_group_ctx_h ctx)
 {
     ucg_builtin_group_ctx_t *gctx = ctx;
+    ucs_status_t st;
     while (!ucs_list_is_empty(&gctx->plans)) {
         destroy_plan(ucs_container_of(gctx->plans.next, ucg_builtin_plan_t, list));
     }
     ucg_builtin_lgroup_destroy(gctx->lgroup);    /* stops the resend timer first */
-    ucg_builtin_shm_iface_close(gctx->iface);
+    /* a peer that is gone ends the close with a status, not the process */
+    st = ucg_builtin_shm_iface_close(gctx->iface);
+    if (st != UCS_OK) {
+        fprintf(stderr, "ucg_builtin: group %u member %u: tear-down with status %d "
+                "(a member failed)\n", (unsigned)gctx->group_id, gctx->my, (int)st);
+    }
+    atomic_store(&g_destroy_status, (int)st);
     ucg_builtin_combine_destroy(gctx->cmb);
 }
 

@@ -34,8 +34,28 @@ typedef struct {
     uint64_t header;    /* followed by the payload: data = &header */
 } cell_t;
 
-#define SEG_CTL_BYTES 128
+#define SEG_HDR_BYTES 128
 #define UNEXP_GROUPS  64
+
+/* Per member, after the object's header: who is attached and which op it
+ * gave up on (round 6). A peer that stops taking part - its
+ * process is gone, or its op ended with an error - must end the ops of the
+ * others with a status, never hang them or kill their process. */
+typedef struct {
+    _Atomic uint64_t pid;       /* the member's process once mapped (0: not yet) */
+    uint64_t         pidns;     /* its pid namespace (0: unknown) */
+    /* per group slot (group_id % UNEXP_GROUPS): the op this member abandoned
+     * last, abandon_word(); 0 = none */
+    _Atomic uint64_t abandoned[UNEXP_GROUPS];
+} member_ctl_t;
+
+/* an abandoned op: the group's incarnation on this iface, its id and the
+ * op's start sequence - the same on every member, since members create
+ * groups and start their ops in the same order (a collective's contract) */
+static inline uint64_t abandon_word(uint16_t gen, uint16_t group_id, uint64_t seq)
+{
+    return ((uint64_t)gen << 48) | ((uint64_t)group_id << 32) | (seq & 0xffffffffull);
+}
 
 /* Incast cell (the SM-root "bcopy into a shared buffer" of the UCX
  * collectives extension the reference's reducing packers are written for,
@@ -78,10 +98,18 @@ struct ucg_builtin_shm_iface {
     int       incast_batched;  /* cells hold every child's message side by side */
     size_t    incast_bytes;    /* one member's incast area */
     size_t    incast_base;     /* offset of member 0's incast area */
+    size_t    ctl_bytes;       /* header + member_ctl_t[members], rounded to 64 */
     size_t    seg_bytes;
     char     *seg;
     uint64_t  barrier_gen;
     ucs_status_t open_status;  /* why ucg_builtin_shm_iface_open failed */
+    /* peer failure (shm_peer_check): the first member found gone, and the
+     * status every later barrier and close returns at once (the barrier's
+     * count is no longer shared once one member gave up on it) */
+    int       dead;            /* member index + 1, 0 = none found */
+    ucs_status_t broken;
+    double    live_check_t;    /* last liveness probe (now_s) */
+    uint16_t  group_gen[UNEXP_GROUPS];  /* groups created per slot */
     /* ops layer: groups by id and messages for groups not created yet
      * (the reference's bctx->group_by_id / bctx->unexpected, builtin.c:
      * 150-205) */
@@ -101,6 +129,19 @@ static inline double wait_timeout_s(void)
     const char *t = getenv("UCX_BUILTIN_WAIT_TIMEOUT");
     return t ? atof(t) : 300.0;
 }
+
+/* how often a waiter that made no progress looks at its peers */
+#define PEER_CHECK_S 0.02
+
+/* builtin_shm.c: peer failure. shm_peer_check: the index of a member whose
+ * process is gone (probed at most every PEER_CHECK_S; sticky), -1 if none -
+ * only called by a member that is idle, so messages a peer sent before it
+ * exited are taken in first. shm_abandon / shm_abandoned: publish / read the
+ * op a member gave up on (member_ctl_t.abandoned). */
+UCG_INTERNAL int      shm_peer_check(ucg_builtin_shm_iface_t *it);
+UCG_INTERNAL void     shm_abandon(ucg_builtin_shm_iface_t *it, unsigned slot, uint64_t word);
+UCG_INTERNAL uint64_t shm_abandoned(ucg_builtin_shm_iface_t *it, unsigned member,
+                                    unsigned slot);
 
 /* ======================================================================== */
 /* f1: engine state                                                         */
@@ -219,6 +260,13 @@ struct ucg_builtin_lgroup {
     _Atomic uint64_t         async_resends;
     unsigned                 mem_reg_opt_cnt; /* starts before registering, 0 = never */
     _Atomic uint64_t         async_combines;   /* combines and folds on the timer thread */
+    /* peer failure: the group's incarnation on its iface, the ops started so
+     * far (an op's sequence number), idle progress calls since the last look
+     * at the peers */
+    uint16_t                 gen;
+    uint64_t                 starts;
+    unsigned                 idle_polls;
+    double                   peer_check_t;
 };
 
 struct ucg_builtin_lcoll {
@@ -304,6 +352,8 @@ struct ucg_builtin_lcoll {
     size_t       comp_flag_off, comp_status_off;
     struct rma_msg *outbox;       /* control messages not sent yet */
     unsigned     out_head, out_tail, out_cap;
+    uint64_t     seq;             /* the group's start count at this start */
+    int          peer_ended;      /* finished because of a peer: not published */
 };
 
 /* planner state (builtin_plan.c) */

@@ -78,7 +78,10 @@ static void slot_stash(op_slot_t *slot, stash_t *m)
     slot->msgs_tail  = &m->next;
 }
 
-/* finish the op: ucg_builtin_comp_last_step_cb, builtin_comp_step.inl:8-38 */
+/* finish the op: ucg_builtin_comp_last_step_cb, builtin_comp_step.inl:8-38.
+ * An op this member gives up on (any error not caused by a peer) is published
+ * (shm_abandon), so that its peers end it with UCS_ERR_CANCELED instead of
+ * waiting for messages that never come (group_check_peers). */
 UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
 {
     op_slot_t *slot = &c->g->slots[c->coll_id % UCG_BUILTIN_OPS_MAX_CONCURRENT];
@@ -88,6 +91,10 @@ UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
             status = st;
         }
         c->step_open = 0;
+    }
+    if (status != UCS_OK && c->active && !c->peer_ended) {
+        shm_abandon(c->g->iface, c->g->group_id,
+                    abandon_word(c->g->gen, c->g->group_id, c->seq));
     }
     c->status       = status;
     c->done         = 1;
@@ -646,6 +653,7 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
                          (params->mem_reg_opt_cnt < 0 ? 0u : (unsigned)params->mem_reg_opt_cnt) :
                          mem_reg_opt_cnt_env();
     rma_group_init(g);
+    g->gen = ++iface->group_gen[group_id % UNEXP_GROUPS];
     iface->groups[group_id % UNEXP_GROUPS] = g;
     /* adopt messages that arrived before the group existed (builtin.c:
      * 424-446) */
@@ -727,14 +735,63 @@ static unsigned group_resend(ucg_builtin_lgroup_t *g)
     return n;
 }
 
+/* Peer failure: every op still running ends with a status
+ * once a member of the iface is gone (UCS_ERR_CONNECTION_RESET: what it sent
+ * before it went was delivered first, a dead process adds nothing more) or a
+ * peer published that it gave up on the same op (UCS_ERR_CANCELED) - the
+ * reference's error completion, recv_handle_error, builtin_comp_step.inl:
+ * 332-333, where a UCX endpoint error would end the request. At most every
+ * PEER_CHECK_S, from a waiter or the timer; called with the group blocked. */
+static void group_check_peers(ucg_builtin_lgroup_t *g)
+{
+    ucg_builtin_shm_iface_t *it = g->iface;
+    const double t = now_s();
+    unsigned i, m;
+    int dead;
+    if (t - g->peer_check_t < PEER_CHECK_S) {
+        return;
+    }
+    g->peer_check_t = t;
+    if ((dead = shm_peer_check(it)) >= 0) {
+        (void)ucg_builtin_shm_progress(it, am_handler, it);
+    }
+    for (i = 0; i < UCG_BUILTIN_OPS_MAX_CONCURRENT; i++) {
+        ucg_builtin_lcoll_t *c = g->slots[i].req;
+        ucs_status_t st = UCS_OK;
+        if (c == NULL || c->done) {
+            continue;
+        }
+        if (dead >= 0) {
+            st = UCS_ERR_CONNECTION_RESET;
+        } else {
+            const uint64_t w = abandon_word(g->gen, g->group_id, c->seq);
+            for (m = 0; m < g->size; m++) {
+                if (m != g->my && shm_abandoned(it, m, g->group_id) == w) {
+                    fprintf(stderr, "ucg_builtin: member %u gave up on collective %u of "
+                            "group %u; ending it here\n", m, c->coll_id, g->group_id);
+                    st = UCS_ERR_CANCELED;
+                    break;
+                }
+            }
+        }
+        if (st != UCS_OK) {
+            c->peer_ended = 1;
+            finish(c, st);
+        }
+    }
+}
+
 /* ucg_builtin_op_progress, builtin.c:318-340: the transport first, then the
- * resend queue */
+ * resend queue; a member that keeps finding nothing looks at its peers */
 unsigned ucg_builtin_lgroup_progress(ucg_builtin_lgroup_t *g)
 {
     unsigned n;
     group_block(g);
     n  = ucg_builtin_shm_progress(g->iface, am_handler, g->iface);
     n += group_resend(g);
+    if (n == 0 && (++g->idle_polls & 1023) == 0) {
+        group_check_peers(g);
+    }
     group_unblock(g);
     return n;
 }
@@ -754,6 +811,7 @@ static void *async_timer(void *arg)
         pthread_cond_timedwait(&g->timer_cv, &g->async_lock, &ts);
         if (!g->timer_stop) {
             g->async_resends += group_resend(g);
+            group_check_peers(g);
         }
     }
     group_unblock(g);
@@ -1036,6 +1094,8 @@ static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id)
     }
     c->coll_id      = coll_id;
     g->next_coll_id = (uint8_t)(coll_id + 1);
+    c->seq          = ++g->starts;
+    c->peer_ended   = 0;
     if (c->rma) {
         return rma_start(c, slot);
     }
@@ -1129,9 +1189,16 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
         if (ucg_builtin_lgroup_progress(c->g) != 0) {
             idle = 0;
             /* progress counts resend attempts too: a peer that stopped
-             * taking messages (its op ended with an error) keeps it
-             * non-zero, so the time limit is checked here as well */
-            if ((++busy & 4095) == 0 && now_s() - t0 > lim) {
+             * taking messages (its op ended with an error, its process is
+             * gone) keeps it non-zero, so the peers and the time limit are
+             * checked here as well */
+            if ((++busy & 4095) != 0) {
+                continue;
+            }
+            group_block(c->g);
+            group_check_peers(c->g);
+            group_unblock(c->g);
+            if (now_s() - t0 > lim) {
                 idle = (unsigned)spin;
             } else {
                 continue;
@@ -1152,6 +1219,9 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
             group_unblock(c->g);
             break;
         }
+        group_block(c->g);
+        group_check_peers(c->g);
+        group_unblock(c->g);
         sched_yield();
     }
     return c->status;

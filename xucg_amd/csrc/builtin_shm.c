@@ -20,7 +20,7 @@
 
 static ring_ctl_t *ring_ctl(ucg_builtin_shm_iface_t *it, unsigned src, unsigned dst)
 {
-    return (ring_ctl_t*)(it->seg + SEG_CTL_BYTES +
+    return (ring_ctl_t*)(it->seg + it->ctl_bytes +
                          ((size_t)src * it->members + dst) * it->ring_bytes);
 }
 
@@ -41,7 +41,7 @@ static incast_cell_t *incast_cell(ucg_builtin_shm_iface_t *it, unsigned member,
                             (size_t)idx * it->incast_cell_size);
 }
 
-/* The object's header (the first SEG_CTL_BYTES): the barrier counter at 0,
+/* The object's header (the first SEG_HDR_BYTES): the barrier counter at 0,
  * then who made it. Member 0 creates the object (O_EXCL) and stamps it with
  * its pid, its pid namespace, the job's token and a random instance; the
  * others map it once it is stamped by a live creator of their own job and the
@@ -67,13 +67,40 @@ typedef struct {
     uint64_t         pidns;             /* the creator's pid namespace (0: unknown) */
     uint64_t         job;               /* the creator's job token (0: none) */
 } seg_hdr_t;
-_Static_assert(sizeof(seg_hdr_t) <= SEG_CTL_BYTES, "segment header size");
+_Static_assert(sizeof(seg_hdr_t) <= SEG_HDR_BYTES, "segment header size");
 #define SHM_STAMP  0x58554347534d3031ull         /* "XUCGSM01" */
 #define SHM_CLOSED 0x58554347534d4344ull
 
+static member_ctl_t *member_ctl(ucg_builtin_shm_iface_t *it, unsigned member)
+{
+    return (member_ctl_t*)(it->seg + SEG_HDR_BYTES) + member;
+}
+
+/* a process that exited but was not reaped yet (a zombie: its launcher has
+ * not waited for it) is gone too, though kill() still finds it */
+static int pid_zombie(uint64_t pid)
+{
+    char path[64], buf[256], *p;
+    ssize_t n;
+    int fd;
+    snprintf(path, sizeof(path), "/proc/%llu/stat", (unsigned long long)pid);
+    if ((fd = open(path, O_RDONLY | O_CLOEXEC)) < 0) {
+        return 0;
+    }
+    n = read(fd, buf, sizeof(buf) - 1);
+    close(fd);
+    if (n <= 0) {
+        return 0;
+    }
+    buf[n] = 0;
+    /* "pid (comm) S ...": the state follows the last ')' */
+    p = strrchr(buf, ')');
+    return p && p[1] == ' ' && (p[2] == 'Z' || p[2] == 'X');
+}
+
 static int pid_alive(uint64_t pid)
 {
-    return pid != 0 && (kill((pid_t)pid, 0) == 0 || errno != ESRCH);
+    return pid != 0 && (kill((pid_t)pid, 0) == 0 || errno != ESRCH) && !pid_zombie(pid);
 }
 
 /* this process's pid namespace: the inode of /proc/self/ns/pid (0: unknown) */
@@ -98,7 +125,8 @@ static int owner_state(uint64_t pid, uint64_t ns)
  * UCX_BUILTIN_JOB_TOKEN, else of the launcher's job id (PMIx namespace, Open
  * MPI's job id, Slurm's job.step, torchrun's run id, the rendezvous
  * MASTER_ADDR:MASTER_PORT); 0 when there is none (a peer can then not tell
- * another job's object from its own: set a job uid). */
+ * another job's object from its own: set a job uid). Exported for the tests
+ * as ucg_builtin_shm_job_token. */
 static uint64_t job_token(void)
 {
     static const char *vars[][2] = {{"UCX_BUILTIN_JOB_TOKEN", NULL},
@@ -113,7 +141,10 @@ static uint64_t job_token(void)
         const char *parts[3];
         uint64_t h = 0xcbf29ce484222325ull;
         unsigned k;
-        if (a == NULL || *a == 0 || b == NULL) {
+        /* torchrun sets TORCHELASTIC_RUN_ID=none for every static-rendezvous
+         * job without --rdzv-id: no job's id, the rendezvous
+         * address decides */
+        if (a == NULL || *a == 0 || b == NULL || strcmp(a, "none") == 0) {
             continue;
         }
         parts[0] = a;
@@ -128,6 +159,56 @@ static uint64_t job_token(void)
         return h ? h : 1;
     }
     return 0;
+}
+
+uint64_t ucg_builtin_shm_job_token(void)
+{
+    return job_token();
+}
+
+/* this member is attached: its process, for the others' liveness probes */
+static void member_attach(ucg_builtin_shm_iface_t *it)
+{
+    member_ctl_t *m = member_ctl(it, it->my);
+    m->pidns = pid_ns();
+    atomic_store_explicit(&m->pid, (uint64_t)getpid(), memory_order_release);
+}
+
+UCG_INTERNAL int shm_peer_check(ucg_builtin_shm_iface_t *it)
+{
+    const double t = now_s();
+    unsigned m;
+    if (it->dead || t - it->live_check_t < PEER_CHECK_S) {
+        return it->dead - 1;
+    }
+    it->live_check_t = t;
+    for (m = 0; m < it->members; m++) {
+        const member_ctl_t *mc = member_ctl(it, m);
+        const uint64_t pid = atomic_load_explicit(&mc->pid, memory_order_acquire);
+        /* not attached yet, or in another pid namespace: cannot tell */
+        if (m == it->my || pid == 0 || owner_state(pid, mc->pidns) != 0) {
+            continue;
+        }
+        fprintf(stderr, "ucg_builtin_shm(%s): member %u (pid %llu) is gone\n", it->name, m,
+                (unsigned long long)pid);
+        it->dead   = (int)m + 1;
+        it->broken = UCS_ERR_CONNECTION_RESET;
+        return (int)m;
+    }
+    return -1;
+}
+
+UCG_INTERNAL void shm_abandon(ucg_builtin_shm_iface_t *it, unsigned slot, uint64_t word)
+{
+    atomic_store_explicit(&member_ctl(it, it->my)->abandoned[slot % UNEXP_GROUPS], word,
+                          memory_order_release);
+}
+
+UCG_INTERNAL uint64_t shm_abandoned(ucg_builtin_shm_iface_t *it, unsigned member,
+                                    unsigned slot)
+{
+    return atomic_load_explicit(&member_ctl(it, member)->abandoned[slot % UNEXP_GROUPS],
+                                memory_order_acquire);
 }
 
 /* an object of another job: both sides carry a token and they differ */
@@ -264,6 +345,7 @@ static ucs_status_t iface_map(ucg_builtin_shm_iface_t *it)
             h->members   = it->members;
             h->pidns     = pid_ns();
             h->job       = job_token();
+            member_attach(it);
             atomic_store_explicit(&h->stamp, SHM_STAMP, memory_order_release);
             return UCS_OK;
         }
@@ -292,6 +374,7 @@ static ucs_status_t iface_map(ucg_builtin_shm_iface_t *it)
             h->members == it->members) {
             peek_hdr(it->name, &ph);
             if (ph.instance == h->instance) {
+                member_attach(it);
                 return UCS_OK;                      /* still the named object */
             }
         } else if (atomic_load_explicit(&h->stamp, memory_order_acquire) == SHM_STAMP &&
@@ -317,6 +400,7 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
                                         ucg_builtin_shm_iface_t **iface_p)
 {
     ucg_builtin_shm_iface_t *it;
+    ucs_status_t st;
 
     if (name == NULL || iface_p == NULL || members == 0 ||
         members > UCG_BUILTIN_OPS_MAX_MEMBERS || my_index >= members ||
@@ -345,7 +429,9 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
                             (it->incast_batched ? members * max_short : max_short - 8) + 63) &
                            ~(size_t)63;
     it->incast_bytes     = sizeof(incast_ctl_t) + (size_t)ring_cells * it->incast_cell_size;
-    it->incast_base      = SEG_CTL_BYTES + (size_t)members * members * it->ring_bytes;
+    it->ctl_bytes        = (SEG_HDR_BYTES + (size_t)members * sizeof(member_ctl_t) + 63) &
+                           ~(size_t)63;
+    it->incast_base      = it->ctl_bytes + (size_t)members * members * it->ring_bytes;
     it->seg_bytes        = it->incast_base + (size_t)members * it->incast_bytes;
 
     if (iface_map(it) != UCS_OK) {
@@ -353,33 +439,52 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
         free(it);
         return st;
     }
-    ucg_builtin_shm_barrier(it);   /* everybody mapped before any send */
+    st = ucg_builtin_shm_barrier(it);   /* everybody mapped before any send */
+    if (st != UCS_OK) {
+        (void)ucg_builtin_shm_iface_close(it);
+        return st;
+    }
     *iface_p = it;
     return UCS_OK;
 }
 
-void ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *it)
+/* A member whose peers are all there meets them at a last barrier, so that
+ * none unmaps (member 0: unlinks) while another still sends. Once a peer is
+ * gone, or a barrier already failed, the object is unmapped at once and the
+ * failure returned: a drop-in component reports a peer's failure as a
+ * status, it never kills its host process (the reference ends
+ * ops with a status, builtin_comp_step.inl:332-333). The last member of a
+ * dead creator's object unlinks it, if the name still refers to it. */
+ucs_status_t ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *it)
 {
+    seg_hdr_t *h, ph;
+    ucs_status_t st;
     stash_t *m;
     if (it == NULL) {
-        return;
+        return UCS_ERR_INVALID_PARAM;
     }
+    h = (seg_hdr_t*)it->seg;
     if (it->my == 0) {
         /* closed before the last barrier: a member reopening the name at
          * once waits for the next instance (iface_map) */
-        atomic_store_explicit(&((seg_hdr_t*)it->seg)->stamp, SHM_CLOSED,
-                              memory_order_release);
+        atomic_store_explicit(&h->stamp, SHM_CLOSED, memory_order_release);
     }
-    ucg_builtin_shm_barrier(it);
-    munmap(it->seg, it->seg_bytes);
+    st = ucg_builtin_shm_barrier(it);
     if (it->my == 0) {
         shm_unlink(it->name);
+    } else if (st != UCS_OK && owner_state(h->owner, h->pidns) == 0) {
+        peek_hdr(it->name, &ph);
+        if (ph.instance == h->instance) {
+            shm_unlink(it->name);
+        }
     }
+    munmap(it->seg, it->seg_bytes);
     while ((m = it->unexpected) != NULL) {
         it->unexpected = m->next;
         free(m);
     }
     free(it);
+    return st;
 }
 
 size_t ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *it)
@@ -387,20 +492,42 @@ size_t ucg_builtin_shm_iface_max_short(ucg_builtin_shm_iface_t *it)
     return it ? it->max_short : 0;
 }
 
-void ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
+/* Every member arrives, or: a member's process is gone (probed while
+ * waiting, UCS_ERR_CONNECTION_RESET), or the wait outlives
+ * UCX_BUILTIN_WAIT_TIMEOUT (UCS_ERR_TIMED_OUT). After a failure the shared
+ * count is out of step, so every later barrier of this member fails at once. */
+ucs_status_t ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
 {
-    _Atomic uint64_t *arrive = &((seg_hdr_t*)it->seg)->arrive;
-    uint64_t gen = ++it->barrier_gen;
-    double t0 = now_s(), lim = wait_timeout_s();
+    _Atomic uint64_t *arrive;
+    uint64_t gen;
+    double t0, lim;
+    unsigned spins = 0;
+    if (it == NULL) {
+        return UCS_ERR_INVALID_PARAM;
+    }
+    if (it->broken != UCS_OK) {
+        return it->broken;
+    }
+    arrive = &((seg_hdr_t*)it->seg)->arrive;
+    gen    = ++it->barrier_gen;
+    t0     = now_s();
+    lim    = wait_timeout_s();
     atomic_fetch_add_explicit(arrive, 1, memory_order_acq_rel);
     while (atomic_load_explicit(arrive, memory_order_acquire) < gen * it->members) {
-        if (now_s() - t0 > lim) {
-            fprintf(stderr, "ucg_builtin_shm_barrier(%s): timed out after %.0f s\n",
-                    it->name, lim);
-            abort();
+        if ((++spins & 255) == 0) {
+            if (shm_peer_check(it) >= 0) {
+                return it->broken;
+            }
+            if (now_s() - t0 > lim) {
+                fprintf(stderr, "ucg_builtin_shm_barrier(%s): timed out after %.0f s\n",
+                        it->name, lim);
+                it->broken = UCS_ERR_TIMED_OUT;
+                return it->broken;
+            }
         }
         sched_yield();
     }
+    return UCS_OK;
 }
 
 ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *it, unsigned peer,
@@ -433,7 +560,10 @@ ucs_status_t ucg_builtin_shm_am_short(ucg_builtin_shm_iface_t *it, unsigned peer
     return UCS_OK;
 }
 
-static void spin_lock(_Atomic uint32_t *l)
+/* the holder packs at most one fragment: spin briefly, then yield; a holder
+ * that never lets go (its process is gone, or it outlives the wait timeout)
+ * ends the send with a status */
+static ucs_status_t spin_lock(ucg_builtin_shm_iface_t *it, _Atomic uint32_t *l)
 {
     unsigned spins = 0;
     uint32_t z = 0;
@@ -441,21 +571,25 @@ static void spin_lock(_Atomic uint32_t *l)
     while (!atomic_compare_exchange_weak_explicit(l, &z, 1, memory_order_acquire,
                                                   memory_order_relaxed)) {
         z = 0;
-        /* the holder packs at most one fragment: spin briefly, then yield;
-         * a holder that never lets go (a dead peer) is fatal, not a hang */
         if (++spins < 256) {
             __builtin_ia32_pause();
             continue;
         }
         if (t0 == 0.0) {
             t0 = now_s();
-        } else if ((spins & 1023) == 0 && now_s() - t0 > wait_timeout_s()) {
-            fprintf(stderr, "ucg_builtin_shm: incast cell lock held for over %.0f s\n",
-                    wait_timeout_s());
-            abort();
+        } else if ((spins & 1023) == 0) {
+            if (shm_peer_check(it) >= 0) {
+                return it->broken;
+            }
+            if (now_s() - t0 > wait_timeout_s()) {
+                fprintf(stderr, "ucg_builtin_shm: incast cell lock held for over %.0f s\n",
+                        wait_timeout_s());
+                return UCS_ERR_TIMED_OUT;
+            }
         }
         sched_yield();
     }
+    return UCS_OK;
 }
 
 static void spin_unlock(_Atomic uint32_t *l)
@@ -470,6 +604,7 @@ ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *it, unsigned roo
 {
     unsigned idx;
     incast_cell_t *c;
+    ucs_status_t st;
     int first;
 
     if (root >= it->members || root == it->my || expected == 0 || pack == NULL) {
@@ -485,7 +620,9 @@ ucs_status_t ucg_builtin_shm_am_incast(ucg_builtin_shm_iface_t *it, unsigned roo
     idx = (unsigned)((((header & 0xffffffffull) * 0x9E3779B97F4A7C15ull) >> 40) +
                      (header >> 32) / (it->max_short - 8)) % it->cells;
     c   = incast_cell(it, root, idx);
-    spin_lock(&c->lock);
+    if ((st = spin_lock(it, &c->lock)) != UCS_OK) {
+        return st;
+    }
     /* acquire: the root's reads of a delivered cell precede our writes */
     if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FREE) {
         atomic_store_explicit(&c->state, INCAST_FILLING, memory_order_relaxed);
@@ -532,6 +669,7 @@ ucs_status_t ucg_builtin_shm_am_incast_batched(ucg_builtin_shm_iface_t *it, unsi
 {
     unsigned idx, k;
     incast_cell_t *c;
+    ucs_status_t st;
     char *slot;
 
     if (root >= it->members || root == it->my || expected == 0 || !it->incast_batched ||
@@ -541,7 +679,9 @@ ucs_status_t ucg_builtin_shm_am_incast_batched(ucg_builtin_shm_iface_t *it, unsi
     idx = (unsigned)((((header & 0xffffffffull) * 0x9E3779B97F4A7C15ull) >> 40) +
                      (header >> 32) / (it->max_short - 8)) % it->cells;
     c   = incast_cell(it, root, idx);
-    spin_lock(&c->lock);
+    if ((st = spin_lock(it, &c->lock)) != UCS_OK) {
+        return st;
+    }
     if (atomic_load_explicit(&c->state, memory_order_acquire) == INCAST_FREE) {
         atomic_store_explicit(&c->state, INCAST_FILLING, memory_order_relaxed);
         atomic_store_explicit(&c->count, 0, memory_order_relaxed);

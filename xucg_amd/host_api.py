@@ -80,11 +80,12 @@ HOST_API = {
     # include/ucg_builtin_ops.h
     "ucg_builtin_shm_iface_open": (_int, [ctypes.c_char_p, _u, _u, _sz, _u,
                                           ctypes.POINTER(_vp)]),
-    "ucg_builtin_shm_iface_close": (None, [_vp]),
+    "ucg_builtin_shm_iface_close": (_int, [_vp]),
+    "ucg_builtin_shm_job_token": (_u64, []),
     "ucg_builtin_shm_iface_max_short": (_sz, [_vp]),
     "ucg_builtin_shm_am_short": (_int, [_vp, _u, _u64, _vp, _sz]),
     "ucg_builtin_shm_progress": (_u, [_vp, _vp, _vp]),
-    "ucg_builtin_shm_barrier": (None, [_vp]),
+    "ucg_builtin_shm_barrier": (_int, [_vp]),
     "ucg_builtin_shm_am_incast_batched": (_int, [_vp, _u, _u64, _u, _vp, _sz]),
     "ucg_builtin_shm_am_incast": (_int, [_vp, _u, _u64, _u, _sz, _vp, _vp, _int]),
     "ucg_builtin_lgroup_create": (_int, [_vp, ctypes.c_uint16, _u, _u, _vp,
@@ -111,4 +112,5 @@ HOST_API = {
     "ucg_builtin_lcoll_set_completion": (_int, [_vp, _vp, _vp, _sz, _sz]),
     # include/ucg_builtin_component.h
     "ucg_builtin_component_set_classifier": (None, [OP_FN, DT_FN]),
+    "ucg_builtin_component_last_destroy_status": (_int, []),
 }

@@ -18,12 +18,18 @@ class ShmIface:
         self.handle = h.value
 
     def barrier(self):
-        _lib.host().ucg_builtin_shm_barrier(self.handle)
+        """every member arrives; UcsError when a member's process is gone
+        (UCS_ERR_CONNECTION_RESET) or the wait timed out"""
+        _lib.check(_lib.host().ucg_builtin_shm_barrier(self.handle), "ucg_builtin_shm_barrier")
 
     def close(self):
+        """unmaps the object; returns the last barrier's status (non-zero when
+        a peer failed - the close still completes)"""
+        st = 0
         if getattr(self, "handle", None):
-            _lib.host().ucg_builtin_shm_iface_close(self.handle)
+            st = _lib.host().ucg_builtin_shm_iface_close(self.handle)
             self.handle = None
+        return st
 
 
 # enum ucg_group_member_distance (api/ucg.h:253-264)
