@@ -49,25 +49,36 @@ def lib_sha16(path):
 def pmc_traffic(count):
     """HBM bytes per launch from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json), and where it comes from: the profile, the
-    library it was measured on and whether that is the library loaded now
-    (stale when they differ: the figure is then an older library's). Not a
-    measurement of this run - PMC counters need their own profiler passes."""
+    device code it was measured on and whether that is the code loaded now.
+    The key is the hash of the library's .hip_fatbin section - its kernels'
+    code objects (_lib.code_object_sha16) - so a host-only edit of the
+    library does not stale kernel counters; a summary
+    without it falls back to the whole-library hash. Stale when they differ:
+    the figure is then other kernels'. Not a measurement of this run - PMC
+    counters need their own profiler passes."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     from xucg_amd import _lib
     loaded = lib_sha16(_lib.DEV_LIB)
+    code = _lib.code_object_sha16()
     try:
         with open(path) as f:
             e = json.load(f).get(str(count))
     except (OSError, ValueError):
         e = None
     if e is None:
-        return None, {"profile": None, "stale": True, "lib_sha16_loaded": loaded}
-    measured = e.get("lib_sha16")
+        return None, {"profile": None, "stale": True, "lib_sha16_loaded": loaded,
+                      "code_sha16_loaded": code}
+    if e.get("code_sha16"):
+        key, stale = "code object (.hip_fatbin)", e["code_sha16"] != code
+    else:
+        key, stale = "whole library", e.get("lib_sha16") is None or e.get("lib_sha16") != loaded
     return e.get("hbm_bytes_per_launch"), {
         "profile": "profiles/pmc_traffic.json <- " + str(e.get("source")),
         "kind": "committed rocprofv3 PMC summary (FETCH_SIZE x 2 + WRITE_SIZE), not this run",
-        "lib_sha16_profiled": measured, "lib_sha16_loaded": loaded,
-        "stale": measured is None or measured != loaded}
+        "keyed_by": key,
+        "code_sha16_profiled": e.get("code_sha16"), "code_sha16_loaded": code,
+        "lib_sha16_profiled": e.get("lib_sha16"), "lib_sha16_loaded": loaded,
+        "stale": stale}
 
 
 def cpu_baseline(count, budget_s=10.0):
@@ -1556,6 +1567,9 @@ def main():
             "timing": "20 warm launches, then median of 5 batches of 20 (HIP events)"}
         pair1.free()
         extra["one_shot_8_operands_64mib_fp32"] = one_shot_shape(ctx)
+        # C4's per-GPU shard: 8 operands of 512 MiB
+        extra["one_shot_8_operands_512mib_fp32"] = one_shot_shape(ctx, per_op=512 << 20,
+                                                                  iters=10)
         extra["same_box_reference_kernels"] = same_box_reference(n)
         # H2D/D2H-inclusive rate: host-resident (pinned) buffers, pipelined
         hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)

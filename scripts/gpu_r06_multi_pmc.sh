@@ -1,0 +1,19 @@
+#!/bin/bash
+# r06: PMC attribution of k_reduce_multi at C4's shard size (8 x 512 MiB
+# fp32, one arena) against its read-only and store-without-dependency
+# ceilings: HBM bytes (FETCH_SIZE, WRITE_SIZE), L2 hit/miss,
+# L2-to-fabric read requests, and the vector L1's address-translation misses,
+# one counter group per pass. Usage: scripts/gpu_r06_multi_pmc.sh OUTDIR
+set -u
+OUT=$1; mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -s KILL 60 rocprofv3 -L > $OUT/avail.txt 2>&1 || echo "list rc $?" >> $OUT/steps.log
+for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum" \
+            "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum"; do
+  tag=$(echo $pass | cut -d' ' -f1)
+  echo "pass $tag $(date +%T)" >> $OUT/steps.log
+  timeout -s KILL 150 rocprofv3 --pmc $pass --output-format csv -d $OUT/pmc_$tag -o m \
+      -- tools/tune_multi_pf multi 8 27 1 > $OUT/pmc_$tag.txt 2>&1 || echo "pass $tag rc $?" >> $OUT/steps.log
+done
+python3 scripts/pmc_kernels.py $OUT > $OUT/pmc_by_kernel.txt 2>&1
+echo "done $(date +%T)" >> $OUT/steps.log

@@ -23,6 +23,9 @@ run() { # name, limit, args...
 # the library every pass below runs (bench.py compares it with the one it
 # loads: roofline.traffic_source.stale)
 sha256sum "$ROOT/xucg_amd/lib/libucg_builtin_dev.so" > "$OUT/lib_sha.txt"
+# and its device code alone (.hip_fatbin): what the counters are keyed to
+python3 -c "import sys; sys.path.insert(0, '$ROOT'); from xucg_amd import _lib; print(_lib.code_object_sha16())" \
+    > "$OUT/code_sha.txt"
 
 # the same command as the driver's bench minus the CPU leg and the extra
 # sizes, so every k_reduce launch in the trace is the headline 2^26 combine

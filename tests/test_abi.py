@@ -132,3 +132,33 @@ def test_kernel_resources():
                     uncapped += 1
                     assert vgpr < 168, (name, vgpr)
     assert capped > 0 and uncapped > 0, (capped, uncapped)
+
+
+def test_code_object_hash_keys_kernel_counters(tmp_path, monkeypatch):
+    """PMC traffic is keyed to the device code (.hip_fatbin of
+    libucg_builtin_dev.so), not the whole library: the hash is found, is
+    stable, is not the file's hash, and bench.py's pmc_traffic calls a
+    summary of the same code fresh even when the library hash differs (a
+    host-only edit), and stale when the code differs."""
+    import hashlib
+    import json
+    import sys
+    code = _lib.code_object_sha16()
+    assert code and len(code) == 16 and code == _lib.code_object_sha16()
+    whole = hashlib.sha256(open(_lib.DEV_LIB, "rb").read()).hexdigest()[:16]
+    assert code != whole
+    assert _lib.code_object_sha16(_lib.HOST_LIB) is None     # no device code there
+    sys.path.insert(0, ROOT)
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    entry = {"hbm_bytes_per_launch": 811463936, "source": "x", "lib_sha16": "0" * 16,
+             "code_sha16": code}
+    (prof / "pmc_traffic.json").write_text(json.dumps({"67108864": entry}))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    traffic, src = bench.pmc_traffic(1 << 26)
+    assert traffic == 811463936 and src["stale"] is False
+    assert src["keyed_by"].startswith("code object")
+    entry["code_sha16"] = "f" * 16
+    (prof / "pmc_traffic.json").write_text(json.dumps({"67108864": entry}))
+    assert bench.pmc_traffic(1 << 26)[1]["stale"] is True

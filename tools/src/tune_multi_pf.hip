@@ -61,6 +61,130 @@ k_read_only(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+/* Round 6: U vectors per lane per operand (a wave's tile is 64 x U vectors of
+ * each operand, lane stride 64), XCD tile map over those tiles, PF1 of every
+ * operand D tiles ahead - fewer, longer per-operand bursts per wave */
+template <int N, int U, int D, int PF, int NTS = 1, int ROT = 0>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_u(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    const size_t tile = xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x);
+    const size_t base = tile * (kReduceBlock * U) + threadIdx.x;
+    const u32x4 *op[N];
+    u32x4 val[U][N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        op[m] = reinterpret_cast<const u32x4*>(srcs.p[m]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * kReduceBlock;
+        const size_t ic = i < nvec ? i : nvec - 1;
+        if constexpr (ROT) {
+            /* the operands in an order rotated by the tile: the waves in
+             * flight spread their first loads over all operands */
+            const unsigned r = (unsigned)tile % N;
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                const unsigned mm = (m + r) % N;
+                const u32x4 v = ld16<1>(op[mm] + ic);
+#pragma unroll
+                for (int q = 0; q < N; q++) {
+                    if ((unsigned)q == mm) val[u][q] = v;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                val[u][m] = ld16<1>(op[m] + ic);
+            }
+        }
+    }
+    if constexpr (PF) {
+        const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+        /* lane 63 - u: the first line of row u of the tile D tiles ahead */
+        const size_t want = tile * (kReduceBlock * U) + (size_t)D * kReduceBlock * U +
+                            (size_t)k * kReduceBlock;
+        const size_t at   = (k < (unsigned)U && want < nvec) ? want : nvec - 1;
+        u32x4 pf[N];
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            pf[m] = ld16<0>(op[m] + at);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            asm volatile("" :: "v"(pf[m][0]));
+        }
+    }
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = base + (size_t)u * kReduceBlock;
+        if (i < nvec) {
+            st16<NTS>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val[u], fv));
+        }
+    }
+}
+
+/* Round 6: the XCD tile map, then the superchunks (8 XCD chunks, 8 x 64
+ * tiles) visited in a segmented order - superchunk s of G segments goes to
+ * (s % G) * (nsc / G) + s / G - so the waves in flight cover G regions far
+ * apart in every operand instead of one window (more DRAM banks busy with
+ * 9 streams). A ragged remainder of superchunks keeps the identity. */
+template <int N, int G, int D>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_seg(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    const unsigned ntiles = gridDim.x;
+    unsigned t = xcd_tile<kXcdChunk>(blockIdx.x, ntiles);
+    constexpr unsigned SC = 8 * kXcdChunk;
+    const unsigned nsc = ntiles / SC, full = (nsc / G) * G;
+    if (t / SC < full) {
+        const unsigned sc = t / SC, per = full / G;
+        t = ((sc % G) * per + sc / G) * SC + t % SC;
+    }
+    const size_t i  = (size_t)t * kReduceBlock + threadIdx.x;
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const u32x4 *op[N];
+    u32x4 val[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        op[m]  = reinterpret_cast<const u32x4*>(srcs.p[m]);
+        val[m] = ld16<1>(op[m] + ic);
+    }
+    next_tile_lines<1, N, D>(op, i, nvec);
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val, fv));
+    }
+}
+
+/* the N operands read and dst written with zeros: the traffic of the
+ * combine, no dependency of a store on its loads */
+template <int N>
+__global__ void __launch_bounds__(kReduceBlock)
+k_read_store0(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    const size_t i = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                     threadIdx.x;
+    if (i >= nvec) {
+        return;
+    }
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        acc ^= ld16<1>(reinterpret_cast<const u32x4*>(srcs.p[m]) + i);
+    }
+    st16<1>(reinterpret_cast<u32x4*>(dst) + i, u32x4{0, 0, 0, 0});
+    if (acc[0] == 0x7fc00123u && acc[1] == 0x7fc00321u) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, acc);
+    }
+}
+
 template <int N>
 static void add_multi(std::vector<Variant> &vs)
 {
@@ -85,7 +209,59 @@ static void add_multi(std::vector<Variant> &vs)
     MV("PF1, operand 0 only, 2 tiles ahead", 1, 1, 1, 1, true, 2);
     MV("PF3, all operands, uncapped", 1, 0, 3, N, true);
     MV("PF1, all operands, uncapped", 1, 0, 1, N, true);
+    MV("PF1, all operands, 8 tiles ahead", 1, 1, 1, N, true, 8);
 #undef MV
+    /* round 6: fewer waves per CU at large operands - the product form with
+     * dynamic LDS bounding the workgroups (one wave each) per CU */
+#define LV(label, D, LDS)                                                                 \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_reduce_multi<float, 0, N, 1, 1, 1, N, D>), dim3(tiles(nv)),  \
+                           dim3(kReduceBlock), LDS, q, d, s, 0u, (size_t)0, nv, (size_t)0); \
+    }, true, {}})
+    LV("PF1 all, 2 ahead, LDS cap 8 waves/CU", 2, 20480);
+    LV("PF1 all, 4 ahead, LDS cap 8 waves/CU", 4, 20480);
+    LV("PF1 all, 2 ahead, LDS cap 6 waves/CU", 2, 27306);
+    LV("PF1 all, 4 ahead, LDS cap 6 waves/CU", 4, 27306);
+    LV("PF1 all, 4 ahead, LDS cap 10 waves/CU", 4, 16384);
+#undef LV
+#define UV(label, U, D, PF, ...)                                                         \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_multi_u<N, U, D, PF __VA_OPT__(,) __VA_ARGS__>),            \
+                           dim3((unsigned)((nv + kReduceBlock * U - 1) / (kReduceBlock * U))), \
+                           dim3(kReduceBlock), 0, q, d, s, nv);                           \
+    }, true, {}})
+#define SV(label, G, D)                                                                  \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_multi_seg<N, G, D>), dim3(tiles(nv)), dim3(kReduceBlock), 0, q, \
+                           d, s, nv);                                                     \
+    }, true, {}})
+    SV("segmented superchunks G=4, PF1 2 ahead", 4, 2);
+    SV("segmented superchunks G=16, PF1 2 ahead", 16, 2);
+    SV("segmented superchunks G=64, PF1 2 ahead", 64, 2);
+    SV("segmented superchunks G=16, PF1 4 ahead", 16, 4);
+#undef SV
+    if constexpr (N <= 8) {
+        UV("U1, PF1 4 tiles ahead, temporal store", 1, 4, 1, 0);
+        UV("U1, PF1 4 tiles ahead, rotated operand order", 1, 4, 1, 1, 1);
+        UV("U1, PF1 2 tiles ahead, rotated operand order", 1, 2, 1, 1, 1);
+        UV("U2, no prefetch", 2, 1, 0);
+        UV("U2, PF1 per 64-vector row, 1 tile ahead", 2, 1, 1);
+        UV("U2, PF1 per 64-vector row, 2 tiles ahead", 2, 2, 1);
+        UV("U4, no prefetch", 4, 1, 0);
+        UV("U4, PF1 per row, 1 tile ahead", 4, 1, 1);
+    }
+#undef UV
+    vs.push_back({"product form, in place: dst = operand 0 (unchecked)",
+                  [](float *d, SrcList s, size_t nv, hipStream_t q) {
+        (void)d;
+        hipLaunchKernelGGL((k_reduce_multi<float, 0, N, 1, 1, 1, N, 2>), dim3(tiles(nv)),
+                           dim3(kReduceBlock), 0, q, (float*)const_cast<void*>(s.p[0]), s,
+                           0u, (size_t)0, nv, (size_t)0);
+    }, false, {}});
+    vs.push_back({"ceiling: read N operands, store zeros (no dependency)",
+                  [](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_read_store0<N>), dim3(tiles(nv)), dim3(kReduceBlock), 0, q, d, s, nv);
+    }, false, {}});
     vs.push_back({"ceiling: read the N operands, no store (N*S bytes)",
                   [](float *d, SrcList s, size_t nv, hipStream_t q) {
         hipLaunchKernelGGL((k_read_only<N>), dim3(tiles(nv)), dim3(kReduceBlock), 0, q, d, s, nv);
@@ -119,7 +295,8 @@ static void add_tree(std::vector<Variant> &vs, unsigned n)
 int main(int argc, char **argv)
 {
     if (argc < 3 || (strcmp(argv[1], "multi") && strcmp(argv[1], "tree"))) {
-        fprintf(stderr, "usage: tune_multi_pf multi|tree N [lg=24] [rounds=5] [stagger=0]\n");
+        fprintf(stderr, "usage: tune_multi_pf multi|tree N [lg=24] [rounds=5] [stagger=0] "
+                "[separate=0]\n");
         return 2;
     }
     const bool tree  = !strcmp(argv[1], "tree");
@@ -129,18 +306,28 @@ int main(int argc, char **argv)
     /* operand m starts m * stagger bytes past m * S (a multiple of 256 B):
      * do operands a power of two apart meet in the same HBM channels? */
     const size_t stagger = argc > 5 ? (size_t)atol(argv[5]) & ~(size_t)255 : 0;
+    /* layout 1: every operand and the output in an allocation of its own (as
+     * N ranks' buffers are), instead of one arena S + stagger apart */
+    const int separate   = argc > 6 ? atoi(argv[6]) : 0;
     const int iters  = 10;
     if ((!tree && (N != 2 && N != 4 && N != 8 && N != 16)) || (tree && (N < 2 || N > 16))) {
         fprintf(stderr, "N: multi 2/4/8/16, tree 2..16\n");
         return 2;
     }
     const size_t n = (size_t)1 << lg, nvec = n / 4, S = n * 4;
-    char *arena;
+    char *arena = nullptr, *own[kMaxMulti + 2] = {};
     const size_t slot = S + stagger;
-    CHECK(hipMalloc(&arena, (N + 2) * slot));
+    if (!separate) {
+        CHECK(hipMalloc(&arena, (N + 2) * slot));
+    } else {
+        for (unsigned m = 0; m < N + 2; m++) {
+            CHECK(hipMalloc(&own[m], S));
+        }
+    }
+    auto at = [&](unsigned m) { return separate ? own[m] : arena + m * slot; };
     SrcList srcs;
     for (unsigned m = 0; m < (unsigned)kMaxMulti; m++) {
-        srcs.p[m] = m < N ? arena + m * slot : nullptr;
+        srcs.p[m] = m < N ? at(m) : nullptr;
     }
     {
         std::vector<float> h(n);
@@ -152,8 +339,8 @@ int main(int argc, char **argv)
             CHECK(hipMemcpy(const_cast<void*>(srcs.p[m]), h.data(), S, hipMemcpyHostToDevice));
         }
     }
-    float *out = reinterpret_cast<float*>(arena + N * slot);
-    float *ref = reinterpret_cast<float*>(arena + (N + 1) * slot);
+    float *out = reinterpret_cast<float*>(at(N));
+    float *ref = reinterpret_cast<float*>(at(N + 1));
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
 
@@ -214,12 +401,14 @@ int main(int argc, char **argv)
     }
     const double bytes = (double)(N + 1) * S;
     printf("%s %u, %zu MiB per operand, (N+1)*S = %.0f MiB per launch, %d rounds x %d, "
-           "stagger %zu B\n", tree ? "tree n =" : "multi N =", N, S >> 20, bytes / 1048576.0,
-           rounds, iters, stagger);
+           "%s, stagger %zu B\n", tree ? "tree n =" : "multi N =", N, S >> 20,
+           bytes / 1048576.0, rounds, iters,
+           separate ? "separate allocations" : "one arena", stagger);
     for (auto &v : vs) {
         std::sort(v.ms.begin(), v.ms.end());
         const float med = v.ms[v.ms.size() / 2];
-        const double b = v.checked ? bytes : bytes * N / (N + 1);
+        const double b = v.name.rfind("ceiling: read the N operands, no store", 0) == 0 ?
+                         bytes * N / (N + 1) : bytes;
         printf("%-52s median %8.2f us  min %8.2f  %7.1f GB/s  %5.1f%% of 8 TB/s\n",
                v.name.c_str(), med * 1e3, v.ms.front() * 1e3, b / (med * 1e-3) / 1e9,
                100.0 * b / (med * 1e-3) / 8e12);

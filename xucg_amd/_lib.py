@@ -117,6 +117,38 @@ DEV_API = {
 }
 
 
+def code_object_sha16(path=None):
+    """First 16 hex digits of the sha256 of the library's device code: its
+    .hip_fatbin section (every kernel's gfx950 code object), read from the
+    ELF section table. Host-only edits leave it unchanged, so PMC counters of
+    a kernel stay attributable to the library that ships.
+    None if the file or the section is missing."""
+    import hashlib
+    import struct
+    path = path or DEV_LIB
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+    except OSError:
+        return None
+    if data[:4] != b"\x7fELF" or data[4] != 2:          # 64-bit ELF only
+        return None
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+
+    def sect(i):
+        name, _typ, _flags, _addr, off, size = struct.unpack_from(
+            "<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sect(shstrndx)
+    for i in range(shnum):
+        name, off, size = sect(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    return None
+
+
 def mem_stats():
     """The shim's process-wide memory accounting (ucg_builtin_dev_mem_stats):
     retired address ranges and their cap, the reuse cache, live shareable

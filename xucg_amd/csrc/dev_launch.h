@@ -103,6 +103,17 @@ constexpr int kMultiPrefetchLines = 1;
 constexpr int kFullPrefetchTiles = 2;
 constexpr int kRootPrefetchTiles = 1;
 
+/* Round 6: k_reduce_multi N = 8 with operands of 128 MiB and
+ * more takes its line four tiles ahead (tools/tune_multi_pf, profiles/r06/
+ * multi, A/B in one process on four boxes): at 512 MiB per operand (C4's
+ * shard) 85.3 / 80.7 / 79.9 / 78.6 % of 8 TB/s against 84.3 / 79.4 / 78.6 /
+ * 77.7 % two tiles ahead, at 256 MiB 81.5 / 81.6 / 81.2 against 80.9 / 80.9 /
+ * 80.4 %; at 64 MiB two tiles stay ahead by 0.1-0.6 points, and N = 16 loses
+ * 2 points at four tiles. PMC at 512 MiB: 1.0101 x the algorithmic bytes
+ * against 1.0123 x two tiles ahead (profiles/r06/multi/pmc_by_kernel.txt). */
+constexpr int kLargePrefetchTiles = 4;
+constexpr size_t kLargePrefetchVecs = (size_t)1 << 23;   /* 128 MiB per operand */
+
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
@@ -265,7 +276,12 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             }
             const dim3 g(grid), b(kReduceBlock);
             if constexpr (N >= 8) {
-                if (cap) {
+                if (cap && N == 8 && chunk >= kLargePrefetchVecs) {
+                    /* the PF form, large operands: the line four tiles ahead */
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N,
+                                                       kLargePrefetchTiles>),
+                                       g, b, 0, st, d + off, sl, self, h, chunk, t);
+                } else if (cap) {
                     /* the PF form: XCD map, the next tile's line of every operand */
                     hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N,
                                                        kFullPrefetchTiles>),
