@@ -309,8 +309,8 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
  * import of the same key returns the same mapping, reference counted). */
 ucs_status_t ucg_builtin_dev_ipc_import(ucg_builtin_dev_ctx_t *ctx,
                                         const void *handle, void **dev_ptr);
-/* Drop one import; the last one waits for this process's device work and
- * unmaps. */
+/* Drop one import; the last one waits for the work queued on this shim's
+ * contexts' streams of the device and unmaps. */
 ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx,
                                          void *dev_ptr);
 
@@ -323,8 +323,12 @@ void        *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
 void        *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes);
 /* 1 when ptr lies in a live allocation of ucg_builtin_dev_malloc_shareable */
 int          ucg_builtin_dev_is_shareable(const void *ptr);
-/* Frees either kind (waits for the device first, as hipFree does) and
- * retires the allocation's keys; a pointer of neither is hipFree'd. A freed
+/* Frees either kind and retires the allocation's keys; a pointer of neither
+ * is hipFree'd. It first waits for the work queued so far on the streams of
+ * this shim's contexts on the allocation's device - not for the whole device
+ * (round 6): work the caller queued on a stream of its own that uses the
+ * buffer must be complete before the free, as with any stream-ordered
+ * allocator. A freed
  * ucg_builtin_dev_malloc allocation is kept for the next allocation of its
  * size - one that was ever exported always (and also handed out whole for
  * a request of at least half its size), others up to
@@ -335,7 +339,14 @@ void         ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr);
  * that ended before every peer was done: a timeout, an error, a destroy
  * while running): retires its keys and keeps the memory allocated, never
  * handed out again, for the life of the process (ucg_builtin_dev_mem_stats
- * [6] counts it). */
+ * [6] counts it, and [7] with the other kept memory).
+ *
+ * Kept memory is bounded (round 6): an ucg_builtin_dev_malloc allocation is
+ * kept for the life of the process from its first export on (its address
+ * must never come back from the runtime with other memory behind it), and
+ * ucg_builtin_dev_ipc_export fails with UCS_ERR_EXCEEDS_LIMIT when exporting
+ * one more would take the kept bytes past UCX_BUILTIN_DEV_KEEP_MAX (default
+ * half of the device's memory; a warning is printed once past half of it). */
 void         ucg_builtin_dev_park(ucg_builtin_dev_ctx_t *ctx, void *ptr);
 /* torch.cuda.memory.CUDAPluggableAllocator entry points over
  * ucg_builtin_dev_malloc_shareable / ucg_builtin_dev_free, so that every
@@ -372,7 +383,11 @@ void         ucg_builtin_dev_set_multi_cap(int capped);
  * builtin_comp_step.inl:332-333). */
 unsigned     ucg_builtin_dev_inject_failure(unsigned after);
 
-/* Process-wide memory accounting of the shim (round 5):
+/* Set the cap on kept memory (0 = back to UCX_BUILTIN_DEV_KEEP_MAX / the
+ * default); for tests. */
+void         ucg_builtin_dev_set_keep_max(uint64_t bytes);
+
+/* Process-wide memory accounting of the shim (round 5, extended in round 6):
  *   [0] bytes of GPU virtual address ranges retired: a shareable allocation
  *       or an import, once unmapped, leaves its reservation behind so that no
  *       address is ever mapped to other physical memory;
@@ -381,11 +396,19 @@ unsigned     ucg_builtin_dev_inject_failure(unsigned after);
  *       with UCS_ERR_EXCEEDS_LIMIT (UCX_BUILTIN_DEV_VA_RETIRED_MAX, default
  *       64 TiB, or ucg_builtin_dev_set_va_retired_max);
  *   [3] bytes held by the reuse cache of freed ucg_builtin_dev_malloc
- *       allocations (UCX_BUILTIN_DEV_CACHE_BYTES);
+ *       allocations (its never-exported part bounded by
+ *       UCX_BUILTIN_DEV_CACHE_BYTES);
  *   [4] bytes of live shareable allocations of this process;
  *   [5] bytes of live shareable imports (peers' allocations mapped here);
- *   [6] bytes parked (ucg_builtin_dev_park). */
-#define UCG_BUILTIN_DEV_NMEMSTATS 7
+ *   [6] bytes parked (ucg_builtin_dev_park);
+ *   [7] bytes kept for the life of the process: ever-exported
+ *       ucg_builtin_dev_malloc allocations, live or cached, and parked ones;
+ *   [8] the cap on [7] (UCX_BUILTIN_DEV_KEEP_MAX);
+ *   [9] of [3], the ever-exported bytes;
+ *   [10] slack: bytes of live allocations beyond their request (a cached
+ *       ever-exported allocation handed out for a request of at least half
+ *       its size). */
+#define UCG_BUILTIN_DEV_NMEMSTATS 11
 void         ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS]);
 /* Set the cap on retired address ranges for this process (0 = back to
  * UCX_BUILTIN_DEV_VA_RETIRED_MAX / the default); for tests. */

@@ -585,6 +585,115 @@ print("OK")
 
 
 @pytest.mark.gpu
+def test_kept_memory_is_capped_and_slack_counted():
+    """memory the shim keeps for the life of the process
+    (ever-exported allocations, live or cached, and parked ones) is bounded by
+    UCX_BUILTIN_DEV_KEEP_MAX: the export that would cross it fails with
+    UCS_ERR_EXCEEDS_LIMIT naming the knob, a warning is printed once past
+    half, and nothing is counted for the refused export. A cached exported
+    allocation handed out for a smaller request counts its extra bytes as
+    slack until it is freed. Only never-exported bytes count against
+    UCX_BUILTIN_DEV_CACHE_BYTES."""
+    import subprocess
+    import sys
+    code = r"""
+import xucg_amd
+from xucg_amd import _lib
+ctx = xucg_amd.DevContext(device=0)
+n = 6 << 20
+s0 = _lib.mem_stats()
+assert s0["keep_max"] == 24 << 20 and s0["kept_bytes"] == 0, s0
+bufs = [ctx.alloc(n) for _ in range(4)]
+for b in bufs[:3]:
+    ctx.ipc_export(b.ptr)
+s = _lib.mem_stats()
+assert s["kept_bytes"] == 3 * n, s
+try:
+    ctx.ipc_export(bufs[3].ptr)
+    raise SystemExit("export past the keep cap succeeded")
+except xucg_amd.UcsError as e:
+    assert e.status == -21 and "UCX_BUILTIN_DEV_KEEP_MAX" in str(e), str(e)
+assert _lib.mem_stats()["kept_bytes"] == 3 * n
+bufs[3].free()                          # never exported: bounded cache (0 here): freed
+s = _lib.mem_stats()
+assert s["plain_cache_bytes"] == 0 and s["plain_cache_exported_bytes"] == 0, s
+bufs[0].free()                          # exported: kept whatever the cache bound
+s = _lib.mem_stats()
+assert s["plain_cache_exported_bytes"] == n and s["plain_cache_bytes"] == n, s
+assert s["kept_bytes"] == 3 * n, s
+small = ctx.alloc(4 << 20)              # takes the kept 6 MiB one: 2 MiB slack
+s = _lib.mem_stats()
+assert s["slack_bytes"] == 2 << 20 and s["plain_cache_exported_bytes"] == 0, s
+small.free()
+assert _lib.mem_stats()["slack_bytes"] == 0
+for b in bufs[1:3]:
+    b.free()
+assert _lib.mem_stats()["kept_bytes"] == 3 * n
+ctx.close()
+print("OK")
+"""
+    env = dict(os.environ, UCX_BUILTIN_DEV_KEEP_MAX="24m", UCX_BUILTIN_DEV_CACHE_BYTES="0")
+    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+    assert p.stderr.count("past half of UCX_BUILTIN_DEV_KEEP_MAX") == 1, p.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_free_waits_for_the_shims_streams_not_the_device():
+    """ucg_builtin_dev_free (plain and shareable memory)
+    waits for the work queued on the streams of the shim's contexts, not for
+    the whole device: with a 1.5-second kernel running on an unrelated torch
+    stream, a free returns in milliseconds (round 5's hipDeviceSynchronize
+    waited for it). Work of the shim's own stream on the buffer is still
+    waited for: a combine queued just before the free has completed, with
+    the right result, before the same memory is handed out again."""
+    import subprocess
+    import sys
+    code = r"""
+import time
+import numpy as np
+import torch
+import xucg_amd
+torch.cuda.init()
+ctx = xucg_amd.DevContext(device=0)
+n = 6 << 20
+side = torch.cuda.Stream()
+with torch.cuda.stream(side):
+    torch.cuda._sleep(int(1.5 * 2.4e9))          # ~1.5 s of one wave spinning
+t_long = time.perf_counter()
+out = {}
+for kind in ("plain", "shareable"):
+    b = ctx.alloc(n, shareable=(kind == "shareable"))
+    t0 = time.perf_counter()
+    b.free()
+    out[kind] = time.perf_counter() - t0
+assert not side.query(), "the side kernel ended before the frees were timed"
+# the shim's own work on a buffer is waited for before its memory is reused
+cnt = 1 << 20
+a, d = ctx.alloc(cnt * 4), ctx.alloc(cnt * 4)
+ctx.fill("float32", "exact", 7, a.ptr, cnt)
+ctx.fill("float32", "exact", 8, d.ptr, cnt)
+want = a.download(np.float32, cnt).astype(np.float64) + d.download(np.float32, cnt)
+pd = d.ptr
+assert ctx.reduce("sum", "float32", d.ptr, a.ptr, cnt) == 0
+d.free()
+e = ctx.alloc(cnt * 4)
+assert e.ptr == pd                                # the same memory, reused
+got = e.download(np.float32, cnt)
+assert np.array_equal(got.astype(np.float64), want)
+side.synchronize()
+print("FREE_S", out, "side kernel", round(time.perf_counter() - t_long, 3))
+assert max(out.values()) < 0.5, out
+ctx.close()
+print("OK")
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
+                       timeout=180, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
+
+
+@pytest.mark.gpu
 def test_plain_allocations_reused_whole(dev_ctx):
     """Round 4: a freed ucg_builtin_dev_malloc allocation is
     kept and handed out again, whole, for the next allocation of its size - the

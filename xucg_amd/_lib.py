@@ -56,10 +56,11 @@ class DevCtxParams(ctypes.Structure):
 
 ZCOPY_NEVER = (1 << 64) - 1   # UCG_BUILTIN_DEV_ZCOPY_NEVER
 NCOUNTERS = 6                 # UCG_BUILTIN_DEV_NCOUNTERS
-NMEMSTATS = 7                 # UCG_BUILTIN_DEV_NMEMSTATS
+NMEMSTATS = 11                # UCG_BUILTIN_DEV_NMEMSTATS
 MEMSTATS = ["va_retired_bytes", "va_retired_ranges", "va_retired_max",
             "plain_cache_bytes", "shareable_live_bytes", "shareable_import_bytes",
-            "parked_bytes"]
+            "parked_bytes",
+            "kept_bytes", "keep_max", "plain_cache_exported_bytes", "slack_bytes"]
 COMPLETION = {"signal": 1, "sync": 2}   # UCG_BUILTIN_DEV_COMPLETION_*
 
 
@@ -112,6 +113,7 @@ DEV_API = {
                                              ctypes.POINTER(ctypes.c_double)]),
     "ucg_builtin_dev_counters": (None, [_vp, ctypes.POINTER(_u64)]),
     "ucg_builtin_dev_mem_stats": (None, [ctypes.POINTER(_u64)]),
+    "ucg_builtin_dev_set_keep_max": (None, [_u64]),
     "ucg_builtin_dev_set_va_retired_max": (None, [_u64]),
     "ucg_builtin_dev_inject_failure": (_u, [_u]),
 }

@@ -16,6 +16,7 @@
 #include <cstring>
 #include <ctime>
 #include <mutex>
+#include <vector>
 #include <string>
 #include <map>
 #include <unordered_map>
@@ -211,6 +212,52 @@ struct ucg_builtin_dev_ctx {
 
     std::atomic<uint64_t> counters[UCG_BUILTIN_DEV_NCOUNTERS];
 };
+
+/* the live contexts (dev_streams_drain) */
+static std::mutex g_ctx_mu;
+static std::vector<ucg_builtin_dev_ctx_t*> g_ctx_list;
+
+hipError_t dev_streams_drain(int device)
+{
+    hipError_t first = hipSetDevice(device);
+    std::vector<hipEvent_t> evs;
+    {
+        /* recorded under the lock: a context being destroyed has left the
+         * list before its streams go */
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        for (ucg_builtin_dev_ctx_t *c : g_ctx_list) {
+            if (c->device != device) {
+                continue;
+            }
+            for (hipStream_t s : {c->stream, c->stream_d2h}) {
+                if (s == nullptr) {
+                    continue;
+                }
+                hipEvent_t ev;
+                hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+                if (e == hipSuccess) {
+                    e = hipEventRecord(ev, s);
+                    if (e == hipSuccess) {
+                        evs.push_back(ev);
+                    } else {
+                        (void)hipEventDestroy(ev);
+                    }
+                }
+                if (e != hipSuccess && first == hipSuccess) {
+                    first = e;
+                }
+            }
+        }
+    }
+    for (hipEvent_t ev : evs) {
+        const hipError_t e = hipEventSynchronize(ev);
+        if (e != hipSuccess && first == hipSuccess) {
+            first = e;
+        }
+        (void)hipEventDestroy(ev);
+    }
+    return first;
+}
 
 static ucs_status_t set_device(ucg_builtin_dev_ctx_t *ctx)
 {
@@ -517,6 +564,10 @@ ucs_status_t ucg_builtin_dev_ctx_create(const ucg_builtin_dev_ctx_params_t *para
         ucg_builtin_dev_ctx_destroy(ctx);
         return st;
     }
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        g_ctx_list.push_back(ctx);
+    }
     *ctx_p = ctx;
     return UCS_OK;
 }
@@ -525,6 +576,15 @@ void ucg_builtin_dev_ctx_destroy(ucg_builtin_dev_ctx_t *ctx)
 {
     if (ctx == nullptr) {
         return;
+    }
+    {
+        std::lock_guard<std::mutex> g(g_ctx_mu);
+        for (auto it = g_ctx_list.begin(); it != g_ctx_list.end(); ++it) {
+            if (*it == ctx) {
+                g_ctx_list.erase(it);
+                break;
+            }
+        }
     }
     if (ctx->device >= 0) {
         (void)hipSetDevice(ctx->device);

@@ -73,6 +73,7 @@ struct own_alloc {
     hipMemGenericAllocationHandle_t handle;   /* KIND_VMM */
     uint64_t key_id;                          /* 0: never exported */
     bool     exported;                        /* KIND_PLAIN: ever exported */
+    size_t   want;                            /* bytes the caller asked for (rounded) */
 };
 
 std::mutex g_mu;                                      /* guards everything here */
@@ -91,8 +92,56 @@ std::unordered_map<void*, own_alloc> g_allocs;        /* base -> allocation */
  * memory, and peers' fresh hipIpc imports of it can map another process's
  * memory). The value is (pointer, ever exported). */
 std::multimap<std::pair<int, size_t>, std::pair<void*, bool>> g_plain_cache;  /* (device, bytes) */
-size_t g_plain_cached = 0;
+size_t g_plain_cached = 0;       /* never-exported bytes in the cache (bounded) */
+size_t g_cached_exported = 0;    /* ever-exported bytes in the cache (kept) */
 uint64_t g_parked = 0;           /* bytes parked by ucg_builtin_dev_park */
+/* Memory this process keeps for its life (round 6): every
+ * ever-exported plain allocation, live or cached, plus what is parked.
+ * Bounded by UCX_BUILTIN_DEV_KEEP_MAX (default half the device's memory):
+ * exporting an allocation that would take it past the cap fails with
+ * UCS_ERR_EXCEEDS_LIMIT, named; half-way there a warning is printed once. */
+uint64_t g_kept = 0;
+std::atomic<uint64_t> g_keep_max_set{0};          /* 0: the environment's / default */
+bool g_keep_warned = false;
+/* bytes of live allocations beyond their request: an ever-exported
+ * allocation handed out whole for a request of at least half its size */
+uint64_t g_slack = 0;
+
+uint64_t parse_bytes(const char *e, uint64_t dflt)
+{
+    if (e == nullptr || *e == 0) {
+        return dflt;
+    }
+    char *end = nullptr;
+    double v = strtod(e, &end);
+    if (end && (*end == 'k' || *end == 'K')) v *= 1024.0;
+    else if (end && (*end == 'm' || *end == 'M')) v *= 1048576.0;
+    else if (end && (*end == 'g' || *end == 'G')) v *= 1073741824.0;
+    else if (end && (*end == 't' || *end == 'T')) v *= 1099511627776.0;
+    return v > 0 ? (uint64_t)v : dflt;
+}
+
+/* the cap on g_kept: ucg_builtin_dev_set_keep_max, else
+ * UCX_BUILTIN_DEV_KEEP_MAX, else half of `device`'s memory */
+uint64_t keep_max(int device)
+{
+    const uint64_t set = g_keep_max_set.load(std::memory_order_relaxed);
+    if (set) {
+        return set;
+    }
+    static std::atomic<uint64_t> lim{0};
+    uint64_t v = lim.load(std::memory_order_relaxed);
+    if (v == 0) {
+        size_t total = 0;
+        if (hipDeviceTotalMem(&total, device) != hipSuccess || total == 0) {
+            (void)hipGetLastError();
+            total = (size_t)256 << 30;
+        }
+        v = parse_bytes(getenv("UCX_BUILTIN_DEV_KEEP_MAX"), (uint64_t)total / 2);
+        lim.store(v, std::memory_order_relaxed);
+    }
+    return v;
+}
 
 size_t plain_cache_limit()
 {
@@ -111,17 +160,20 @@ size_t plain_cache_limit()
     return lim;
 }
 
-/* give the never-exported cached allocations back to the runtime (hipMalloc
- * ran out of memory: the cache may hold what it needs, at other sizes);
- * returns how many. Caller does not hold g_mu. */
-size_t plain_cache_drain()
+/* give `device`'s never-exported cached allocations back to the runtime
+ * (hipMalloc ran out of memory there: the cache may hold what it needs, at
+ * other sizes); returns how many. The calling thread's current device is
+ * `device` on return (a retried hipMalloc on the device drained
+ * last could land on the wrong GPU). Caller does not hold g_mu. */
+size_t plain_cache_drain(int device)
 {
-    std::vector<std::pair<int, void*>> out;
+    std::vector<void*> out;
     {
         std::lock_guard<std::mutex> g(g_mu);
-        for (auto it = g_plain_cache.begin(); it != g_plain_cache.end();) {
+        for (auto it = g_plain_cache.lower_bound({device, 0});
+             it != g_plain_cache.end() && it->first.first == device;) {
             if (!it->second.second) {
-                out.emplace_back(it->first.first, it->second.first);
+                out.push_back(it->second.first);
                 g_plain_cached -= it->first.second;
                 it = g_plain_cache.erase(it);
             } else {
@@ -129,9 +181,9 @@ size_t plain_cache_drain()
             }
         }
     }
-    for (auto &d : out) {
-        (void)hipSetDevice(d.first);
-        (void)hipFree(d.second);
+    (void)hipSetDevice(device);
+    for (void *p : out) {
+        (void)hipFree(p);
     }
     return out.size();
 }
@@ -536,6 +588,7 @@ hipError_t import_fd(hipMemGenericAllocationHandle_t *h, int fd, int device)
 
 /* map an imported VMM allocation (fd) at a new reservation of this process */
 ucs_status_t va_room(size_t bytes, const char *what);
+void va_unclaim(size_t bytes);
 
 ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
 {
@@ -544,9 +597,14 @@ ucs_status_t map_vmm(int fd, size_t size, int device, import_rec *m)
         return room;
     }
     hipMemGenericAllocationHandle_t h;
-    HIP_TRY(import_fd(&h, fd, device));
+    hipError_t e = import_fd(&h, fd, device);
+    if (e != hipSuccess) {
+        va_unclaim(size);
+        return hip_status(e, "import_fd(&h, fd, device)");
+    }
     void *va = nullptr;
-    hipError_t e = hipMemAddressReserve(&va, size, kGran, nullptr, 0);
+    e = hipMemAddressReserve(&va, size, kGran, nullptr, 0);
+    va_unclaim(size);
     if (e == hipSuccess) {
         e = hipMemMap(va, size, 0, h, 0);
         if (e == hipSuccess) {
@@ -594,36 +652,42 @@ uint64_t va_retired_max()
     if (set) {
         return set;
     }
-    static const uint64_t lim = [] {
-        const char *e = getenv("UCX_BUILTIN_DEV_VA_RETIRED_MAX");
-        const uint64_t dflt = (uint64_t)64 << 40;
-        if (e == nullptr || *e == 0) {
-            return dflt;
-        }
-        char *end = nullptr;
-        double v = strtod(e, &end);
-        if (end && (*end == 'k' || *end == 'K')) v *= 1024.0;
-        else if (end && (*end == 'm' || *end == 'M')) v *= 1048576.0;
-        else if (end && (*end == 'g' || *end == 'G')) v *= 1073741824.0;
-        else if (end && (*end == 't' || *end == 'T')) v *= 1099511627776.0;
-        return v > 0 ? (uint64_t)v : dflt;
-    }();
+    static const uint64_t lim = parse_bytes(getenv("UCX_BUILTIN_DEV_VA_RETIRED_MAX"),
+                                            (uint64_t)64 << 40);
     return lim;
 }
 
 /* may a new range of `bytes` be reserved? (UCS_ERR_EXCEEDS_LIMIT, named, if
- * the retired ranges are past the cap) */
+ * the retired ranges are past the cap). The check and the claim are one
+ * compare-and-swap on the retired count plus the claims in flight (ADVICE
+ * r05: threads checking at once could together pass the cap); the caller
+ * gives the claim back with va_unclaim once its range is mapped or failed -
+ * the range counts again when it is retired. */
+std::atomic<uint64_t> g_va_claimed{0};
+
 ucs_status_t va_room(size_t bytes, const char *what)
 {
-    const uint64_t r = g_va_retired.load(std::memory_order_relaxed), cap = va_retired_max();
-    if (r + bytes > cap) {
-        char b[200];
-        snprintf(b, sizeof(b), "retired address ranges %llu B + %zu B past "
-                 "UCX_BUILTIN_DEV_VA_RETIRED_MAX %llu B (never-remapped ranges, DESIGN.md 6)",
-                 (unsigned long long)r, bytes, (unsigned long long)cap);
-        return set_error(UCS_ERR_EXCEEDS_LIMIT, what, b);
+    const uint64_t cap = va_retired_max();
+    uint64_t c = g_va_claimed.load(std::memory_order_relaxed);
+    for (;;) {
+        const uint64_t r = g_va_retired.load(std::memory_order_relaxed);
+        if (r + c + bytes > cap) {
+            char b[220];
+            snprintf(b, sizeof(b), "retired address ranges %llu B + %llu B in flight + %zu B "
+                     "past UCX_BUILTIN_DEV_VA_RETIRED_MAX %llu B (never-remapped ranges, "
+                     "DESIGN.md 6)", (unsigned long long)r, (unsigned long long)c, bytes,
+                     (unsigned long long)cap);
+            return set_error(UCS_ERR_EXCEEDS_LIMIT, what, b);
+        }
+        if (g_va_claimed.compare_exchange_weak(c, c + bytes)) {
+            return UCS_OK;
+        }
     }
-    return UCS_OK;
+}
+
+void va_unclaim(size_t bytes)
+{
+    g_va_claimed.fetch_sub(bytes);
 }
 
 void va_retire(size_t bytes)
@@ -737,6 +801,19 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
             e.fd = fd;
         } else {
             e.kind = KIND_PLAIN;
+            if (own != g_allocs.end() && !own->second.exported) {
+                /* exported once, this allocation is kept for the life of the
+                 * process (ucg_builtin_dev_free): within the keep cap */
+                const uint64_t cap = keep_max(own->second.device);
+                if (g_kept + own->second.bytes > cap) {
+                    char b[220];
+                    snprintf(b, sizeof(b), "memory kept for exported allocations %llu B + "
+                             "%zu B past UCX_BUILTIN_DEV_KEEP_MAX %llu B (exported memory "
+                             "is never given back, DESIGN.md 7)", (unsigned long long)g_kept,
+                             own->second.bytes, (unsigned long long)cap);
+                    return set_error(UCS_ERR_EXCEEDS_LIMIT, "ipc_export", b);
+                }
+            }
             HIP_TRY(hipPointerGetAttribute(&e.buffer_id, HIP_POINTER_ATTRIBUTE_BUFFER_ID,
                                            base));
             HIP_TRY(hipIpcGetMemHandle(&e.ih, (void*)base));
@@ -746,6 +823,16 @@ ucs_status_t ucg_builtin_dev_ipc_export(ucg_builtin_dev_ctx_t *ctx,
         g_export_of[(void*)base] = id;
         if (own != g_allocs.end()) {
             own->second.key_id = id;
+            if (own->second.kind == KIND_PLAIN && !own->second.exported) {
+                g_kept += own->second.bytes;
+                const uint64_t cap = keep_max(own->second.device);
+                if (g_kept > cap / 2 && !g_keep_warned) {
+                    g_keep_warned = true;
+                    fprintf(stderr, "xucg: %llu B kept for exported allocations (never "
+                            "given back), past half of UCX_BUILTIN_DEV_KEEP_MAX (%llu B)\n",
+                            (unsigned long long)g_kept, (unsigned long long)cap);
+                }
+            }
             own->second.exported = true;
         }
     }
@@ -904,10 +991,10 @@ ucs_status_t ucg_builtin_dev_ipc_release(ucg_builtin_dev_ctx_t *ctx, void *dev_p
         }
     }
     if (last && m.kind) {
-        /* nothing of this process may still read it (outside the lock: the
-         * key server keeps answering peers meanwhile) */
-        (void)hipSetDevice(dev_ctx_device(ctx));
-        const hipError_t e = hipDeviceSynchronize();
+        /* nothing of this shim may still read it: the streams of this
+         * device's contexts are drained, not the whole device (outside the
+         * lock: the key server keeps answering peers meanwhile) */
+        const hipError_t e = dev_streams_drain(dev_ctx_device(ctx));
         unmap_import(m);
         std::lock_guard<std::mutex> g(g_mu);
         note_event('C', dev_ptr, m.base, m.size, (int)e);
@@ -938,14 +1025,15 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
             p = c->second.first;
             const bool was_exported = c->second.second;
             g_plain_cache.erase(c);
-            g_plain_cached -= bytes;
-            g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0, was_exported};
+            (was_exported ? g_cached_exported : g_plain_cached) -= bytes;
+            g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0, was_exported, bytes};
             note_event('R', p, p, bytes, 0);
             return p;
         }
         /* else the smallest ever-exported one up to twice the size: those are
          * never given back, so a caller whose sizes vary reuses them rather
-         * than adding one per size */
+         * than adding one per size; what it holds beyond the request is
+         * counted as slack (ucg_builtin_dev_mem_stats [10]) */
         for (auto x = g_plain_cache.lower_bound({device, bytes});
              x != g_plain_cache.end() && x->first.first == device &&
              x->first.second <= 2 * bytes; ++x) {
@@ -953,16 +1041,18 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
                 const size_t have = x->first.second;
                 p = x->second.first;
                 g_plain_cache.erase(x);
-                g_plain_cached -= have;
-                g_allocs[p] = own_alloc{KIND_PLAIN, device, have, {}, 0, true};
+                g_cached_exported -= have;
+                g_slack += have - bytes;
+                g_allocs[p] = own_alloc{KIND_PLAIN, device, have, {}, 0, true, bytes};
                 note_event('R', p, p, have, 0);
                 return p;
             }
         }
     }
     hipError_t e = hipMalloc(&p, bytes);
-    if (e == hipErrorOutOfMemory && plain_cache_drain() > 0) {
-        /* the reuse cache held memory of other sizes: given back, once more */
+    if (e == hipErrorOutOfMemory && plain_cache_drain(device) > 0) {
+        /* the reuse cache held memory of other sizes: given back, once more,
+         * on this allocation's device (the drain leaves it current) */
         (void)hipGetLastError();
         e = hipMalloc(&p, bytes);
     }
@@ -971,7 +1061,7 @@ void *ucg_builtin_dev_malloc(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         return nullptr;
     }
     std::lock_guard<std::mutex> g(g_mu);
-    g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0, false};
+    g_allocs[p] = own_alloc{KIND_PLAIN, device, bytes, {}, 0, false, bytes};
     note_event('M', p, p, bytes, 0);
     return p;
 }
@@ -1005,11 +1095,13 @@ void *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
     hipMemGenericAllocationHandle_t h;
     hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
     if (e != hipSuccess) {
+        va_unclaim(bytes);
         hip_status(e, "hipMemCreate");
         return nullptr;
     }
     void *va = nullptr;
     e = hipMemAddressReserve(&va, bytes, kGran, nullptr, 0);
+    va_unclaim(bytes);
     if (e == hipSuccess) {
         e = hipMemMap(va, bytes, 0, h, 0);
         if (e == hipSuccess) {
@@ -1029,7 +1121,7 @@ void *ucg_builtin_dev_malloc_shareable(ucg_builtin_dev_ctx_t *ctx, size_t bytes)
         return nullptr;
     }
     std::lock_guard<std::mutex> g(g_mu);
-    g_allocs[va] = own_alloc{KIND_VMM, device, bytes, h, 0, false};
+    g_allocs[va] = own_alloc{KIND_VMM, device, bytes, h, 0, false, bytes};
     note_event('V', va, va, bytes, 0);
     return va;
 }
@@ -1060,6 +1152,7 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         if (it != g_allocs.end()) {
             a = it->second;
             own = true;
+            g_slack -= a.bytes - a.want;
             g_allocs.erase(it);
         }
         /* retire its key: a peer's import of it is refused from now on */
@@ -1078,10 +1171,10 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
     }
     hipError_t e;
     if (own && a.kind == KIND_VMM) {
-        /* as hipFree does: nothing queued may still use it. Peers that mapped
+        /* nothing this shim queued may still use it (its contexts' streams
+         * on the device, not the whole device: round 6). Peers that mapped
          * it keep the physical memory until they release their mapping. */
-        (void)hipSetDevice(a.device);
-        e = hipDeviceSynchronize();
+        e = dev_streams_drain(a.device);
         (void)hipMemUnmap(ptr, a.bytes);
         (void)hipMemRelease(a.handle);
         va_retire(a.bytes);                /* the range is never reused */
@@ -1095,16 +1188,20 @@ void ucg_builtin_dev_free(ucg_builtin_dev_ctx_t *ctx, void *ptr)
          * buffer in 3,608 of 6,974 checks (12 processes,
          * tools/va_reuse_probe ipc). Reused here it is the same
          * memory. A buffer that a peer may still be reading is parked
-         * instead (ucg_builtin_dev_park: ADVICE r04). */
-        (void)hipSetDevice(a.device);
-        e = hipDeviceSynchronize();
+         * instead (ucg_builtin_dev_park: ADVICE r04). Before it is handed
+         * out again, the work this shim queued on it has drained: the
+         * streams of the device's contexts (round 6: no device-wide sync,
+         * which waited for RCCL's and the application's streams too). Only
+         * never-exported bytes count against UCX_BUILTIN_DEV_CACHE_BYTES
+         * (ADVICE r05); exported ones are bounded by the keep cap. */
+        e = dev_streams_drain(a.device);
         bool kept = false;
         {
             std::lock_guard<std::mutex> g(g_mu);
             if (a.exported || g_plain_cached + a.bytes <= plain_cache_limit()) {
                 g_plain_cache.emplace(std::make_pair(a.device, a.bytes),
                                       std::make_pair(ptr, a.exported));
-                g_plain_cached += a.bytes;
+                (a.exported ? g_cached_exported : g_plain_cached) += a.bytes;
                 kept = true;
             }
         }
@@ -1131,6 +1228,10 @@ void ucg_builtin_dev_park(ucg_builtin_dev_ctx_t *ctx, void *ptr)
         return;                                  /* not this shim's: left alone */
     }
     g_parked += it->second.bytes;
+    if (!(it->second.kind == KIND_PLAIN && it->second.exported)) {
+        g_kept += it->second.bytes;              /* exported ones count already */
+    }
+    g_slack -= it->second.bytes - it->second.want;
     g_allocs.erase(it);                          /* never freed, never handed out */
     auto ex = g_export_of.find(ptr);
     if (ex != g_export_of.end()) {               /* its keys retire all the same */
@@ -1164,16 +1265,29 @@ void ucg_builtin_dev_mem_stats(uint64_t out[UCG_BUILTIN_DEV_NMEMSTATS])
     out[0] = g_va_retired.load();
     out[1] = g_va_retired_ranges.load();
     out[2] = va_retired_max();
-    out[3] = g_plain_cached;
+    int device = 0;
+    (void)hipGetDevice(&device);
+    out[3] = g_plain_cached + g_cached_exported;
     out[4] = live_vmm;
     out[5] = live_imp;
     out[6] = g_parked;
+    out[7] = g_kept;
+    out[8] = keep_max(device);
+    out[9] = g_cached_exported;
+    out[10] = g_slack;
 }
 
 void ucg_builtin_dev_set_va_retired_max(uint64_t bytes)
 {
     g_va_retired_max_set.store(bytes);
     g_va_warned.store(false);
+}
+
+void ucg_builtin_dev_set_keep_max(uint64_t bytes)
+{
+    g_keep_max_set.store(bytes);
+    std::lock_guard<std::mutex> g(g_mu);
+    g_keep_warned = false;
 }
 
 /* torch.cuda.memory.CUDAPluggableAllocator entry points: every tensor of a
@@ -1191,7 +1305,7 @@ void ucg_builtin_dev_torch_free(void *ptr, size_t bytes, int device, void *strea
     (void)bytes;
     (void)stream;
     (void)hipSetDevice(device);
-    ucg_builtin_dev_free(nullptr, ptr);        /* synchronises the device first */
+    ucg_builtin_dev_free(nullptr, ptr);        /* drains the shim's streams first */
 }
 
 /* Diagnostics for a buffer found corrupted (tests/_worker_topo.py): what the
