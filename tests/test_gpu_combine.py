@@ -602,7 +602,7 @@ from xucg_amd import _lib
 ctx = xucg_amd.DevContext(device=0)
 n = 6 << 20
 s0 = _lib.mem_stats()
-assert s0["keep_max"] == 24 << 20 and s0["kept_bytes"] == 0, s0
+assert s0["keep_max"] == 20 << 20 and s0["kept_bytes"] == 0, s0
 bufs = [ctx.alloc(n) for _ in range(4)]
 for b in bufs[:3]:
     ctx.ipc_export(b.ptr)
@@ -632,7 +632,7 @@ assert _lib.mem_stats()["kept_bytes"] == 3 * n
 ctx.close()
 print("OK")
 """
-    env = dict(os.environ, UCX_BUILTIN_DEV_KEEP_MAX="24m", UCX_BUILTIN_DEV_CACHE_BYTES="0")
+    env = dict(os.environ, UCX_BUILTIN_DEV_KEEP_MAX="20m", UCX_BUILTIN_DEV_CACHE_BYTES="0")
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=120, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert p.returncode == 0 and "OK" in p.stdout, p.stdout[-2000:] + p.stderr[-2000:]
