@@ -295,6 +295,11 @@ static int ipc_mode(int argc, char **argv)
         barrier(dir, "b" + std::to_string(i), rank, np);          /* every peer read it */
         if (!hold) {
             for (void *m : maps) CHECK(hipIpcCloseMemHandle(m));
+            /* round 6: every peer closed its imports of this buffer before it
+             * is freed (without this barrier an exporter could free, and
+             * allocate the address again, under a slower peer's open import:
+             * the hold mode's hazard) */
+            barrier(dir, "c" + std::to_string(i), rank, np);
         }
         CHECK(hipDeviceSynchronize());
         CHECK(hipFree(p));
