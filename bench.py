@@ -1078,6 +1078,114 @@ def one_shot_shape(ctx, nsrc=8, per_op=64 << 20, iters=20):
                     f"{iters} back-to-back launches"}
 
 
+def collective_alloc_plan(world=8):
+    """One rank's device allocations in collective_phases, phase by phase, in
+    order: (phase, "alloc"|"free", name, bytes). Mirrors the
+    code above at full size (COLL_SCALE 1) on the default hipIpc path, where
+    every exported tensor stays allocated until the phases end (keep()).
+    RCCL's own buffers and the engine's pinned host ring are not in it."""
+    from xucg_amd import group as G
+    n4 = 1 << 30                               # C4: 4 GiB fp32
+    shard = n4 // world
+    lo1, hi1 = G.shard_bounds(1 << 28, 4, world, 0)
+    n5 = 1 << 26                               # C5: 512 MiB fp64
+    slot = G.stage_slot_bytes(n4, 4, world)
+    slot5 = G.stage_slot_bytes(n5, 8, world)
+    win = 18 * SAMPLE_ELEMS                    # sampled windows per shard (PlanWindows)
+    return [
+        ("c4", "alloc", "x (send)", n4 * 4),
+        ("c4", "alloc", "rs_out (RCCL reduce-scatter output)", shard * 4),
+        ("c4", "alloc", "ag_out (RCCL all-gather output, one-shot recv)", n4 * 4),
+        ("c4 one-shot", "alloc", "PlanWindows index + gathered windows", 2 * world * win * 8),
+        ("c4 one-shot", "alloc", "mine (one-shot shard)", shard * 4),
+        ("c4 one-shot", "alloc", "mine1 (1 GiB leg shard)", (hi1 - lo1) * 4),
+        ("c4 one-shot", "alloc", "rccl1 (1 GiB leg RCCL shard)", (1 << 28) // world * 4),
+        ("c4 one-shot", "free", "mine1 (1 GiB leg shard)", (hi1 - lo1) * 4),
+        ("c4 one-shot", "free", "rccl1 (1 GiB leg RCCL shard)", (1 << 28) // world * 4),
+        ("c4 one-shot", "alloc", "ag_rccl (RCCL all-gather copy)", n4 * 4),
+        ("c4 push", "alloc", "stage (push reduce-scatter)", world * slot),
+        ("c4 push", "free", "ag_rccl (RCCL all-gather copy)", n4 * 4),
+        ("c4 rounded", "alloc", "|x| (tolerance input)", n4 * 4),
+        ("c4 rounded", "alloc", "|x| reduce-scatter", shard * 4),
+        ("c4 rounded", "free", "|x| (tolerance input)", n4 * 4),
+        ("c4 rounded", "alloc", "tolerance", shard * 4),
+        ("c4 rounded", "alloc", "error", shard * 4),
+        ("c4 rounded", "free", "|x| reduce-scatter", shard * 4),
+        ("c4 rounded", "free", "tolerance", shard * 4),
+        ("c4 rounded", "free", "error", shard * 4),
+        ("c4 end", "free", "rs_out (RCCL reduce-scatter output)", shard * 4),
+        # x, mine, ag_out and stage stay: exported (keep) until the phases end
+        ("c5", "alloc", "init (send)", n5 * 8),
+        ("c5", "alloc", "acc (recv)", n5 * 8),
+        ("c5", "alloc", "tmp (exchange)", n5 * 8),
+        ("c5", "alloc", "stage5 (push allreduce)", world * slot5),
+        ("c5 end", "free", "tmp (exchange)", n5 * 8),
+        # init, acc and stage5 stay: exported (keep)
+        ("c5 engine", "alloc", "init (engine send)", n5 * 8),
+        ("c5 engine", "alloc", "acc (engine recv)", n5 * 8),
+        ("c5 engine", "alloc", "group arena (UCX_BUILTIN_DEV_ARENA_BYTES)", 32 << 20),
+        ("c5 engine", "alloc", "registered send buffer (lgroup_mem_alloc)", n5 * 8),
+        ("c5 engine", "alloc", "op buffer 0 (remote-key steps)", n5 * 8),
+        ("c5 engine", "alloc", "op buffer 1 (remote-key steps)", n5 * 8),
+    ]
+
+
+def collective_dry_alloc(world=8):
+    """--collective-dry-alloc: one rank's C4 and C5 buffers at full size, in
+    the order collective_plan lists them, on this process's one GPU - torch
+    tensors from torch's caching allocator as in the collective child, the
+    engine's from the shim (ucg_builtin_dev_malloc) - and the device memory in
+    use after every step (hipMemGetInfo). No collective runs. Prints one JSON
+    line with the peak."""
+    import torch
+    import xucg_amd
+    torch.cuda.set_device(0)
+    ctx = xucg_amd.DevContext(device=0)
+    free0, total = torch.cuda.mem_get_info()
+    live, steps, peak = {}, [], 0
+    for phase, act, name, nbytes in collective_alloc_plan(world):
+        key = (phase.split()[0], name)
+        if act == "alloc":
+            if phase == "c5 engine":
+                live[key] = ctx.alloc(nbytes)
+            else:
+                live[key] = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+                live[key].fill_(1)                      # touched, as the phases do
+        else:
+            k = next(k for k in live if k[1] == name)
+            b = live.pop(k)
+            if hasattr(b, "free"):
+                b.free()
+            del b
+        torch.cuda.synchronize()
+        used = free0 - torch.cuda.mem_get_info()[0]
+        peak = max(peak, used)
+        steps.append({"phase": phase, act: name, "bytes": nbytes,
+                      "device_used_gib": round(used / GIB, 3)})
+    res = {"collective_dry_alloc": True, "world": world, "rank_modelled": 0,
+           "device_total_gib": round(total / GIB, 1),
+           "peak_device_used_gib": round(peak / GIB, 3),
+           "planned_peak_gib": round(plan_peak(collective_alloc_plan(world)) / GIB, 3),
+           "torch_max_reserved_gib": round(torch.cuda.max_memory_reserved() / GIB, 3),
+           "steps": steps,
+           "not_included": "RCCL's own buffers; the engine's pinned host staging ring"}
+    for b in live.values():
+        if hasattr(b, "free"):
+            b.free()
+    live.clear()
+    ctx.close()
+    print(json.dumps(res), flush=True)
+
+
+def plan_peak(plan):
+    """the largest sum of live bytes over the plan's steps"""
+    cur = peak = 0
+    for _, act, _, nbytes in plan:
+        cur += nbytes if act == "alloc" else -nbytes
+        peak = max(peak, cur)
+    return peak
+
+
 def run_collective_children(dist, rank, world, timeout_s=300):
     """Run collective_phases in one child process per rank (a fresh process
     group on a new port), so that a fault in the multi-GPU phases - the IPC
@@ -1411,6 +1519,9 @@ def plumbing(world, rank):
 def main():
     if "--collective-child" in sys.argv:
         collective_child()
+        return
+    if "--collective-dry-alloc" in sys.argv:
+        collective_dry_alloc(8)
         return
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1,

@@ -74,3 +74,23 @@ def test_collective_child_result_keeps_finished_phases(tmp_path):
     # no file at all
     res = bench.read_child_result(str(tmp_path / "none.json"), 1, "boom")
     assert res["error"] == "collective child exited with 1" and res["tail"] == "boom"
+
+
+def test_collective_alloc_plan_is_balanced_and_fits():
+    """the per-rank allocation plan of the 8-GPU collective
+    phases (bench.collective_alloc_plan, also what --collective-dry-alloc
+    allocates): every free matches an earlier allocation of the same size,
+    nothing goes negative, and the peak stays far below one MI355X's 288 GB."""
+    import bench
+    plan = bench.collective_alloc_plan(8)
+    live = {}
+    for phase, act, name, nbytes in plan:
+        assert act in ("alloc", "free") and nbytes > 0
+        if act == "alloc":
+            assert name not in live, name
+            live[name] = nbytes
+        else:
+            assert live.pop(name) == nbytes, name
+    peak = bench.plan_peak(plan)
+    assert 16 << 30 < peak < 20 << 30, peak          # C4's rounded leg: 17.5 GiB
+    assert bench.plan_peak(bench.collective_alloc_plan(2)) > peak   # bigger shards
