@@ -205,6 +205,54 @@ k_gather_ms(char *dst, SrcList srcs, size_t row_bytes, size_t nvec)
     }
 }
 
+/* round 6: k_gather_ms<0, 0> with two consecutive tiles of its row per wave:
+ * tile 0's lane 63 takes tile 1's first vector from tile 1's own load
+ * (readfirstlane), so one extra vector per 2 KiB */
+template <int U>
+__global__ void __launch_bounds__(kReduceBlock)
+k_gather_msu(char *dst, SrcList srcs, size_t row_bytes, size_t nvec)
+{
+    const unsigned r = blockIdx.x % 8, t = blockIdx.x / 8;
+    const char *p = static_cast<const char*>(srcs.p[r]);
+    const unsigned rs = (unsigned)((uintptr_t)p & 15);
+    const u32x4 *a4 = reinterpret_cast<const u32x4*>(p - rs);
+    const size_t i0 = (size_t)t * U * kReduceBlock + threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    u32x4 lo[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const size_t i = i0 + (size_t)u * kReduceBlock;
+        lo[u] = ld16<1>(a4 + (i < nvec ? i : nvec));
+    }
+    const size_t il = i0 + (size_t)(U - 1) * kReduceBlock;
+    u32x4 ex = {0, 0, 0, 0};
+    if (rs) {
+        ex = ld16<0>(a4 + (last_lane && il < nvec ? il + 1 : nvec));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 *o = reinterpret_cast<u32x4*>(dst + (size_t)r * row_bytes);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        u32x4 v = lo[u];
+        if (rs) {
+            u32x4 hi, nx;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                hi[k] = from_next_lane(lo[u][k]);
+                nx[k] = __builtin_amdgcn_readfirstlane(lo[u + 1 < U ? u + 1 : u][k]);
+            }
+            if (last_lane) {
+                hi = u + 1 < U ? nx : ex;
+            }
+            v = funnel16(lo[u], hi, rs);
+        }
+        const size_t i = i0 + (size_t)u * kReduceBlock;
+        if (i < nvec) {
+            st16<1>(o + i, v);
+        }
+    }
+}
+
 /* In-phase operands (round 4, r04o): the realigning kernel fed in-phase
  * operands read 84.8 % where k_reduce_multi read 79.9 % (capped, N = 8). What
  * of the realigning kernel does it? All forms capped, on the XCD tile map:
@@ -422,6 +470,39 @@ int main(int argc, char **argv)
         {"gather 8 rows, XCD map, ex temporal", 2.0 * 8 * nm * 4, [&] {
              hipLaunchKernelGGL((k_gather_ms<0, 1>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
                                 (char*)dst, sl, nm * 4, nvm); }, {}},
+        /* round 6: the same layout with every source in
+         * phase (the aligned path), and the out-of-phase rows with fewer
+         * waves per CU (dynamic LDS bounding the one-wave workgroups) */
+        {"gather 8 rows in phase, round-robin", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<0, 0>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl_al, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, ex temporal, 16 waves/CU", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<0, 0>), dim3(8 * gm), dim3(kReduceBlock), 10240, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, ex temporal, 12 waves/CU", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<0, 0>), dim3(8 * gm), dim3(kReduceBlock), 13653, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, ex temporal, 8 waves/CU", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_ms<0, 0>), dim3(8 * gm), dim3(kReduceBlock), 20480, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, 2 tiles per wave", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_msu<2>), dim3(8 * ((gm + 1) / 2)), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, 4 tiles per wave", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_msu<4>), dim3(8 * ((gm + 3) / 4)), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
+        {"gather 8 rows in phase, 1 tile per wave (msu)", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_msu<1>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl_al, nm * 4, nvm); }, {}},
+        {"gather 8 rows in phase, 2 tiles per wave", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_msu<2>), dim3(8 * ((gm + 1) / 2)), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl_al, nm * 4, nvm); }, {}},
+        {"gather 8 rows in phase, 4 tiles per wave", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_msu<4>), dim3(8 * ((gm + 3) / 4)), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl_al, nm * 4, nvm); }, {}},
+        {"gather 8 rows, round-robin, 1 tile per wave (msu)", 2.0 * 8 * nm * 4, [&] {
+             hipLaunchKernelGGL((k_gather_msu<1>), dim3(8 * gm), dim3(kReduceBlock), 0, 0,
+                                (char*)dst, sl, nm * 4, nvm); }, {}},
         {"N=8 aligned capped, XCD map", 9.0 * nm * 4, [&] {
              hipLaunchKernelGGL((k_reduce_multi<float, 0, 8, 1, 1>), dim3(gm), dim3(kReduceBlock),
                                 0, 0, dst, sl_al, 0u, (size_t)0, nvm, (size_t)0); }, {}},
@@ -581,6 +662,14 @@ int main(int argc, char **argv)
         {"N=8 shift (product)", "N=8 plain misaligned (capped)"},
         {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, ex temporal"},
         {"gather 8 rows, round-robin, ex nt", "gather 8 rows, XCD map, ex temporal"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, ex temporal, 16 waves/CU"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, ex temporal, 8 waves/CU"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, 2 tiles per wave"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, 4 tiles per wave"},
+        {"gather 8 rows, round-robin, ex nt", "gather 8 rows, round-robin, 1 tile per wave (msu)"},
+        {"gather 8 rows in phase, round-robin", "gather 8 rows in phase, 2 tiles per wave"},
+        {"gather 8 rows in phase, round-robin", "gather 8 rows in phase, 4 tiles per wave"},
+        {"gather 8 rows in phase, round-robin", "gather 8 rows in phase, 1 tile per wave (msu)"},
         {"N=8 aligned (capped)", "N=8 aligned capped, XCD map"},
         {"N=4 aligned capped", "N=4 aligned capped, XCD map"},
         {"tree n=8 aligned capped", "tree n=8 aligned capped, XCD map"},

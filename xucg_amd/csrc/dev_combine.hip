@@ -811,9 +811,17 @@ __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbyt
     const char *sp     = src + head;
     const unsigned rs  = (unsigned)((uintptr_t)sp & 15);
     u32x4 *o4          = reinterpret_cast<u32x4*>(out + head);
-    if (rs == 0) {
+    /* Round 6: clamped, unmasked loads held ahead of
+     * everything else by a sched barrier, as k_reduce_shift does - without
+     * it the compiler let the shuffles of the realigning path wait on the
+     * loads one at a time. tools/tune_misalign, profiles/r06/gather: 8 rows
+     * of 64 MiB out of phase 83.8 % of 8 TB/s against 79.7 % for the form
+     * without the barrier, in phase 84.4 against 79.8 % (same box). */
+    if (rs == 0 && nvec != 0) {
+        const u32x4 v = ld16<1>(reinterpret_cast<const u32x4*>(sp) + (i < nvec ? i : nvec - 1));
+        __builtin_amdgcn_sched_barrier(0);
         if (i < nvec) {
-            st16<1>(o4 + i, ld16<1>(reinterpret_cast<const u32x4*>(sp) + i));
+            st16<1>(o4 + i, v);
         }
     } else if (nvec != 0) {
         /* every lane of the wave takes part in the shuffle: clamped loads */
@@ -821,6 +829,7 @@ __device__ __forceinline__ void copy_row(char *out, const char *src, size_t nbyt
         const bool last_lane = threadIdx.x == kReduceBlock - 1;
         const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
         const u32x4 ex = ld16<0>(a4 + (last_lane && i < nvec ? i + 1 : nvec));  /* temporal */
+        __builtin_amdgcn_sched_barrier(0);
         u32x4 hi;
 #pragma unroll
         for (int k = 0; k < 4; k++) {
