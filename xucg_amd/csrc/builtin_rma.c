@@ -179,13 +179,38 @@ static size_t shm_key_bytes(const void *key)
  * made on the group's first device-buffer (remote-key) buffer, not with the
  * group: a group that never runs a device-buffer step costs no HBM (ADVICE
  * r04). arena_bytes holds the size still to make while arena is NULL. */
+/* the arena, once; a failure is reported once and leaves the group without
+ * one (a member whose arena failed silently took per-buffer
+ * allocations while its peers did not) */
+static void rma_arena_make(ucg_builtin_lgroup_t *g)
+{
+    if (g->arena != NULL || g->arena_bytes == 0) {
+        return;
+    }
+    g->arena = ucg_builtin_combine_dev_alloc(g->cmb, g->arena_bytes);
+    if (g->arena == NULL) {
+        fprintf(stderr, "ucg_builtin: group %u member %u: the %zu B device arena "
+                "(UCX_BUILTIN_DEV_POOL_BYTES) could not be allocated (%s); its "
+                "registered buffers are allocated one by one\n", (unsigned)g->group_id,
+                g->my, g->arena_bytes, ucg_builtin_dev_last_error());
+        g->arena_bytes = 0;
+    }
+}
+
+/* UCX_BUILTIN_DEV_POOL_EAGER=y makes the arena with the group, so that the
+ * first device-buffer operation pays no allocation (a hipMalloc of 32 MiB
+ * may synchronise the device) */
 UCG_INTERNAL void rma_group_init(ucg_builtin_lgroup_t *g)
 {
     const size_t bytes = parse_memunits(getenv("UCX_BUILTIN_DEV_POOL_BYTES"),
                                         (size_t)32 << 20);
+    const char *eager = getenv("UCX_BUILTIN_DEV_POOL_EAGER");
     g->arena = NULL;
     g->arena_used = 0;
     g->arena_bytes = (bytes && ucg_builtin_combine_has_device(g->cmb)) ? bytes : 0;
+    if (eager && (eager[0] == 'y' || eager[0] == '1')) {
+        rma_arena_make(g);
+    }
 }
 
 /* registered buffers come in size classes - at least 64 KiB, eight per
@@ -238,14 +263,8 @@ static int rma_pool_get(ucg_builtin_lgroup_t *g, size_t bytes, int kind)
         p->ptr = shm_seg_alloc(bytes, p->key);
         return p->ptr ? (int)g->npool++ : -1;
     }
-    if (g->arena == NULL && g->arena_bytes) {
-        /* the group's first device buffer: make the arena now (once; a
-         * failure leaves the group without one) */
-        g->arena = ucg_builtin_combine_dev_alloc(g->cmb, g->arena_bytes);
-        if (g->arena == NULL) {
-            g->arena_bytes = 0;
-        }
-    }
+    /* the group's first device buffer: make the arena now */
+    rma_arena_make(g);
     if (g->arena && g->arena_used + bytes <= g->arena_bytes) {
         /* from the group's arena: one allocation per group, not one per
          * buffer, and the peers map the whole arena once (one key, offsets) */
