@@ -796,7 +796,7 @@ def test_group_destroy_parks_buffers_a_peer_may_read(monkeypatch):
     and destroying the group parks it (ucg_builtin_dev_park) rather than
     returning it to the reuse cache, where the next allocation of its size
     would change it under the reader."""
-    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "30")
+    monkeypatch.setenv("UCX_BUILTIN_WAIT_TIMEOUT", "8")
     codes, outs = launch("_worker_park.py", 2, args=(shm_name(),), timeout=150)
     assert codes == [0, 0], "\n".join(outs)
     assert "parked" in outs[0], outs[0]
