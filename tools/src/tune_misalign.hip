@@ -367,6 +367,35 @@ k2p(float *dst, const float *src, size_t nvec)
     }
 }
 
+/* Round 6: the headline's PF form (XCD map, the first PF lines of the next
+ * tile's src temporally) with its loads and store issued as buffer
+ * instructions carrying explicit cache-policy bits (1 sc0, 2 nt, 16 sc1;
+ * the product uses nt for both). Offsets 32-bit: < 4 GiB per operand. */
+template <int LAUX, int SAUX, int PF = 3>
+__global__ void __launch_bounds__(kReduceBlock)
+k2buf(float *dst, const float *src, size_t nvec)
+{
+    const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                      threadIdx.x;
+    const size_t ic = i < nvec ? i : nvec - 1;
+    __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(src), 0,
+                                                                  0xffffffffu, 0x00020000);
+    __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0xffffffffu,
+                                                                  0x00020000);
+    const u32x4 a = __builtin_amdgcn_raw_buffer_load_b128(rs, (unsigned)(ic * 16), 0, LAUX);
+    const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rd, (unsigned)(ic * 16), 0, LAUX);
+    const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+    const size_t want = (i - threadIdx.x + kReduceBlock) + (size_t)k * 8;
+    const u32x4 pf = ld16<0>(reinterpret_cast<const u32x4*>(src) +
+                             (k < (unsigned)PF && want < nvec ? want : nvec - 1));
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" :: "v"(pf[0]));
+    if (i < nvec) {
+        __builtin_amdgcn_raw_buffer_store_b128(vapply<float, 0>(a, b), rd, (unsigned)(i * 16), 0,
+                                               SAUX);
+    }
+}
+
 struct Case {
     std::string name;
     double bytes;
@@ -543,6 +572,30 @@ int main(int argc, char **argv)
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 3>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
                                 nvec, (size_t)0); }, {}},
+        {"2-op buffer ld/st nt (= product)", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<2, 2>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld nt, st sc0 sc1 nt", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<2, 19>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld nt, st nt sc1", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<2, 18>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld nt, st sc0 nt", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<2, 3>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld sc1 nt, st nt", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<18, 2>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld sc0 sc1 nt, st nt", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<19, 2>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld default, st nt", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<0, 2>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
+        {"2-op buffer ld nt, st sc1", 3.0 * n * 4, [&] {
+             hipLaunchKernelGGL((k2buf<2, 16>), dim3(g2), dim3(kReduceBlock), 0, 0, dst,
+                                (const float*)src, nvec); }, {}},
         {"2-op k_reduce PF=4 (next tile's first 4 lines)", 3.0 * n * 4, [&] {
              hipLaunchKernelGGL((k_reduce<float, 0, 1, 1, kReduceBlock, 1, 4>), dim3(g2),
                                 dim3(kReduceBlock), 0, 0, dst, (const float*)src, (size_t)0,
@@ -702,6 +755,9 @@ int main(int argc, char **argv)
         {"1 GiB: round 3's k_reduce", "1 GiB: PF 3 lines"},
         {"2-op aligned k_reduce (round 3's form)", "2-op k_reduce PF=4 (next tile's first 4 lines)"},
         {"2-op aligned k_reduce (round 3's form)", "2-op product: k_reduce PF=3 (next tile's first 3 lines)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op buffer ld/st nt (= product)"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op buffer ld nt, st sc0 sc1 nt"},
+        {"2-op aligned k_reduce (round 3's form)", "2-op buffer ld sc0 sc1 nt, st nt"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 8 lines (the whole next tile)"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 4 lines of src and of dst"},
         {"2-op aligned k_reduce (round 3's form)", "PF: 2 lines, chunk 128"},

@@ -162,6 +162,41 @@ k_multi_seg(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+/* Round 6: the product's PF form (every operand's line D tiles ahead) with
+ * the store - and, BUFLD, the operand loads - issued as buffer instructions
+ * carrying explicit cache-policy bits (AUX: 1 sc0, 2 nt, 16 sc1; the
+ * product's non-temporal store is nt). Offsets are 32-bit: operands < 4 GiB. */
+template <int N, int D, int SAUX, int BUFLD = 0, int LAUX = 2>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_buf(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                      threadIdx.x;
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const u32x4 *op[N];
+    u32x4 val[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        op[m] = reinterpret_cast<const u32x4*>(srcs.p[m]);
+        if constexpr (BUFLD) {
+            __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<void*>(srcs.p[m]), 0, 0xffffffffu, 0x00020000);
+            val[m] = __builtin_amdgcn_raw_buffer_load_b128(r, (unsigned)(ic * 16), 0, LAUX);
+        } else {
+            val[m] = ld16<1>(op[m] + ic);
+        }
+    }
+    next_tile_lines<1, N, D>(op, i, nvec);
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    if (i < nvec) {
+        __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0xffffffffu,
+                                                                      0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(rd_tree<N>(val, fv), rd, (unsigned)(i * 16), 0,
+                                               SAUX);
+    }
+}
+
 /* the N operands read and dst written with zeros: the traffic of the
  * combine, no dependency of a store on its loads */
 template <int N>
@@ -230,6 +265,25 @@ static void add_multi(std::vector<Variant> &vs)
                            dim3((unsigned)((nv + kReduceBlock * U - 1) / (kReduceBlock * U))), \
                            dim3(kReduceBlock), 0, q, d, s, nv);                           \
     }, true, {}})
+#define BV(label, D, SAUX, ...)                                                          \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_multi_buf<N, D, SAUX __VA_OPT__(,) __VA_ARGS__>), dim3(tiles(nv)), \
+                           dim3(kReduceBlock), 0, q, d, s, nv);                           \
+    }, true, {}})
+    BV("buffer store nt (= product), 2 ahead", 2, 2);
+    BV("buffer store nt, 4 ahead", 4, 2);
+    BV("buffer store default policy, 4 ahead", 4, 0);
+    BV("buffer store sc0, 4 ahead", 4, 1);
+    BV("buffer store sc1, 4 ahead", 4, 16);
+    BV("buffer store sc0 sc1, 4 ahead", 4, 17);
+    BV("buffer store nt sc1, 4 ahead", 4, 18);
+    BV("buffer store sc0 sc1 nt, 4 ahead", 4, 19);
+    BV("buffer store sc0 nt, 4 ahead", 4, 3);
+    BV("buffer loads nt + store nt, 4 ahead", 4, 2, 1, 2);
+    BV("buffer loads sc1 nt + store nt, 4 ahead", 4, 2, 1, 18);
+    BV("buffer loads sc0 sc1 nt + store nt, 4 ahead", 4, 2, 1, 19);
+    BV("buffer loads default + store nt, 4 ahead", 4, 2, 1, 0);
+#undef BV
 #define SV(label, G, D)                                                                  \
     vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
         hipLaunchKernelGGL((k_multi_seg<N, G, D>), dim3(tiles(nv)), dim3(kReduceBlock), 0, q, \
