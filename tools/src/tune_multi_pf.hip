@@ -101,6 +101,9 @@ k_multi_u(float *dst, SrcList srcs, size_t nvec)
             }
         }
     }
+    if constexpr (!PF) {
+        __builtin_amdgcn_sched_barrier(0);     /* every load issued before any use */
+    }
     if constexpr (PF) {
         const unsigned k  = kReduceBlock - 1 - threadIdx.x;
         /* lane 63 - u: the first line of row u of the tile D tiles ahead */
@@ -294,6 +297,7 @@ static void add_multi(std::vector<Variant> &vs)
     SV("segmented superchunks G=64, PF1 2 ahead", 64, 2);
     SV("segmented superchunks G=16, PF1 4 ahead", 16, 4);
 #undef SV
+    UV("U1, clamped loads + sched barrier, no prefetch", 1, 1, 0);
     if constexpr (N <= 8) {
         UV("U1, PF1 4 tiles ahead, temporal store", 1, 4, 1, 0);
         UV("U1, PF1 4 tiles ahead, rotated operand order", 1, 4, 1, 1, 1);
@@ -344,6 +348,24 @@ static void add_tree(std::vector<Variant> &vs, unsigned n)
     TV("PF1, all operands, 4 tiles ahead", 1, C, 1, NMAX, 4);
     TV("PF1, operand 0 only, 2 tiles ahead", 1, C, 1, 1, 2);
 #undef TV
+}
+
+/* Round 6: the tree fan-in built for exactly n operands (NMAX = n: no
+ * reloads of the root's operand past n), in the product's n == NMAX form
+ * (every operand's line two tiles ahead) and the root-only form */
+template <int NX>
+static void add_tree_exact(std::vector<Variant> &vs, unsigned n)
+{
+    vs.push_back({"exact NMAX = n, PF1 all operands, 2 tiles ahead",
+                  [n](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_reduce_tree<float, 0, NX, 1, 1, 1, NX, 2>), dim3(tiles(nv)),
+                           dim3(kReduceBlock), 0, q, d, s, n, (size_t)0, nv, (size_t)0);
+    }, true, {}});
+    vs.push_back({"exact NMAX = n, PF1 root only, 1 tile ahead",
+                  [n](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_reduce_tree<float, 0, NX, 1, 1, 1, 1, 1>), dim3(tiles(nv)),
+                           dim3(kReduceBlock), 0, q, d, s, n, (size_t)0, nv, (size_t)0);
+    }, true, {}});
 }
 
 int main(int argc, char **argv)
@@ -412,6 +434,14 @@ int main(int argc, char **argv)
         add_tree<8>(vs, N);
     } else {
         add_tree<16>(vs, N);
+    }
+    if (tree) {
+        switch (N) {
+        case 3:  add_tree_exact<3>(vs, N); break;
+        case 6:  add_tree_exact<6>(vs, N); break;
+        case 12: add_tree_exact<12>(vs, N); break;
+        default: break;
+        }
     }
 
     vs[0].run(ref, srcs, nvec, st);

@@ -109,7 +109,9 @@ constexpr int kRootPrefetchTiles = 1;
  * shard) 85.3 / 80.7 / 79.9 / 78.6 % of 8 TB/s against 84.3 / 79.4 / 78.6 /
  * 77.7 % two tiles ahead, at 256 MiB 81.5 / 81.6 / 81.2 against 80.9 / 80.9 /
  * 80.4 %; at 64 MiB two tiles stay ahead by 0.1-0.6 points, and N = 16 loses
- * 2 points at four tiles. PMC at 512 MiB: 1.0101 x the algorithmic bytes
+ * 2 points at four tiles. (N = 16 without any prefetch read 77.2 against
+ * 75.2 % at 256 MiB but 77.5 against 81.1 % at 512 MiB, r06m / r06n: not
+ * taken.) PMC at 512 MiB: 1.0101 x the algorithmic bytes
  * against 1.0123 x two tiles ahead (profiles/r06/multi/pmc_by_kernel.txt). */
 constexpr int kLargePrefetchTiles = 4;
 constexpr size_t kLargePrefetchVecs = (size_t)1 << 23;   /* 128 MiB per operand */
@@ -448,6 +450,42 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
     } while (done < nvec);
 }
 
+/* Round 6 (tree n = 12 at 82.4 %): in-phase operands of a
+ * fan-in that does not fill its NMAX bucket (5-7, 9-15 children and root)
+ * take a kernel built for exactly n operands - no reloads of the root's
+ * operand past n - in the n == NMAX form (capped, every operand's line two
+ * tiles ahead). tools/tune_multi_pf, profiles/r06/multi/r06m_pf_tree_*:
+ * n = 12 84.2 % of 8 TB/s at 64 MiB per operand against 82.0 % (the bucket's
+ * root-only form) and 76.8 against 75.4 % at 256 MiB; n = 6 84.5 against
+ * 82.1 %. Prefetching every operand in the NMAX = 16 kernel instead lost
+ * (76.7 %: its registers pass the occupancy cap). n <= 4 keeps the
+ * uncapped bucket (an exact capped n = 3 read 69 %). */
+template <typename T, int OP, int NX>
+void launch_tree_exact(T *d, const SrcList &srcs, size_t head, size_t nvec, size_t tail,
+                       hipStream_t st)
+{
+    constexpr size_t V = 16 / sizeof(T);
+    size_t done = 0;
+    do {
+        const size_t chunk = nvec - done < kMaxVecPerLaunch ? nvec - done : kMaxVecPerLaunch;
+        const bool first = (done == 0), last = (done + chunk == nvec);
+        const size_t off = first ? 0 : head + done * V;
+        SrcList sl;
+        for (int m = 0; m < kMaxMulti; m++) {
+            sl.p[m] = srcs.p[m] ? static_cast<const T*>(srcs.p[m]) + off : nullptr;
+        }
+        unsigned grid = grid_for(chunk, kReduceBlock, 0x7fffffff);
+        if (first && div_up(head, kReduceBlock) > grid) {
+            grid = (unsigned)div_up(head, kReduceBlock);
+        }
+        hipLaunchKernelGGL((k_reduce_tree<T, OP, NX, 1, 1, kMultiPrefetchLines, NX,
+                                          kFullPrefetchTiles>),
+                           dim3(grid), dim3(kReduceBlock), 0, st, d + off, sl, (unsigned)NX,
+                           first ? head : 0, chunk, last ? tail : 0);
+        done += chunk;
+    } while (done < nvec);
+}
+
 template <int DT, int OP>
 hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
                        hipStream_t st)
@@ -466,6 +504,21 @@ hipError_t launch_tree(void *dst, const SrcList &srcs, unsigned n, size_t count,
         xm = xm || straddles_lines(static_cast<const T*>(srcs.p[m]) + head);
     }
     const size_t rem = count - head, nvec = rem / V, tail = rem % V;
+    if (aligned && n > 4 && n != 8 && n != 16 && (!uncapped_ab<T, OP>() || multi_capped())) {
+        switch (n) {
+        case 5:  launch_tree_exact<T, OP, 5>(d, srcs, head, nvec, tail, st); break;
+        case 6:  launch_tree_exact<T, OP, 6>(d, srcs, head, nvec, tail, st); break;
+        case 7:  launch_tree_exact<T, OP, 7>(d, srcs, head, nvec, tail, st); break;
+        case 9:  launch_tree_exact<T, OP, 9>(d, srcs, head, nvec, tail, st); break;
+        case 10: launch_tree_exact<T, OP, 10>(d, srcs, head, nvec, tail, st); break;
+        case 11: launch_tree_exact<T, OP, 11>(d, srcs, head, nvec, tail, st); break;
+        case 12: launch_tree_exact<T, OP, 12>(d, srcs, head, nvec, tail, st); break;
+        case 13: launch_tree_exact<T, OP, 13>(d, srcs, head, nvec, tail, st); break;
+        case 14: launch_tree_exact<T, OP, 14>(d, srcs, head, nvec, tail, st); break;
+        default: launch_tree_exact<T, OP, 15>(d, srcs, head, nvec, tail, st); break;
+        }
+        return hipGetLastError();
+    }
     if (n <= 4) {
         launch_tree_n<T, OP, 4>(d, srcs, n, head, nvec, tail, aligned, xm, st);
     } else if (n <= 8) {
