@@ -283,6 +283,34 @@ def test_component_and_timer_host_sanitizers(monkeypatch, exe, world, args):
         assert "Sanitizer" not in out and "runtime error" not in out, out
 
 
+@pytest.mark.parametrize("exe,world,args", [("async_resend", 2, None),
+                                             ("async_resend", 4, ("round",)),
+                                             ("component_test", 4, ("host",))])
+def test_engine_thread_sanitizer(monkeypatch, exe, world, args):
+    """SURVEY 5, race detection: the host engine rebuilt with ThreadSanitizer
+    (tests/c/Makefile, target tsan), with the resend timer's thread working
+    against the owner thread (async_resend: the timer sends and combines
+    while the owner sleeps, then both wait; the plan component with its
+    timer running). Any data race report fails the rank. Round 6 found one:
+    ucg_builtin_lgroup_stats read the counters the timer thread writes
+    without the group's lock."""
+    import fcntl
+    import subprocess
+    cdir = os.path.join(os.path.dirname(__file__), "c")
+    with open(os.path.join(cdir, ".make.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-s", "-C", cdir, "tsan"], check=True)
+    monkeypatch.setenv("TSAN_OPTIONS", "halt_on_error=0 second_deadlock_stack=1")
+    if exe == "async_resend":
+        a = (shm_name(), "host") + (args or ())
+    else:
+        a = args
+    codes, outs = launch_exe(os.path.join(cdir, "_build", "tsan", exe), world, a, timeout=180)
+    assert codes == [0] * world, "\n".join(outs)
+    for out in outs:
+        assert "ThreadSanitizer" not in out, out
+
+
 @pytest.mark.parametrize("world", [3, 4])
 def test_completion_callback_and_flags(world):
     """ucg_params_t.completion (api/ucg.h:162-171) as

@@ -848,9 +848,17 @@ void ucg_builtin_lgroup_async_stats(ucg_builtin_lgroup_t *g, uint64_t out[2])
 void ucg_builtin_lgroup_stats(ucg_builtin_lgroup_t *g, uint64_t out[4])
 {
     int i;
-    for (i = 0; i < 4; i++) {
-        out[i] = g ? g->stats[i] : 0;
+    if (g == NULL) {
+        memset(out, 0, 4 * sizeof(uint64_t));
+        return;
     }
+    /* under the group's lock: the resend timer's thread counts too (a race
+     * ThreadSanitizer found, round 6) */
+    group_block(g);
+    for (i = 0; i < 4; i++) {
+        out[i] = g->stats[i];
+    }
+    group_unblock(g);
 }
 
 static void lcoll_free(ucg_builtin_lcoll_t *c)
