@@ -105,10 +105,11 @@ struct ucg_builtin_shm_iface {
     ucs_status_t open_status;  /* why ucg_builtin_shm_iface_open failed */
     /* peer failure (shm_peer_check): the first member found gone, and the
      * status every later barrier and close returns at once (the barrier's
-     * count is no longer shared once one member gave up on it) */
-    int       dead;            /* member index + 1, 0 = none found */
-    ucs_status_t broken;
-    double    live_check_t;    /* last liveness probe (now_s) */
+     * count is no longer shared once one member gave up on it). Atomic: the
+     * owner's barrier and every group's resend timer thread probe them. */
+    _Atomic int      dead;          /* member index + 1, 0 = none found */
+    _Atomic int      broken;        /* ucs_status_t; first non-OK one sticks */
+    _Atomic uint64_t live_check_ns; /* last liveness probe (monotonic ns) */
     uint16_t  group_gen[UNEXP_GROUPS];  /* groups created per slot */
     /* ops layer: groups by id and messages for groups not created yet
      * (the reference's bctx->group_by_id / bctx->unexpected, builtin.c:

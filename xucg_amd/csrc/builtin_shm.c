@@ -174,26 +174,49 @@ static void member_attach(ucg_builtin_shm_iface_t *it)
     atomic_store_explicit(&m->pid, (uint64_t)getpid(), memory_order_release);
 }
 
+/* the first failure sticks: later ones (a timeout after a reset) keep it */
+static ucs_status_t set_broken(ucg_builtin_shm_iface_t *it, ucs_status_t st)
+{
+    int ok = UCS_OK;
+    atomic_compare_exchange_strong_explicit(&it->broken, &ok, (int)st, memory_order_acq_rel,
+                                            memory_order_acquire);
+    return (ucs_status_t)atomic_load_explicit(&it->broken, memory_order_acquire);
+}
+
+static inline ucs_status_t broken_status(ucg_builtin_shm_iface_t *it)
+{
+    return (ucs_status_t)atomic_load_explicit(&it->broken, memory_order_acquire);
+}
+
 UCG_INTERNAL int shm_peer_check(ucg_builtin_shm_iface_t *it)
 {
-    const double t = now_s();
+    const uint64_t t = (uint64_t)(now_s() * 1e9);
+    uint64_t last = atomic_load_explicit(&it->live_check_ns, memory_order_relaxed);
+    int dead = atomic_load_explicit(&it->dead, memory_order_acquire);
     unsigned m;
-    if (it->dead || t - it->live_check_t < PEER_CHECK_S) {
-        return it->dead - 1;
+    /* one prober per interval: the owner and the timer threads race for it */
+    if (dead || t - last < (uint64_t)(PEER_CHECK_S * 1e9) ||
+        !atomic_compare_exchange_strong_explicit(&it->live_check_ns, &last, t,
+                                                 memory_order_relaxed,
+                                                 memory_order_relaxed)) {
+        return atomic_load_explicit(&it->dead, memory_order_acquire) - 1;
     }
-    it->live_check_t = t;
     for (m = 0; m < it->members; m++) {
         const member_ctl_t *mc = member_ctl(it, m);
         const uint64_t pid = atomic_load_explicit(&mc->pid, memory_order_acquire);
+        int none = 0;
         /* not attached yet, or in another pid namespace: cannot tell */
         if (m == it->my || pid == 0 || owner_state(pid, mc->pidns) != 0) {
             continue;
         }
-        fprintf(stderr, "ucg_builtin_shm(%s): member %u (pid %llu) is gone\n", it->name, m,
-                (unsigned long long)pid);
-        it->dead   = (int)m + 1;
-        it->broken = UCS_ERR_CONNECTION_RESET;
-        return (int)m;
+        if (atomic_compare_exchange_strong_explicit(&it->dead, &none, (int)m + 1,
+                                                    memory_order_acq_rel,
+                                                    memory_order_acquire)) {
+            fprintf(stderr, "ucg_builtin_shm(%s): member %u (pid %llu) is gone\n", it->name,
+                    m, (unsigned long long)pid);
+        }
+        set_broken(it, UCS_ERR_CONNECTION_RESET);
+        return atomic_load_explicit(&it->dead, memory_order_acquire) - 1;
     }
     return -1;
 }
@@ -505,8 +528,8 @@ ucs_status_t ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
     if (it == NULL) {
         return UCS_ERR_INVALID_PARAM;
     }
-    if (it->broken != UCS_OK) {
-        return it->broken;
+    if (broken_status(it) != UCS_OK) {
+        return broken_status(it);
     }
     arrive = &((seg_hdr_t*)it->seg)->arrive;
     gen    = ++it->barrier_gen;
@@ -516,13 +539,12 @@ ucs_status_t ucg_builtin_shm_barrier(ucg_builtin_shm_iface_t *it)
     while (atomic_load_explicit(arrive, memory_order_acquire) < gen * it->members) {
         if ((++spins & 255) == 0) {
             if (shm_peer_check(it) >= 0) {
-                return it->broken;
+                return broken_status(it);
             }
             if (now_s() - t0 > lim) {
                 fprintf(stderr, "ucg_builtin_shm_barrier(%s): timed out after %.0f s\n",
                         it->name, lim);
-                it->broken = UCS_ERR_TIMED_OUT;
-                return it->broken;
+                return set_broken(it, UCS_ERR_TIMED_OUT);
             }
         }
         sched_yield();
@@ -579,7 +601,7 @@ static ucs_status_t spin_lock(ucg_builtin_shm_iface_t *it, _Atomic uint32_t *l)
             t0 = now_s();
         } else if ((spins & 1023) == 0) {
             if (shm_peer_check(it) >= 0) {
-                return it->broken;
+                return broken_status(it);
             }
             if (now_s() - t0 > wait_timeout_s()) {
                 fprintf(stderr, "ucg_builtin_shm: incast cell lock held for over %.0f s\n",
