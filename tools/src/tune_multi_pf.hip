@@ -223,6 +223,86 @@ k_read_store0(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+
+/* Round 6: persistent waves - a grid of G one-wave workgroups (a multiple of
+ * 8, so logical tile b + G stays on b's XCD) walks the same XCD tile map as
+ * the product; PIPE issues the next tile's N loads before the current tile's
+ * combine and store, so a wave always has loads in flight behind its store */
+template <int N, int D, int PIPE, int CAPV = 1>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_persist(float *dst, SrcList srcs, size_t nvec)
+{
+    if constexpr (CAPV) {
+        UCG_MULTI_CAP_CLOBBER();
+    }
+    const unsigned ntiles = (unsigned)((nvec + kReduceBlock - 1) / kReduceBlock);
+    const unsigned G = gridDim.x;
+    unsigned b = blockIdx.x;
+    if (b >= ntiles) {
+        return;
+    }
+    const u32x4 *op[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        op[m] = reinterpret_cast<const u32x4*>(srcs.p[m]);
+    }
+    u32x4 *d4 = reinterpret_cast<u32x4*>(dst);
+    auto fv = [](u32x4 a, u32x4 c) { return vapply<float, 0>(a, c); };
+    size_t i = (size_t)xcd_tile<kXcdChunk>(b, ntiles) * kReduceBlock + threadIdx.x;
+    u32x4 cur[N];
+    {
+        const size_t ic = i < nvec ? i : nvec - 1;
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            cur[m] = ld16<1>(op[m] + ic);
+        }
+    }
+    for (;;) {
+        const unsigned bn = b + G;
+        const bool more = bn < ntiles;
+        const size_t in = more ? (size_t)xcd_tile<kXcdChunk>(bn, ntiles) * kReduceBlock +
+                                 threadIdx.x : i;
+        const size_t inc = in < nvec ? in : nvec - 1;
+        /* the prefetch lines first, then the next tile's loads: waiting for
+         * the prefetch (and so the current tile) leaves those in flight */
+        const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+        const size_t want = (i - threadIdx.x + (size_t)D * kReduceBlock) + (size_t)k * 8;
+        const size_t at   = (k < 1u && want < nvec) ? want : nvec - 1;
+        u32x4 pf[N], nxt[N];
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            pf[m] = ld16<0>(op[m] + at);
+        }
+        if constexpr (PIPE) {
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                nxt[m] = ld16<1>(op[m] + inc);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            asm volatile("" :: "v"(pf[m][0]));
+        }
+        if (i < nvec) {
+            st16<1>(d4 + i, rd_tree<N>(cur, fv));
+        }
+        if (!more) {
+            break;
+        }
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            if constexpr (PIPE) {
+                cur[m] = nxt[m];
+            } else {
+                cur[m] = ld16<1>(op[m] + inc);
+            }
+        }
+        i = in;
+        b = bn;
+    }
+}
+
 template <int N>
 static void add_multi(std::vector<Variant> &vs)
 {
@@ -309,6 +389,31 @@ static void add_multi(std::vector<Variant> &vs)
         UV("U4, PF1 per row, 1 tile ahead", 4, 1, 1);
     }
 #undef UV
+    /* round 6 (r06p): persistent waves, and occupancy between 12 and 16
+     * waves per CU (uncapped registers, LDS bounding the workgroups) */
+#define PV(label, G, D, PIPE, CAPV)                                                      \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_multi_persist<N, D, PIPE, CAPV>), dim3(G), dim3(kReduceBlock), \
+                           0, q, d, s, nv);                                               \
+    }, true, {}})
+    PV("persistent 12/CU, no pipeline, 4 ahead", 3072, 4, 0, 1);
+    PV("persistent 12/CU, pipelined, 4 ahead", 3072, 4, 1, 1);
+    PV("persistent 12/CU, pipelined, 2 ahead", 3072, 2, 1, 1);
+    PV("persistent 8/CU, pipelined, 4 ahead", 2048, 4, 1, 1);
+    PV("persistent 16/CU, pipelined, 4 ahead", 4096, 4, 1, 0);
+    PV("persistent 16/CU, no pipeline, 4 ahead", 4096, 4, 0, 0);
+#undef PV
+#define OV(label, D, LDS)                                                                 \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_reduce_multi<float, 0, N, 1, 0, 1, N, D>), dim3(tiles(nv)),  \
+                           dim3(kReduceBlock), LDS, q, d, s, 0u, (size_t)0, nv, (size_t)0); \
+    }, true, {}})
+    OV("uncapped regs, LDS cap 12 waves/CU, 4 ahead", 4, 163840 / 12);
+    OV("uncapped regs, LDS cap 13 waves/CU, 4 ahead", 4, 163840 / 13);
+    OV("uncapped regs, LDS cap 14 waves/CU, 4 ahead", 4, 163840 / 14);
+    OV("uncapped regs, LDS cap 16 waves/CU, 4 ahead", 4, 163840 / 16);
+    OV("uncapped regs, LDS cap 20 waves/CU, 4 ahead", 4, 163840 / 20);
+#undef OV
     vs.push_back({"product form, in place: dst = operand 0 (unchecked)",
                   [](float *d, SrcList s, size_t nv, hipStream_t q) {
         (void)d;
@@ -385,6 +490,9 @@ int main(int argc, char **argv)
     /* layout 1: every operand and the output in an allocation of its own (as
      * N ranks' buffers are), instead of one arena S + stagger apart */
     const int separate   = argc > 6 ? atoi(argv[6]) : 0;
+    /* optional: only the variants whose names contain one of these
+     * ','-separated substrings (the reference variant and ceilings always) */
+    const std::string only = argc > 7 ? argv[7] : "";
     const int iters  = 10;
     if ((!tree && (N != 2 && N != 4 && N != 8 && N != 16)) || (tree && (N < 2 || N > 16))) {
         fprintf(stderr, "N: multi 2/4/8/16, tree 2..16\n");
@@ -444,6 +552,23 @@ int main(int argc, char **argv)
         }
     }
 
+    if (!only.empty()) {
+        std::vector<Variant> keep;
+        for (size_t k = 0; k < vs.size(); k++) {
+            bool hit = k == 0 || vs[k].name.rfind("ceiling", 0) == 0;
+            size_t a = 0;
+            while (!hit && a <= only.size()) {
+                const size_t e = std::min(only.find(',', a), only.size());
+                const std::string w = only.substr(a, e - a);
+                hit = !w.empty() && vs[k].name.find(w) != std::string::npos;
+                a = e + 1;
+            }
+            if (hit) {
+                keep.push_back(vs[k]);
+            }
+        }
+        vs.swap(keep);
+    }
     vs[0].run(ref, srcs, nvec, st);
     CHECK(hipStreamSynchronize(st));
     std::vector<float> hr(n), ho(n);
