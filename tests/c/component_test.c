@@ -93,17 +93,19 @@ static int dt_cls(void *dt)
 }
 
 typedef struct {
-    volatile int  done;
+    int           done;
     ucs_status_t  status;
     int           calls;
 } request_t;
 
+/* may run on the resend timer's thread (builtin.c:284-294): the status is
+ * published by the release store, and the poller reads it after an acquire */
 static void comp_cb(void *req, ucs_status_t status)
 {
     request_t *r = req;
     r->status = status;
     r->calls++;
-    r->done = 1;
+    __atomic_store_n(&r->done, 1, __ATOMIC_RELEASE);
 }
 
 static char in_place_marker;
@@ -192,7 +194,7 @@ static ucs_status_t coll_run(ucg_group_h g, ucg_coll_h coll)
     if (st != UCS_OK && st != UCS_INPROGRESS) {
         return st;
     }
-    while (!req.done) {
+    while (!__atomic_load_n(&req.done, __ATOMIC_ACQUIRE)) {
         progress(coll);
         if ((++polls & 4095) == 0 && time(NULL) - t0 > 60) {
             return UCS_ERR_TIMED_OUT;

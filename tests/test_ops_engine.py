@@ -283,17 +283,34 @@ def test_component_and_timer_host_sanitizers(monkeypatch, exe, world, args):
         assert "Sanitizer" not in out and "runtime error" not in out, out
 
 
+@pytest.mark.parametrize("world,groups", [(4, 3), (2, 5), (3, 2)])
+def test_groups_sharing_one_interface_with_timers(world, groups):
+    """Several groups on one transport object, each with a resend timer
+    thread, every group's allreduce in flight at once on a 2-cell ring
+    (tests/c/multi_group_timers.c). Every group's progress and timer reach the
+    shared rings and the group table, so the engine's lock is the
+    interface's, as the reference's UCS_ASYNC_BLOCK is the worker's
+    (builtin/builtin.c:263-267, 284-294, 331-335). Before round 6 it was the
+    group's: two timers wrote the same ring cell and the members hung."""
+    exe = os.path.join(ROOT, "tests", "c", "_build", "multi_group_timers")
+    codes, outs = launch_exe(exe, world, (shm_name(), groups, 40), timeout=120)
+    assert codes == [0] * world, "\n".join(outs)
+
+
 @pytest.mark.parametrize("exe,world,args", [("async_resend", 2, None),
                                              ("async_resend", 4, ("round",)),
-                                             ("component_test", 4, ("host",))])
+                                             ("component_test", 4, ("host",)),
+                                             ("multi_group_timers", 4, ("3", "40"))])
 def test_engine_thread_sanitizer(monkeypatch, exe, world, args):
     """SURVEY 5, race detection: the host engine rebuilt with ThreadSanitizer
     (tests/c/Makefile, target tsan), with the resend timer's thread working
     against the owner thread (async_resend: the timer sends and combines
     while the owner sleeps, then both wait; the plan component with its
-    timer running). Any data race report fails the rank. Round 6 found one:
-    ucg_builtin_lgroup_stats read the counters the timer thread writes
-    without the group's lock."""
+    timer running; several groups with timers on one interface). Any data
+    race report fails the rank. Round 6 found three: ucg_builtin_lgroup_stats
+    read the counters the timer thread writes without the group's lock; the
+    interface's liveness state was plain fields; and groups sharing an
+    interface each had a lock of their own for the shared rings."""
     import fcntl
     import subprocess
     cdir = os.path.join(os.path.dirname(__file__), "c")
@@ -303,6 +320,8 @@ def test_engine_thread_sanitizer(monkeypatch, exe, world, args):
     monkeypatch.setenv("TSAN_OPTIONS", "halt_on_error=0 second_deadlock_stack=1")
     if exe == "async_resend":
         a = (shm_name(), "host") + (args or ())
+    elif exe == "multi_group_timers":
+        a = (shm_name(),) + args
     else:
         a = args
     codes, outs = launch_exe(os.path.join(cdir, "_build", "tsan", exe), world, a, timeout=180)

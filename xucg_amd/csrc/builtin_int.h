@@ -116,6 +116,9 @@ struct ucg_builtin_shm_iface {
      * 150-205) */
     ucg_builtin_lgroup_t *groups[UNEXP_GROUPS];
     stash_t  *unexpected;
+    /* the worker's async context: one recursive lock for every group of this
+     * interface (ucg_builtin_lgroup.async_lock points here) */
+    pthread_mutex_t async_lock;
 };
 
 static inline double now_s(void)
@@ -251,8 +254,12 @@ struct ucg_builtin_lgroup {
     unsigned                 nimp;
     /* the worker's async context (UCS_ASYNC_BLOCK, builtin.c:263-267, 331-335):
      * every entry point holds this recursive lock, and so does the resend
-     * timer (builtin.c:284-294, 408-413) when it runs on its own thread */
-    pthread_mutex_t          async_lock;
+     * timer (builtin.c:284-294, 408-413) when it runs on its own thread. It is
+     * the interface's (ucg_builtin_shm_iface.async_lock), as the reference's is
+     * the worker's: every group's progress and timer reach the shared rings,
+     * the group table and the unexpected list, and deliver each other's
+     * messages */
+    pthread_mutex_t         *async_lock;
     pthread_cond_t           timer_cv;
     pthread_t                timer;
     int                      timer_on;
@@ -290,7 +297,7 @@ struct ucg_builtin_lcoll {
     unsigned     nsteps;
     /* request state (builtin_ops.h:233-241) */
     int          active;
-    int          done;
+    int          done;            /* set by lcoll_set_done: a waiter polls it unlocked */
     ucs_status_t status;
     uint8_t      coll_id;
     unsigned     cur;
@@ -356,6 +363,19 @@ struct ucg_builtin_lcoll {
     uint64_t     seq;             /* the group's start count at this start */
     int          peer_ended;      /* finished because of a peer: not published */
 };
+
+/* An op may finish on the resend timer's thread while its owner polls `done`
+ * outside the lock (lcoll_wait, lcoll_test): the status is written first and
+ * published by the release store. */
+static inline void lcoll_set_done(ucg_builtin_lcoll_t *c)
+{
+    __atomic_store_n(&c->done, 1, __ATOMIC_RELEASE);
+}
+
+static inline int lcoll_is_done(const ucg_builtin_lcoll_t *c)
+{
+    return __atomic_load_n(&c->done, __ATOMIC_ACQUIRE);
+}
 
 /* planner state (builtin_plan.c) */
 #define TREE_MAX_RADIX 128   /* UCG_BUILTIN_TREE_MAX_RADIX, builtin_plan.h:98 */

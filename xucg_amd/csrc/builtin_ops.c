@@ -43,12 +43,12 @@ UCG_INTERNAL int ops_on_timer_thread(void)
  * the stash drain re-enter the engine on the same thread) */
 static inline void group_block(ucg_builtin_lgroup_t *g)
 {
-    pthread_mutex_lock(&g->async_lock);
+    pthread_mutex_lock(g->async_lock);
 }
 
 static inline void group_unblock(ucg_builtin_lgroup_t *g)
 {
-    pthread_mutex_unlock(&g->async_lock);
+    pthread_mutex_unlock(g->async_lock);
 }
 
 static stash_t *stash_new(uint64_t header, const void *payload, size_t length)
@@ -97,7 +97,7 @@ UCG_INTERNAL void finish(ucg_builtin_lcoll_t *c, ucs_status_t status)
                     abandon_word(c->g->gen, c->g->group_id, c->seq));
     }
     c->status       = status;
-    c->done         = 1;
+    lcoll_set_done(c);
     c->active       = 0;
     c->send_pending = 0;
     c->step_started = 0;
@@ -607,21 +607,20 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
             }
         }
     }
-    if (iface->groups[group_id % UNEXP_GROUPS] != NULL) {
-        return UCS_ERR_BUSY;
-    }
     g = calloc(1, sizeof(*g));
     if (g == NULL) {
         return UCS_ERR_NO_MEMORY;
     }
-    {
-        pthread_mutexattr_t a;
-        pthread_mutexattr_init(&a);
-        pthread_mutexattr_settype(&a, PTHREAD_MUTEX_RECURSIVE);
-        pthread_mutex_init(&g->async_lock, &a);
-        pthread_mutexattr_destroy(&a);
-        pthread_cond_init(&g->timer_cv, NULL);
+    /* the other groups' timers may be delivering into the table and the
+     * unexpected list right now */
+    pthread_mutex_lock(&iface->async_lock);
+    if (iface->groups[group_id % UNEXP_GROUPS] != NULL) {
+        pthread_mutex_unlock(&iface->async_lock);
+        free(g);
+        return UCS_ERR_BUSY;
     }
+    pthread_cond_init(&g->timer_cv, NULL);
+    g->async_lock = &iface->async_lock;
     g->iface    = iface;
     g->group_id = group_id;
     g->size     = member_count;
@@ -670,6 +669,7 @@ ucs_status_t ucg_builtin_lgroup_create_ex(ucg_builtin_shm_iface_t *iface,
             pp = &(*pp)->next;
         }
     }
+    pthread_mutex_unlock(&iface->async_lock);
     *group_p = g;
     return UCS_OK;
 }
@@ -699,6 +699,10 @@ void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
         pthread_join(g->timer, NULL);
         g->timer_on = 0;
     }
+    /* out of the table first: another group's timer delivers nothing more
+     * here once it is gone */
+    group_block(g);
+    g->iface->groups[g->group_id % UNEXP_GROUPS] = NULL;
     for (i = 0; i < UCG_BUILTIN_OPS_MAX_CONCURRENT; i++) {
         stash_t *m;
         while ((m = g->slots[i].msgs) != NULL) {
@@ -706,10 +710,9 @@ void ucg_builtin_lgroup_destroy(ucg_builtin_lgroup_t *g)
             free(m);
         }
     }
-    g->iface->groups[g->group_id % UNEXP_GROUPS] = NULL;
+    group_unblock(g);
     rma_group_free(g);
     pthread_cond_destroy(&g->timer_cv);
-    pthread_mutex_destroy(&g->async_lock);
     free(g);
 }
 
@@ -808,7 +811,7 @@ static void *async_timer(void *arg)
         const double t = now_s() + g->timer_tick;   /* CLOCK_MONOTONIC, as the condvar */
         ts.tv_sec  = (time_t)t;
         ts.tv_nsec = (long)((t - (double)(time_t)t) * 1e9);
-        pthread_cond_timedwait(&g->timer_cv, &g->async_lock, &ts);
+        pthread_cond_timedwait(&g->timer_cv, g->async_lock, &ts);
         if (!g->timer_stop) {
             g->async_resends += group_resend(g);
             group_check_peers(g);
@@ -913,8 +916,8 @@ static ucs_status_t lcoll_new(ucg_builtin_lgroup_t *g, const void *sbuf,
     c->length = (size_t)count * dt_len;
     c->rma    = rma;              /* buffers set up once the plan is known */
     c->pool_idx[0] = c->pool_idx[1] = -1;
-    c->done   = 1;
     c->status = UCS_OK;
+    lcoll_set_done(c);
     *coll_p   = c;
     return UCS_OK;
 }
@@ -1130,8 +1133,8 @@ static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id)
     c->step_started = 0;
     c->send_pending = 0;
     if (c->nsteps == 0 || c->length == 0) {
-        c->done   = 1;
         c->status = UCS_OK;
+        lcoll_set_done(c);
         lcoll_notify(c);
         return UCS_OK;
     }
@@ -1143,10 +1146,11 @@ static ucs_status_t lcoll_start_at(ucg_builtin_lcoll_t *c, uint8_t coll_id)
 
 int ucg_builtin_lcoll_test(ucg_builtin_lcoll_t *c, ucs_status_t *status)
 {
-    if (c->done && status) {
+    const int done = lcoll_is_done(c);
+    if (done && status) {
         *status = c->status;
     }
-    return c->done;
+    return done;
 }
 
 /* UCX_BUILTIN_TIMEOUT_DUMP=y: on a timed-out wait, the op's state and what
@@ -1193,7 +1197,7 @@ ucs_status_t ucg_builtin_lcoll_wait(ucg_builtin_lcoll_t *c)
         lim  = wait_timeout_s();
         spin = e ? atol(e) : 4096;
     }
-    while (!c->done) {
+    while (!lcoll_is_done(c)) {
         if (ucg_builtin_lgroup_progress(c->g) != 0) {
             idle = 0;
             /* progress counts resend attempts too: a peer that stopped

@@ -1085,8 +1085,8 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     c->send_pending = 0;
     memset(c->rdy_cnt, 0, sizeof(c->rdy_cnt));
     if (c->length == 0) {
-        c->done   = 1;
         c->status = UCS_OK;
+        lcoll_set_done(c);
         lcoll_notify(c);
         return UCS_OK;
     }
@@ -1096,8 +1096,8 @@ UCG_INTERNAL ucs_status_t rma_start(ucg_builtin_lcoll_t *c, op_slot_t *slot)
     c->cur_buf = c->exp_sbuf ? 2 : 0;
     st = c->exp_sbuf ? UCS_OK : rma_copy(c, c->dbuf[0], c->sbuf ? c->sbuf : c->rbuf);
     if (st != UCS_OK) {
-        c->done   = 1;
         c->status = st;
+        lcoll_set_done(c);
         lcoll_notify(c);
         return st;
     }

@@ -434,6 +434,13 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
     if (it == NULL) {
         return UCS_ERR_NO_MEMORY;
     }
+    {
+        pthread_mutexattr_t a;
+        pthread_mutexattr_init(&a);
+        pthread_mutexattr_settype(&a, PTHREAD_MUTEX_RECURSIVE);
+        pthread_mutex_init(&it->async_lock, &a);
+        pthread_mutexattr_destroy(&a);
+    }
     snprintf(it->name, sizeof(it->name), "/%s", name[0] == '/' ? name + 1 : name);
     it->members    = members;
     it->my         = my_index;
@@ -459,6 +466,7 @@ ucs_status_t ucg_builtin_shm_iface_open(const char *name, unsigned members,
 
     if (iface_map(it) != UCS_OK) {
         ucs_status_t st = it->open_status;
+        pthread_mutex_destroy(&it->async_lock);
         free(it);
         return st;
     }
@@ -506,6 +514,7 @@ ucs_status_t ucg_builtin_shm_iface_close(ucg_builtin_shm_iface_t *it)
         it->unexpected = m->next;
         free(m);
     }
+    pthread_mutex_destroy(&it->async_lock);
     free(it);
     return st;
 }
