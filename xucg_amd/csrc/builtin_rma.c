@@ -1176,22 +1176,32 @@ void *ucg_builtin_lgroup_mem_alloc(ucg_builtin_lgroup_t *g, size_t bytes, int on
         (on_device && !ucg_builtin_combine_has_device(g->cmb))) {
         return NULL;
     }
+    /* the pool is the group's: an op starting or resent on the timer's
+     * thread takes buffers from it under the same lock */
+    void *ptr = NULL;
+    pthread_mutex_lock(g->async_lock);
     k = rma_pool_get(g, bytes, kind);
-    if (k < 0) {
-        return NULL;
+    if (k >= 0) {
+        g->pool[k].user = 1;
+        ptr = g->pool[k].ptr;       /* the table may grow once unlocked */
     }
-    g->pool[k].user = 1;
-    return g->pool[k].ptr;
+    pthread_mutex_unlock(g->async_lock);
+    return ptr;
 }
 
 void ucg_builtin_lgroup_mem_free(ucg_builtin_lgroup_t *g, void *ptr)
 {
     unsigned i;
-    for (i = 0; g && ptr && i < g->npool; i++) {
+    if (g == NULL || ptr == NULL) {
+        return;
+    }
+    pthread_mutex_lock(g->async_lock);
+    for (i = 0; i < g->npool; i++) {
         if (g->pool[i].user && g->pool[i].ptr == ptr) {
             g->pool[i].user = 0;      /* back to the pool: the memory and its key */
             g->pool[i].busy = 0;      /* stay valid until the group is destroyed */
-            return;
+            break;
         }
     }
+    pthread_mutex_unlock(g->async_lock);
 }
