@@ -9,6 +9,8 @@
 #            (scripts/profile_round.sh, pmc_summary.py)
 #   dryalloc bench.py --collective-dry-alloc (one rank's C4 + C5 buffers)
 #   gather   the out-of-phase gather A/B (tools/tune_misalign)
+#   c3       BASELINE config 3: every dtype x op, 1 KiB - 1 GiB (sweep_c3.py), and
+#            the lowest pairs interleaved with fp32 SUM (c3_interleaved.py)
 # usage: scripts/gpu_r06.sh TAG step...
 set -u
 TAG=$1; shift
@@ -40,6 +42,9 @@ for s in "$@"; do
     timeout -k 10 300 python bench.py --collective-dry-alloc > $OUT/dryalloc.json 2> $OUT/dryalloc.err || { tail -5 $OUT/dryalloc.err; exit 1; } ;;
   gather)
     timeout -k 10 200 tools/tune_misalign 5 > $OUT/tune_misalign.txt 2>&1 || exit 1 ;;
+  c3)
+    timeout -k 10 400 python scripts/sweep_c3.py $OUT/c3_sweep.json > $OUT/c3_sweep.log 2>&1 || exit 1
+    timeout -k 10 300 python scripts/c3_interleaved.py $OUT/c3_interleaved.json > $OUT/c3_interleaved.log 2>&1 || exit 1 ;;
   esac
   echo "done $s $(date +%T)" >> $OUT/steps.log
 done
