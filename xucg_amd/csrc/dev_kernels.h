@@ -132,7 +132,7 @@ __device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
  * (tools/tune_misalign, profiles/r04/r04q-r04v). Loads are
  * clamped and unmasked behind a sched barrier, as in k_reduce_shift.
  */
-template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0>
+template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0, int ORD = 0>
 __global__ void __launch_bounds__(BS)
 k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 {
@@ -164,9 +164,31 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
          * vector (one line, an L2 hit), so the load needs no branch */
         const unsigned k = BS - 1 - threadIdx.x;
         const size_t want = (i - threadIdx.x + BS) + (size_t)k * 8;
-        const u32x4 a  = ld16<NT>(s4 + ic);
-        const u32x4 b  = ld16<NT>(d4 + ic);
-        const u32x4 pf = ld16<0>(s4 + (k < (unsigned)PF && want < nvec ? want : nvec - 1));
+        const u32x4 *at   = s4 + (k < (unsigned)PF && want < nvec ? want : nvec - 1);
+        u32x4 a, b, pf;
+        if constexpr (ORD == 0) {           /* the compiler's order */
+            a  = ld16<NT>(s4 + ic);
+            b  = ld16<NT>(d4 + ic);
+            pf = ld16<0>(at);
+        } else if constexpr (ORD == 1) {    /* src, the prefetch, dst */
+            a  = ld16<NT>(s4 + ic);
+            __builtin_amdgcn_sched_barrier(0);
+            pf = ld16<0>(at);
+            __builtin_amdgcn_sched_barrier(0);
+            b  = ld16<NT>(d4 + ic);
+        } else if constexpr (ORD == 2) {    /* the prefetch, src, dst */
+            pf = ld16<0>(at);
+            __builtin_amdgcn_sched_barrier(0);
+            a  = ld16<NT>(s4 + ic);
+            __builtin_amdgcn_sched_barrier(0);
+            b  = ld16<NT>(d4 + ic);
+        } else {                            /* src, dst, the prefetch */
+            a  = ld16<NT>(s4 + ic);
+            __builtin_amdgcn_sched_barrier(0);
+            b  = ld16<NT>(d4 + ic);
+            __builtin_amdgcn_sched_barrier(0);
+            pf = ld16<0>(at);
+        }
         __builtin_amdgcn_sched_barrier(0);
         asm volatile("" :: "v"(pf[0]));     /* the load stays; its value is unused */
         if (i < nvec) {

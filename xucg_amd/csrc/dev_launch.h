@@ -80,6 +80,13 @@ inline bool straddles_lines(const void *p)
  * ahead (k_reduce's PF form) */
 constexpr int kPrefetchLines = 3;
 
+/* the order its three loads issue in (k_reduce's ORD): the next tile's lines
+ * first, then src, then dst. The compiler's own order varied with the
+ * (dtype, op) and the translation unit; at 256 MiB per operand this order read
+ * 0.5-1.1 points above the others for all 7 pairs timed, on two boxes, and at
+ * 1 GiB within 0.4 of the best (tools/tune_order, profiles/r06/order/) */
+constexpr int kLoadOrder = 2;
+
 /* The in-phase multi-operand kernels' PF form (round 5):
  * one line of the next tile per prefetched operand (tools/tune_multi_pf,
  * profiles/r05/pf, 64 MiB per operand, A/B in one process): N = 8 and 16,
@@ -131,7 +138,8 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStre
         if (first && div_up(head, kReduceBlock) > grid) {
             grid = (unsigned)div_up(head, kReduceBlock);
         }
-        hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, kPrefetchLines>), dim3(grid),
+        hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, kPrefetchLines, kLoadOrder>),
+                           dim3(grid),
                            dim3(kReduceBlock), 0, st, d + off, s + off, first ? head : 0,
                            chunk, last ? tail : 0);
         done += chunk;
