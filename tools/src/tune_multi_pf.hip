@@ -200,6 +200,47 @@ k_multi_buf(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+/* Round 6 (r06v): the product's PF form with its prefetch lines issued
+ * BEFORE the operand loads (the 2-operand combine gained 0.5-1.1 points at
+ * 256 MiB from that order, tools/tune_order); PFM operands' lines D tiles
+ * ahead, sched barriers fixing the order */
+template <int N, int D, int PFM>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_pffirst(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * kReduceBlock +
+                      threadIdx.x;
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const u32x4 *op[N];
+    u32x4 val[N], pf[PFM];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        op[m] = reinterpret_cast<const u32x4*>(srcs.p[m]);
+    }
+    const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+    const size_t want = (i - threadIdx.x + (size_t)D * kReduceBlock) + (size_t)k * 8;
+    const size_t at   = (k < 1u && want < nvec) ? want : nvec - 1;
+#pragma unroll
+    for (int m = 0; m < PFM; m++) {
+        pf[m] = ld16<0>(op[m] + at);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        val[m] = ld16<1>(op[m] + ic);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < PFM; m++) {
+        asm volatile("" :: "v"(pf[m][0]));
+    }
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val, fv));
+    }
+}
+
 /* the N operands read and dst written with zeros: the traffic of the
  * combine, no dependency of a store on its loads */
 template <int N>
@@ -328,6 +369,11 @@ static void add_multi(std::vector<Variant> &vs)
     MV("PF3, all operands, uncapped", 1, 0, 3, N, true);
     MV("PF1, all operands, uncapped", 1, 0, 1, N, true);
     MV("PF1, all operands, 8 tiles ahead", 1, 1, 1, N, true, 8);
+    /* r06w: the product kernel with PFO = 1 (its lines issued first) */
+    MV("product PFO, all operands, 2 tiles ahead", 1, 1, 1, N, true, 2, 1);
+    MV("product PFO, all operands, 4 tiles ahead", 1, 1, 1, N, true, 4, 1);
+    MV("product PFO, all operands, 8 tiles ahead", 1, 1, 1, N, true, 8, 1);
+    MV("product PFO, operand 0, 4 tiles ahead", 1, 1, 1, 1, true, 4, 1);
 #undef MV
     /* round 6: fewer waves per CU at large operands - the product form with
      * dynamic LDS bounding the workgroups (one wave each) per CU */
@@ -403,6 +449,15 @@ static void add_multi(std::vector<Variant> &vs)
     PV("persistent 16/CU, pipelined, 4 ahead", 4096, 4, 1, 0);
     PV("persistent 16/CU, no pipeline, 4 ahead", 4096, 4, 0, 0);
 #undef PV
+#define FV(label, D, PFM)                                                                \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_multi_pffirst<N, D, PFM>), dim3(tiles(nv)),                 \
+                           dim3(kReduceBlock), 0, q, d, s, nv);                           \
+    }, true, {}})
+    FV("prefetch first, all operands, 2 tiles ahead", 2, N);
+    FV("prefetch first, all operands, 4 tiles ahead", 4, N);
+    FV("prefetch first, operand 0, 2 tiles ahead", 2, 1);
+#undef FV
 #define OV(label, D, LDS)                                                                 \
     vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
         hipLaunchKernelGGL((k_reduce_multi<float, 0, N, 1, 0, 1, N, D>), dim3(tiles(nv)),  \
@@ -452,6 +507,10 @@ static void add_tree(std::vector<Variant> &vs, unsigned n)
     TV("PF1, all operands, 2 tiles ahead", 1, C, 1, NMAX, 2);
     TV("PF1, all operands, 4 tiles ahead", 1, C, 1, NMAX, 4);
     TV("PF1, operand 0 only, 2 tiles ahead", 1, C, 1, 1, 2);
+    TV("product PFO, all operands, 2 tiles ahead", 1, C, 1, NMAX, 2, 1);
+    TV("product PFO, all operands, 4 tiles ahead", 1, C, 1, NMAX, 4, 1);
+    TV("product PFO, root only, 1 tile ahead", 1, C, 1, 1, 1, 1);
+    TV("product PFO, root only, 4 tiles ahead", 1, C, 1, 1, 4, 1);
 #undef TV
 }
 
@@ -464,6 +523,16 @@ static void add_tree_exact(std::vector<Variant> &vs, unsigned n)
     vs.push_back({"exact NMAX = n, PF1 all operands, 2 tiles ahead",
                   [n](float *d, SrcList s, size_t nv, hipStream_t q) {
         hipLaunchKernelGGL((k_reduce_tree<float, 0, NX, 1, 1, 1, NX, 2>), dim3(tiles(nv)),
+                           dim3(kReduceBlock), 0, q, d, s, n, (size_t)0, nv, (size_t)0);
+    }, true, {}});
+    vs.push_back({"exact NMAX = n, PFO all operands, 2 tiles ahead",
+                  [n](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_reduce_tree<float, 0, NX, 1, 1, 1, NX, 2, 1>), dim3(tiles(nv)),
+                           dim3(kReduceBlock), 0, q, d, s, n, (size_t)0, nv, (size_t)0);
+    }, true, {}});
+    vs.push_back({"exact NMAX = n, PFO all operands, 4 tiles ahead",
+                  [n](float *d, SrcList s, size_t nv, hipStream_t q) {
+        hipLaunchKernelGGL((k_reduce_tree<float, 0, NX, 1, 1, 1, NX, 4, 1>), dim3(tiles(nv)),
                            dim3(kReduceBlock), 0, q, d, s, n, (size_t)0, nv, (size_t)0);
     }, true, {}});
     vs.push_back({"exact NMAX = n, PF1 root only, 1 tile ahead",

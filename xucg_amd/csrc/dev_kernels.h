@@ -377,8 +377,37 @@ __device__ __forceinline__ void next_tile_lines(const u32x4 *const (&ops)[PFM > 
     }
 }
 
+/* The same lines issued BEFORE the tile's own loads (PFO = 1 in the
+ * multi-operand kernels): tile_lines_issue, a sched barrier, the operand
+ * loads, then tile_lines_keep. Issued first, the lines are in flight while
+ * the wave waits for its operands (the 2-operand combine's ORD 2). */
+template <int PF, int PFM, int D>
+__device__ __forceinline__ void tile_lines_issue(const u32x4 *const (&ops)[PFM > 0 ? PFM : 1],
+                                                 size_t i, size_t nvec,
+                                                 u32x4 (&pf)[PFM > 0 ? PFM : 1])
+{
+    const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+    const size_t want = (i - threadIdx.x + (size_t)D * kReduceBlock) + (size_t)k * 8;
+    const size_t at   = (k < (unsigned)PF && want < nvec) ? want : nvec - 1;
+#pragma unroll
+    for (int m = 0; m < PFM; m++) {
+        pf[m] = ld16<0>(ops[m] + at);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int PFM>
+__device__ __forceinline__ void tile_lines_keep(const u32x4 (&pf)[PFM > 0 ? PFM : 1])
+{
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int m = 0; m < PFM; m++) {
+        asm volatile("" :: "v"(pf[m][0]));    /* the load stays; its value is unused */
+    }
+}
+
 template <typename T, int OP, int N, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0,
-          int PFD = 1>
+          int PFD = 1, int PFO = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
                size_t tail)
@@ -424,17 +453,39 @@ k_reduce_multi(T *dst, SrcList srcs, unsigned self, size_t head, size_t nvec,
         const size_t ic = i < nvec ? i : nvec - 1;
         const u32x4 *op[N];
         u32x4 val[N];
+        if constexpr (PFO) {
+            /* the next tiles' lines first (tile_lines_issue) */
+            const u32x4 *pops[PFM > 0 ? PFM : 1];
+            u32x4 pf[PFM > 0 ? PFM : 1];
 #pragma unroll
-        for (int m = 0; m < N; m++) {
-            op[m]  = reinterpret_cast<const u32x4*>(static_cast<const T*>(srcs.p[self ^ m]) + head);
-            val[m] = ld16<1>(op[m] + ic);
-        }
-        const u32x4 *pops[PFM > 0 ? PFM : 1];
+            for (int m = 0; m < N; m++) {
+                op[m] = reinterpret_cast<const u32x4*>(static_cast<const T*>(srcs.p[self ^ m]) +
+                                                       head);
+            }
 #pragma unroll
-        for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
-            pops[m] = op[m];
+            for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
+                pops[m] = op[m];
+            }
+            tile_lines_issue<PF, PFM, PFD>(pops, i, nvec, pf);
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                val[m] = ld16<1>(op[m] + ic);
+            }
+            tile_lines_keep<PFM>(pf);
+        } else {
+#pragma unroll
+            for (int m = 0; m < N; m++) {
+                op[m]  = reinterpret_cast<const u32x4*>(static_cast<const T*>(srcs.p[self ^ m]) +
+                                                        head);
+                val[m] = ld16<1>(op[m] + ic);
+            }
+            const u32x4 *pops[PFM > 0 ? PFM : 1];
+#pragma unroll
+            for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
+                pops[m] = op[m];
+            }
+            next_tile_lines<PF, PFM, PFD>(pops, i, nvec);
         }
-        next_tile_lines<PF, PFM, PFD>(pops, i, nvec);
         if (i < nvec) {
             st16<1>(d4 + i, rd_tree<N>(val, fv));
         }
@@ -571,7 +622,7 @@ k_reduce_multi_shift(T *dst, SrcList srcs, unsigned self, size_t head, size_t nv
  * no branch between the loads) and are not combined.
  */
 template <typename T, int OP, int NMAX, int XM = 0, int CAP = 0, int PF = 0, int PFM = 0,
-          int PFD = 1>
+          int PFD = 1, int PFO = 0>
 __global__ void __launch_bounds__(kReduceBlock)
 k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t tail)
 {
@@ -612,18 +663,39 @@ k_reduce_tree(T *dst, SrcList srcs, unsigned n, size_t head, size_t nvec, size_t
         const size_t ic = i < nvec ? i : nvec - 1;
         const u32x4 *op[NMAX];
         u32x4 val[NMAX];
+        if constexpr (PFO) {
+            /* the next tiles' lines first (tile_lines_issue) */
+            const u32x4 *pops[PFM > 0 ? PFM : 1];
+            u32x4 pf[PFM > 0 ? PFM : 1];
 #pragma unroll
-        for (int m = 0; m < NMAX; m++) {
-            op[m]  = reinterpret_cast<const u32x4*>(
-                static_cast<const T*>(srcs.p[(unsigned)m < n ? m : 0]) + head);
-            val[m] = ld16<1>(op[m] + ic);
-        }
-        const u32x4 *pops[PFM > 0 ? PFM : 1];
+            for (int m = 0; m < NMAX; m++) {
+                op[m] = reinterpret_cast<const u32x4*>(
+                    static_cast<const T*>(srcs.p[(unsigned)m < n ? m : 0]) + head);
+            }
 #pragma unroll
-        for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
-            pops[m] = op[m];
+            for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
+                pops[m] = op[m];
+            }
+            tile_lines_issue<PF, PFM, PFD>(pops, i, nvec, pf);
+#pragma unroll
+            for (int m = 0; m < NMAX; m++) {
+                val[m] = ld16<1>(op[m] + ic);
+            }
+            tile_lines_keep<PFM>(pf);
+        } else {
+#pragma unroll
+            for (int m = 0; m < NMAX; m++) {
+                op[m]  = reinterpret_cast<const u32x4*>(
+                    static_cast<const T*>(srcs.p[(unsigned)m < n ? m : 0]) + head);
+                val[m] = ld16<1>(op[m] + ic);
+            }
+            const u32x4 *pops[PFM > 0 ? PFM : 1];
+#pragma unroll
+            for (int m = 0; m < (PFM > 0 ? PFM : 1); m++) {
+                pops[m] = op[m];
+            }
+            next_tile_lines<PF, PFM, PFD>(pops, i, nvec);
         }
-        next_tile_lines<PF, PFM, PFD>(pops, i, nvec);
         if (i < nvec) {
             u32x4 acc = val[0];
 #pragma unroll

@@ -123,6 +123,20 @@ constexpr int kRootPrefetchTiles = 1;
 constexpr int kLargePrefetchTiles = 4;
 constexpr size_t kLargePrefetchVecs = (size_t)1 << 23;   /* 128 MiB per operand */
 
+/* Round 6, last: below 256 MiB per operand the every-operand PF forms
+ * (k_reduce_multi N = 8 and 16, the tree fan-in at n = NMAX and the exact-n
+ * kernels) issue their lines four tiles ahead BEFORE the operand loads (PFO,
+ * tile_lines_issue; the 2-operand combine's kLoadOrder). tools/tune_multi_pf,
+ * profiles/r06/pfo/, A/B in one process on two boxes: k_reduce_multi N = 8
+ * 87.8 / 87.3 % of 8 TB/s at 64 MiB per operand against 86.1 / 84.1 %, 88.5 /
+ * 88.1 against 85.2 / 85.2 % at 128 MiB; N = 16 84.6 against 82.2 % at 64 MiB;
+ * tree n = 8 87.9 against 85.4 %, exact n = 12 87.4 against 83.5 % and 87.9
+ * against 84.5 % at 128 MiB, exact n = 6 87.6 against 84.7 %. At 256 MiB it
+ * lost 1.5 points at N = 8 and n = 6 (79.8 against 81.3 %, 83.0 against
+ * 84.6 %), so from there the forms above stay. */
+constexpr int kPfoTiles = 4;
+constexpr size_t kPfoMaxVecs = (size_t)1 << 24;          /* 256 MiB per operand */
+
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
@@ -286,7 +300,12 @@ hipError_t launch_multi_n(void *dst, const SrcList &srcs, unsigned self,
             }
             const dim3 g(grid), b(kReduceBlock);
             if constexpr (N >= 8) {
-                if (cap && N == 8 && chunk >= kLargePrefetchVecs) {
+                if (cap && chunk < kPfoMaxVecs) {
+                    /* the PF form, lines issued first (PFO), four tiles ahead */
+                    hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N,
+                                                       kPfoTiles, 1>),
+                                       g, b, 0, st, d + off, sl, self, h, chunk, t);
+                } else if (cap && N == 8 && chunk >= kLargePrefetchVecs) {
                     /* the PF form, large operands: the line four tiles ahead */
                     hipLaunchKernelGGL((k_reduce_multi<T, OP, N, 1, 1, kMultiPrefetchLines, N,
                                                        kLargePrefetchTiles>),
@@ -425,7 +444,10 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             } else if (cap) {
                 /* the PF form, capped: every operand's next line when n fills
                  * NMAX, else the root's only */
-                if (n == (unsigned)NMAX)
+                if (n == (unsigned)NMAX && chunk < kPfoMaxVecs)
+                    hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX, kPfoTiles, 1>),
+                                       g, b, 0, st, d + off, sl, n, h, chunk, t);
+                else if (n == (unsigned)NMAX)
                     hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX, DF>), g, b, 0, st,
                                        d + off, sl, n, h, chunk, t);
                 else
@@ -486,10 +508,17 @@ void launch_tree_exact(T *d, const SrcList &srcs, size_t head, size_t nvec, size
         if (first && div_up(head, kReduceBlock) > grid) {
             grid = (unsigned)div_up(head, kReduceBlock);
         }
-        hipLaunchKernelGGL((k_reduce_tree<T, OP, NX, 1, 1, kMultiPrefetchLines, NX,
-                                          kFullPrefetchTiles>),
-                           dim3(grid), dim3(kReduceBlock), 0, st, d + off, sl, (unsigned)NX,
-                           first ? head : 0, chunk, last ? tail : 0);
+        if (chunk < kPfoMaxVecs) {
+            hipLaunchKernelGGL((k_reduce_tree<T, OP, NX, 1, 1, kMultiPrefetchLines, NX,
+                                              kPfoTiles, 1>),
+                               dim3(grid), dim3(kReduceBlock), 0, st, d + off, sl,
+                               (unsigned)NX, first ? head : 0, chunk, last ? tail : 0);
+        } else {
+            hipLaunchKernelGGL((k_reduce_tree<T, OP, NX, 1, 1, kMultiPrefetchLines, NX,
+                                              kFullPrefetchTiles>),
+                               dim3(grid), dim3(kReduceBlock), 0, st, d + off, sl,
+                               (unsigned)NX, first ? head : 0, chunk, last ? tail : 0);
+        }
         done += chunk;
     } while (done < nvec);
 }
