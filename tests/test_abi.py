@@ -120,11 +120,12 @@ def test_kernel_resources():
     for obj in objs:
         for name, vgpr, lds in _kernel_metadata(obj):
             assert lds == 0, (obj, name, lds)
-            # template arguments T, OP, N, XM, CAP, PF, PFM, PFD: CAP is
-            # the fourth integer (round 5 added the prefetch arguments)
+            # template arguments T, OP, N, XM, CAP, PF, PFM, PFD, PFO: CAP
+            # is the fourth integer (round 5 added the prefetch arguments,
+            # round 6 the prefetch order)
             m = re.match(r"_ZN6ucgdev1[34]k_reduce_(multi|tree)I([fd])?", name)
             ints = re.findall(r"Li(\d+)E", name)
-            if m and len(ints) == 7:
+            if m and len(ints) == 8:
                 if ints[3] == "1":
                     capped += 1
                     assert vgpr >= 168, (name, vgpr)
