@@ -1041,13 +1041,15 @@ def same_box_reference(n, iters=50):
             "d2d_copy_gbs": round(2 * n * 4 / (copy_us * 1e-6) / 1e9, 1)}
 
 
-def one_shot_shape(ctx, nsrc=8, per_op=64 << 20, iters=20):
+def one_shot_shape(ctx, nsrc=8, per_op=64 << 20, iters=100):
     """The C4/C5 one-shot reduce-scatter's kernel on one GPU: 8 local operands
     of 64 MiB (ucg_builtin_dev_reduce_multi, the recursive-doubling
     association, occupancy-capped), operands and output in one
     allocation. (N + 1) x S algorithmic bytes per launch; wall clock over
-    back-to-back launches after a warm-up, then a sampled exactness check
-    ("exact" inputs: every association gives the same bits)."""
+    back-to-back launches after a warm-up (enough of them, about 10 ms, that
+    the first launch's latency and the final sync's stay below 1 %), then a
+    sampled exactness check ("exact" inputs: every association gives the
+    same bits)."""
     import numpy as np
     n = per_op // 4
     arena = ctx.alloc((nsrc + 1) * per_op)
@@ -1680,7 +1682,7 @@ def main():
         extra["one_shot_8_operands_64mib_fp32"] = one_shot_shape(ctx)
         # C4's per-GPU shard: 8 operands of 512 MiB
         extra["one_shot_8_operands_512mib_fp32"] = one_shot_shape(ctx, per_op=512 << 20,
-                                                                  iters=10)
+                                                                  iters=20)
         extra["same_box_reference_kernels"] = same_box_reference(n)
         # H2D/D2H-inclusive rate: host-resident (pinned) buffers, pipelined
         hs, hd = xucg_amd.HostBuffer(n * 4), xucg_amd.HostBuffer(n * 4)
