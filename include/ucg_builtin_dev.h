@@ -437,6 +437,15 @@ ucs_status_t ucg_builtin_dev_profile_reduce(ucg_builtin_dev_ctx_t *ctx,
                                             size_t count, unsigned iters,
                                             double *avg_us);
 
+/* The same for ucg_builtin_dev_reduce_multi (the one-shot reduce-scatter's
+ * kernel): `iters` back-to-back launches between two HIP events. */
+ucs_status_t ucg_builtin_dev_profile_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
+                                                  ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                                  void *dst, const void *const *srcs,
+                                                  unsigned nsrc, unsigned self,
+                                                  size_t count, unsigned iters,
+                                                  double *avg_us);
+
 /* Measurement reference, not part of the combine path: the same launch
  * geometry (one wave per workgroup, one non-temporal 16-B vector per lane per
  * stream) streaming `bytes` bytes per stream. kind 0: read two streams (src,

@@ -109,6 +109,9 @@ DEV_API = {
     "ucg_builtin_dev_fill": (_st, [_vp, _int, _int, _u64, _vp, _sz]),
     "ucg_builtin_dev_profile_reduce": (_st, [_vp, _int, _int, _vp, _vp, _sz, _u,
                                              ctypes.POINTER(ctypes.c_double)]),
+    "ucg_builtin_dev_profile_reduce_multi": (_st, [_vp, _int, _int, _vp, ctypes.POINTER(_vp),
+                                                   _u, _u, _sz, _u,
+                                                   ctypes.POINTER(ctypes.c_double)]),
     "ucg_builtin_dev_profile_stream": (_st, [_vp, _int, _vp, _vp, _sz, _u,
                                              ctypes.POINTER(ctypes.c_double)]),
     "ucg_builtin_dev_counters": (None, [_vp, ctypes.POINTER(_u64)]),

@@ -1430,6 +1430,37 @@ ucs_status_t ucg_builtin_dev_profile_reduce(ucg_builtin_dev_ctx_t *ctx,
     return st;
 }
 
+ucs_status_t ucg_builtin_dev_profile_reduce_multi(ucg_builtin_dev_ctx_t *ctx,
+                                                  ucg_dev_op_t op, ucg_dev_dtype_t dt,
+                                                  void *dst, const void *const *srcs,
+                                                  unsigned nsrc, unsigned self,
+                                                  size_t count, unsigned iters,
+                                                  double *avg_us)
+{
+    ucs_status_t st = check_args(ctx, op, dt, "profile_reduce_multi");
+    if (st != UCS_OK) {
+        return st;
+    }
+    if (iters == 0 || avg_us == nullptr) {
+        return set_error(UCS_ERR_INVALID_PARAM, "profile_reduce_multi", "bad arguments");
+    }
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, ctx->stream));
+    for (unsigned i = 0; i < iters && st == UCS_OK; i++) {
+        st = ucg_builtin_dev_reduce_multi(ctx, op, dt, dst, srcs, nsrc, self, count);
+    }
+    HIP_TRY(hipEventRecord(e1, ctx->stream));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *avg_us = 1000.0 * ms / iters;
+    return st;
+}
+
 /* ---- measured ceiling (reference for the roofline, not the combine) ------ */
 static __global__ void __launch_bounds__(kReduceBlock)
 k_stream_probe(u32x4 *dst, const u32x4 *src, size_t nvec, int kind)

@@ -273,6 +273,17 @@ class DevContext:
               "ucg_builtin_dev_profile_reduce")
         return us.value
 
+    def profile_reduce_multi(self, op, dt, dst, srcs, self_index, count, iters):
+        """reduce_multi launched `iters` times back to back between two HIP
+        events on the context stream: average us per launch."""
+        us = ctypes.c_double()
+        arr = (ctypes.c_void_p * len(srcs))(*[_ptr(s) for s in srcs])
+        check(_lib.dev().ucg_builtin_dev_profile_reduce_multi(
+                  self.handle, op_index(op), dt_index(dt), _ptr(dst), arr, len(srcs),
+                  self_index, count, iters, ctypes.byref(us)),
+              "ucg_builtin_dev_profile_reduce_multi")
+        return us.value
+
     def profile_stream(self, kind, dst, src, nbytes, iters):
         """Measured ceiling in the combine's geometry: kind 0 reads both
         buffers (no stores), kind 1 copies src -> dst. Average us per launch."""
