@@ -1,11 +1,16 @@
 /*
- * tune_copy.hip - A/B of the device copy (copy_row in dev_combine.hip: the
- * engine's init and final copies, the all-gather and the push copies): one
- * 16-B non-temporal vector per lane per wave (the product) against U vectors
- * per lane (more bytes in flight per wave), and the runtime's
- * hipMemcpyAsync D2D. Every variant's output is checked against the source.
+ * tune_copy.hip - A/B of the all-gather's row copy (copy_row in
+ * dev_combine.hip, k_gather_multi's in-phase path) against the same copy with
+ * the next tile's first lines loaded ahead (the combine's PF form, issued
+ * before or after the tile's own load).
  *
- *   tune_copy [log2 bytes = 28] [rounds = 5]
+ *   tune_copy [log2 bytes per row = 26] [rounds = 9]
+ *
+ * 8 rows in one allocation, the gather's grid: workgroup b copies tile b / 8
+ * of row b % 8 (dealt round-robin over the rows, so row r runs on XCD r and a
+ * row's next tile is its own XCD's). Output checked bit for bit, then the
+ * variants run interleaved over rounds, 20 launches per sample, HIP events;
+ * 2 x the bytes moved per launch.
  *
  * Built by `make -C tools/src` into tools/ (not part of the product).
  */
@@ -15,7 +20,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <functional>
 #include <string>
 #include <vector>
 
@@ -26,106 +30,135 @@ using namespace ucgdev;
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
     fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
 
-template <int U, int NTL, int NTS>
-__global__ void __launch_bounds__(64)
-k_copy_var(u32x4 *dst, const u32x4 *src, size_t nvec)
+constexpr unsigned kRows = 8;
+
+/* PF 0: the product's aligned row copy; PF > 0: lanes 63 .. 64 - PF also load
+ * the first PF lines of the row's tile D ahead (temporal, discarded), FIRST
+ * = 1 before the tile's own load */
+template <int PF, int D, int FIRST>
+__global__ void __launch_bounds__(kReduceBlock)
+k_copy_rows(char *dst, const char *src, size_t row_bytes)
 {
-    const size_t base = (size_t)blockIdx.x * 64 * U + threadIdx.x;
-    u32x4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        if (base + u * 64 < nvec) {
-            v[u] = ld16<NTL>(src + base + u * 64);
+    const unsigned r  = blockIdx.x % kRows;
+    const size_t wg   = blockIdx.x / kRows;
+    const size_t nvec = row_bytes / 16;
+    const size_t i    = wg * kReduceBlock + threadIdx.x;
+    const u32x4 *s4   = reinterpret_cast<const u32x4*>(src + (size_t)r * row_bytes);
+    u32x4 *o4         = reinterpret_cast<u32x4*>(dst + (size_t)r * row_bytes);
+    const size_t ic   = i < nvec ? i : nvec - 1;
+    u32x4 v, pf;
+    if constexpr (PF > 0) {
+        const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+        const size_t want = (i - threadIdx.x + (size_t)D * kReduceBlock) + (size_t)k * 8;
+        const u32x4 *at   = s4 + (k < (unsigned)PF && want < nvec ? want : nvec - 1);
+        if constexpr (FIRST) {
+            pf = ld16<0>(at);
+            __builtin_amdgcn_sched_barrier(0);
+            v  = ld16<1>(s4 + ic);
+        } else {
+            v  = ld16<1>(s4 + ic);
+            __builtin_amdgcn_sched_barrier(0);
+            pf = ld16<0>(at);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" :: "v"(pf[0]));
+    } else {
+        v = ld16<1>(s4 + ic);
+        __builtin_amdgcn_sched_barrier(0);
     }
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        if (base + u * 64 < nvec) {
-            st16<NTS>(dst + base + u * 64, v[u]);
-        }
+    if (i < nvec) {
+        st16<1>(o4 + i, v);
     }
 }
 
 struct Variant {
     std::string name;
-    std::function<void(u32x4*, const u32x4*, size_t, hipStream_t)> run;
-    std::vector<float> us;
+    void (*f)(char *, const char *, size_t, hipStream_t);
+    std::vector<float> ms;
 };
+
+template <int PF, int D, int FIRST>
+static void run(char *d, const char *s, size_t rb, hipStream_t q)
+{
+    const size_t tiles = (rb / 16 + kReduceBlock - 1) / kReduceBlock;
+    hipLaunchKernelGGL((k_copy_rows<PF, D, FIRST>), dim3((unsigned)(tiles * kRows)),
+                       dim3(kReduceBlock), 0, q, d, s, rb);
+}
+
+__global__ void k_init(uint32_t *p, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        p[i] = (uint32_t)(i * 2654435761u);
+    }
+}
 
 int main(int argc, char **argv)
 {
-    const int lg     = argc > 1 ? atoi(argv[1]) : 28;
-    const int rounds = argc > 2 ? atoi(argv[2]) : 5;
+    const int lg     = argc > 1 ? atoi(argv[1]) : 26;
+    const int rounds = argc > 2 ? atoi(argv[2]) : 9;
     const int iters  = 20;
-    const size_t bytes = (size_t)1 << lg, nvec = bytes / 16;
-    char *pair;
-    /* source and destination as the two halves of one allocation (the
-     * bench's layout for the combine) */
-    CHECK(hipMalloc(&pair, 2 * bytes));
-    u32x4 *src = reinterpret_cast<u32x4*>(pair), *dst = reinterpret_cast<u32x4*>(pair + bytes);
-    hipLaunchKernelGGL((k_fill<UCG_DEV_DT_FLOAT32>), dim3(4096), dim3(256), 0, 0,
-                       (void*)src, 1, 7ull, bytes / 4);
+    const size_t rb = (size_t)1 << lg, total = rb * kRows;
+    std::vector<Variant> vs = {
+        {"product row copy (no prefetch)", run<0, 1, 0>, {}},
+        {"PF1 next tile, after", run<1, 1, 0>, {}},
+        {"PF1 next tile, first", run<1, 1, 1>, {}},
+        {"PF3 next tile, after", run<3, 1, 0>, {}},
+        {"PF3 next tile, first", run<3, 1, 1>, {}},
+        {"PF1 2 tiles ahead, first", run<1, 2, 1>, {}},
+        {"PF3 2 tiles ahead, first", run<3, 2, 1>, {}},
+    };
+    char *arena;
+    CHECK(hipMalloc(&arena, 2 * total));
+    char *src = arena, *dst = arena + total;
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
-    CHECK(hipDeviceSynchronize());
-
-    std::vector<Variant> vs;
-#define VAR(U, NTL, NTS, W)                                                              \
-    vs.push_back({"copy U" #U " ntl" #NTL " nts" #NTS " cap" #W,                          \
-                  [=](u32x4 *d, const u32x4 *s, size_t nv, hipStream_t q) {              \
-        const size_t lds = (W) ? (size_t)163840 / (W) / 512 * 512 : 0;                    \
-        hipLaunchKernelGGL((k_copy_var<U, NTL, NTS>), dim3((unsigned)((nv + 64 * (U) - 1) / (64 * (U)))), \
-                           dim3(64), lds, q, d, s, nv);                                  \
-    }, {}})
-    VAR(1, 1, 1, 0);
-    VAR(2, 1, 1, 0);
-    VAR(4, 1, 1, 0);
-    VAR(2, 1, 1, 16);
-    VAR(2, 1, 1, 24);
-    VAR(4, 1, 1, 8);
-    VAR(4, 1, 1, 16);
-    VAR(1, 0, 1, 0);
-    VAR(2, 0, 1, 0);
-#undef VAR
-    vs.push_back({"hipMemcpyAsync D2D", [=](u32x4 *d, const u32x4 *s, size_t nv, hipStream_t q) {
-        (void)hipMemcpyAsync(d, s, nv * 16, hipMemcpyDeviceToDevice, q);
-    }, {}});
-
-    std::vector<uint32_t> want(bytes / 4), got(bytes / 4);
-    CHECK(hipMemcpy(want.data(), src, bytes, hipMemcpyDeviceToHost));
-    for (auto &v : vs) {
-        CHECK(hipMemset(dst, 0, bytes));
-        v.run(dst, src, nvec, st);
-        CHECK(hipStreamSynchronize(st));
-        CHECK(hipMemcpy(got.data(), dst, bytes, hipMemcpyDeviceToHost));
-        if (memcmp(got.data(), want.data(), bytes) != 0) {
-            printf("MISMATCH %s\n", v.name.c_str());
-            return 3;
+    hipLaunchKernelGGL(k_init, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st,
+                       reinterpret_cast<uint32_t*>(src), total / 4);
+    CHECK(hipStreamSynchronize(st));
+    {
+        std::vector<char> hs(total), hd(total);
+        CHECK(hipMemcpy(hs.data(), src, total, hipMemcpyDeviceToHost));
+        for (auto &v : vs) {
+            CHECK(hipMemset(dst, 0, total));
+            v.f(dst, src, rb, st);
+            CHECK(hipStreamSynchronize(st));
+            CHECK(hipMemcpy(hd.data(), dst, total, hipMemcpyDeviceToHost));
+            if (memcmp(hs.data(), hd.data(), total) != 0) {
+                printf("MISMATCH %s\n", v.name.c_str());
+                return 3;
+            }
         }
     }
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
+    for (auto &v : vs) {
+        for (int i = 0; i < 3; i++) {
+            v.f(dst, src, rb, st);
+        }
+    }
     for (int r = 0; r < rounds; r++) {
         for (auto &v : vs) {
-            v.run(dst, src, nvec, st);
+            v.f(dst, src, rb, st);
             CHECK(hipEventRecord(e0, st));
             for (int i = 0; i < iters; i++) {
-                v.run(dst, src, nvec, st);
+                v.f(dst, src, rb, st);
             }
             CHECK(hipEventRecord(e1, st));
             CHECK(hipEventSynchronize(e1));
             float ms;
             CHECK(hipEventElapsedTime(&ms, e0, e1));
-            v.us.push_back(1000.f * ms / iters);
+            v.ms.push_back(ms / iters);
         }
     }
-    printf("copy of %zu MiB (2x bytes moved), %d rounds x %d iters\n", bytes >> 20, rounds, iters);
+    printf("row copy, %u rows of %zu MiB (the gather's grid), %d rounds x %d\n", kRows,
+           rb >> 20, rounds, iters);
     for (auto &v : vs) {
-        std::sort(v.us.begin(), v.us.end());
-        const double med = v.us[v.us.size() / 2];
-        printf("%-34s median %9.2f us  %7.0f GB/s  %5.1f%% of 8 TB/s\n", v.name.c_str(), med,
-               2.0 * bytes / (med * 1e-6) / 1e9, 100.0 * 2.0 * bytes / (med * 1e-6) / 8e12);
+        std::sort(v.ms.begin(), v.ms.end());
+        const float med = v.ms[v.ms.size() / 2];
+        printf("%-34s median %8.2f us  min %8.2f  %5.1f%% of 8 TB/s\n", v.name.c_str(),
+               med * 1e3, v.ms.front() * 1e3, 100.0 * 2.0 * total / (med * 1e-3) / 8e12);
     }
     return 0;
 }
