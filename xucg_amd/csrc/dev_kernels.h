@@ -130,7 +130,9 @@ __device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
  * wave. The realigning kernel had run 2 points above the plain one on six
  * boxes; this form matched it, against neither the map nor the load alone
  * (tools/tune_misalign, profiles/r04/r04q-r04v). Loads are
- * clamped and unmasked behind a sched barrier, as in k_reduce_shift.
+ * clamped and unmasked behind a sched barrier, as in k_reduce_shift. ORD
+ * fixes the order the three loads issue in (the product's kLoadOrder = 2:
+ * those lines first, then src, then dst; round 6, tools/tune_order).
  */
 template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0, int ORD = 0>
 __global__ void __launch_bounds__(BS)
