@@ -43,6 +43,18 @@ static void run(void *dst, const void *src, size_t nvec, hipStream_t q)
                        static_cast<const T*>(src), (size_t)0, nvec, (size_t)0);
 }
 
+/* the product's form (ORD 2) with dynamic LDS bounding the one-wave
+ * workgroups per CU (160 KiB / LDS): does the 2-operand combine gain from
+ * an occupancy cap as the multi-operand kernels did? */
+template <typename T, int OP, unsigned LDS>
+static void run_cap(void *dst, const void *src, size_t nvec, hipStream_t q)
+{
+    hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, 3, 2>),
+                       dim3((unsigned)((nvec + kReduceBlock - 1) / kReduceBlock)),
+                       dim3(kReduceBlock), LDS, q, static_cast<T*>(dst),
+                       static_cast<const T*>(src), (size_t)0, nvec, (size_t)0);
+}
+
 /* the PF form's aligned body (no ragged edges: the harness sizes are whole
  * tiles) with the load order of ORD and SLP x 64 cycles of s_sleep between
  * the loads' return and the store - does a later store let HBM batch more
@@ -133,6 +145,11 @@ int main(int argc, char **argv)
     PAIR(int16_t, UCG_DEV_OP_MIN, "int16 min");
     PAIR(int64_t, UCG_DEV_OP_SUM, "int64 sum");
     PAIR(int8_t, UCG_DEV_OP_LXOR, "int8 lxor");
+    /* occupancy caps, fp32 SUM (pair 0) */
+#define CAPV(W) vs.push_back({"fp32 sum ORD 2, LDS cap " #W " waves/CU", 0, \
+                              run_cap<float, UCG_DEV_OP_SUM, 163840u / W>, {}});
+    CAPV(8) CAPV(12) CAPV(16) CAPV(20) CAPV(24) CAPV(28)
+#undef CAPV
     /* sleep before the store, fp32 SUM and int32 MAX (pair indices 0, 1) */
 #define SLV(T, OP, P, label, ORD, SLP) \
     vs.push_back({std::string(label), P, run_sleep<T, OP, ORD, SLP>, {}});

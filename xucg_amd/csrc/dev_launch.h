@@ -111,7 +111,8 @@ constexpr int kFullPrefetchTiles = 2;
 constexpr int kRootPrefetchTiles = 1;
 
 /* Round 6: k_reduce_multi N = 8 with operands of 128 MiB and
- * more takes its line four tiles ahead (tools/tune_multi_pf, profiles/r06/
+ * more takes its line four tiles ahead (since the lines-first form below
+ * took the sizes under 256 MiB, from 256 MiB on; tools/tune_multi_pf, profiles/r06/
  * multi, A/B in one process on four boxes): at 512 MiB per operand (C4's
  * shard) 85.3 / 80.7 / 79.9 / 78.6 % of 8 TB/s against 84.3 / 79.4 / 78.6 /
  * 77.7 % two tiles ahead, at 256 MiB 81.5 / 81.6 / 81.2 against 80.9 / 80.9 /
