@@ -1191,6 +1191,51 @@ def test_random_tree_cases_against_oracle(dev_ctx):
 
 
 @pytest.mark.gpu
+def test_multi_and_tree_either_side_of_the_lines_first_threshold(dev_ctx):
+    """Round 6: below 256 MiB per operand the every-operand PF forms issue
+    their lines first (dev_launch.h kPfoMaxVecs, PFO), from there the earlier
+    forms run. k_reduce_multi N = 8 and 16 and the tree fan-in at n = 8 (the
+    NMAX form), 12 and 6 (the exact-n kernels), fp32 SUM on rounded inputs
+    (the association shows), just under and just past 2^24 vectors per
+    operand: sampled windows (head, tile and XCD-chunk edges, tail) of every
+    result bit-exact against the oracle's plan over the same windows of the
+    device-filled operands (ucg_builtin_dev_fill == the oracle's generator)."""
+    dt, op, st = "float32", "sum", np.float32
+    counts = [(1 << 26) - 12, (1 << 26) + 20]
+    cap = (counts[1] + 64) * 4
+    bufs = [dev_ctx.alloc(cap) for _ in range(17)]
+    try:
+        for count in counts:
+            for r in range(16):
+                dev_ctx.fill(dt, "round", 4000 + r, bufs[r], count)
+            dev_ctx.sync()
+            w = 4096
+            starts = [0, count - w, (1 << 24) * 4 - 2048, 64 * 64 * 4 * 8 - 100,
+                      (count // 3) & ~63, (2 * count // 3) | 5]
+            wins = [(a, min(count, a + w)) for a in starts]
+            xs = {r: [bufs[r].download(st, b - a, a * 4) for a, b in wins] for r in range(16)}
+            for kind, n, me in [("multi", 8, 3), ("multi", 16, 5), ("tree", 8, 0),
+                                ("tree", 12, 0), ("tree", 6, 0)]:
+                srcs = [bufs[r].ptr for r in range(n)]
+                if kind == "multi":
+                    rc = dev_ctx.reduce_multi(op, dt, bufs[16].ptr, srcs, me, count)
+                else:
+                    rc = dev_ctx.reduce_tree(op, dt, bufs[16].ptr, srcs, count)
+                assert rc == 0, _lib.last_error()
+                dev_ctx.sync()
+                for k, (a, b) in enumerate(wins):
+                    got = bufs[16].download(st, b - a, a * 4)
+                    ops_k = [xs[r][k] for r in range(n)]
+                    want = (O.reduce_multi(op, dt, ops_k, me) if kind == "multi"
+                            else O.tree_reduce(op, dt, ops_k, root=0))
+                    bad = np.flatnonzero(O.bits(got) != O.bits(want))
+                    assert bad.size == 0, (kind, n, count, a, bad[:8])
+    finally:
+        for b in bufs:
+            b.free()
+
+
+@pytest.mark.gpu
 def test_shift_kernel_every_dtype_and_op(dev_ctx):
     """Every supported (dtype, op) pair through the realigning kernel: src one
     element out of dst's 16-B phase, a ragged count spanning several waves,
