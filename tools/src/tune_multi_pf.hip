@@ -617,6 +617,9 @@ int main(int argc, char **argv)
         case 3:  add_tree_exact<3>(vs, N); break;
         case 6:  add_tree_exact<6>(vs, N); break;
         case 12: add_tree_exact<12>(vs, N); break;
+        case 5:  add_tree_exact<5>(vs, N); break;
+        case 10: add_tree_exact<10>(vs, N); break;
+        case 15: add_tree_exact<15>(vs, N); break;
         default: break;
         }
     }
