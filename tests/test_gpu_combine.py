@@ -1194,7 +1194,8 @@ def test_random_tree_cases_against_oracle(dev_ctx):
 def test_multi_and_tree_either_side_of_the_lines_first_threshold(dev_ctx):
     """Round 6: below 256 MiB per operand the every-operand PF forms issue
     their lines first (dev_launch.h kPfoMaxVecs, PFO), from there the earlier
-    forms run. k_reduce_multi N = 8 and 16 and the tree fan-in at n = 8 (the
+    forms run (fan-ins of 9 operands and more take the lines-first form at
+    every size). k_reduce_multi N = 8 and 16 and the tree fan-in at n = 8 (the
     NMAX form), 12 and 6 (the exact-n kernels), fp32 SUM on rounded inputs
     (the association shows), just under and just past 2^24 vectors per
     operand: sampled windows (head, tile and XCD-chunk edges, tail) of every

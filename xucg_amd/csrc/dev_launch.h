@@ -138,6 +138,14 @@ constexpr size_t kLargePrefetchVecs = (size_t)1 << 23;   /* 128 MiB per operand 
 constexpr int kPfoTiles = 4;
 constexpr size_t kPfoMaxVecs = (size_t)1 << 24;          /* 256 MiB per operand */
 
+/* ... except the tree fan-ins of 9 operands and more, which gained at every
+ * size measured (profiles/r06/pfo/r06zg_*, r06zh_*): exact n = 10 79.9 against
+ * 77.3 % at 256 MiB and 81.0 against 78.4 % at 512 MiB, n = 12 81.1 against
+ * 79.2 % and 76.3 against 75.3 %, n = 16 level at 256 MiB and 84.6 against
+ * 81.9 % at 512 MiB. (The multi-operand kernel at N = 16 lost 1.2 points at
+ * 256 MiB and gained 2.0 at 512 MiB: not taken.) */
+constexpr int kPfoAnySizeOperands = 9;
+
 template <typename T, int OP>
 void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStream_t st)
 {
@@ -445,7 +453,7 @@ void launch_tree_n(T *d, const SrcList &srcs, unsigned n, size_t head, size_t nv
             } else if (cap) {
                 /* the PF form, capped: every operand's next line when n fills
                  * NMAX, else the root's only */
-                if (n == (unsigned)NMAX && chunk < kPfoMaxVecs)
+                if (n == (unsigned)NMAX && (NMAX >= kPfoAnySizeOperands || chunk < kPfoMaxVecs))
                     hipLaunchKernelGGL((k_reduce_tree<T, OP, NMAX, 1, 1, L, NMAX, kPfoTiles, 1>),
                                        g, b, 0, st, d + off, sl, n, h, chunk, t);
                 else if (n == (unsigned)NMAX)
@@ -509,7 +517,7 @@ void launch_tree_exact(T *d, const SrcList &srcs, size_t head, size_t nvec, size
         if (first && div_up(head, kReduceBlock) > grid) {
             grid = (unsigned)div_up(head, kReduceBlock);
         }
-        if (chunk < kPfoMaxVecs) {
+        if (NX >= kPfoAnySizeOperands || chunk < kPfoMaxVecs) {
             hipLaunchKernelGGL((k_reduce_tree<T, OP, NX, 1, 1, kMultiPrefetchLines, NX,
                                               kPfoTiles, 1>),
                                dim3(grid), dim3(kReduceBlock), 0, st, d + off, sl,
