@@ -55,6 +55,16 @@ static void run_cap(void *dst, const void *src, size_t nvec, hipStream_t q)
                        static_cast<const T*>(src), (size_t)0, nvec, (size_t)0);
 }
 
+/* the product's load order with PF lines of the next tile (the product: 3) */
+template <typename T, int OP, int PF>
+static void run_pf(void *dst, const void *src, size_t nvec, hipStream_t q)
+{
+    hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, PF, 2>),
+                       dim3((unsigned)((nvec + kReduceBlock - 1) / kReduceBlock)),
+                       dim3(kReduceBlock), 0, q, static_cast<T*>(dst),
+                       static_cast<const T*>(src), (size_t)0, nvec, (size_t)0);
+}
+
 /* the PF form's aligned body (no ragged edges: the harness sizes are whole
  * tiles) with the load order of ORD and SLP x 64 cycles of s_sleep between
  * the loads' return and the store - does a later store let HBM batch more
@@ -145,10 +155,16 @@ int main(int argc, char **argv)
     PAIR(int16_t, UCG_DEV_OP_MIN, "int16 min");
     PAIR(int64_t, UCG_DEV_OP_SUM, "int64 sum");
     PAIR(int8_t, UCG_DEV_OP_LXOR, "int8 lxor");
+    /* prefetch depth with the lines first, fp32 SUM (pair 0) */
+    vs.push_back({"fp32 sum ORD 2, PF 1 line", 0, run_pf<float, UCG_DEV_OP_SUM, 1>, {}});
+    vs.push_back({"fp32 sum ORD 2, PF 2 lines", 0, run_pf<float, UCG_DEV_OP_SUM, 2>, {}});
+    vs.push_back({"fp32 sum ORD 2, PF 4 lines", 0, run_pf<float, UCG_DEV_OP_SUM, 4>, {}});
+    vs.push_back({"fp32 sum ORD 2, PF 5 lines", 0, run_pf<float, UCG_DEV_OP_SUM, 5>, {}});
+    vs.push_back({"fp32 sum ORD 2, PF 6 lines", 0, run_pf<float, UCG_DEV_OP_SUM, 6>, {}});
     /* occupancy caps, fp32 SUM (pair 0) */
 #define CAPV(W) vs.push_back({"fp32 sum ORD 2, LDS cap " #W " waves/CU", 0, \
                               run_cap<float, UCG_DEV_OP_SUM, 163840u / W>, {}});
-    CAPV(8) CAPV(12) CAPV(16) CAPV(20) CAPV(24) CAPV(28)
+    (void)0; /* caps: r06zd (every cap lost) */
 #undef CAPV
     /* sleep before the store, fp32 SUM and int32 MAX (pair indices 0, 1) */
 #define SLV(T, OP, P, label, ORD, SLP) \
