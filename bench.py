@@ -1750,7 +1750,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_source,
-                "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64, XM=1, PF=3, ORD=2>",
+                "kernel": "ucgdev::k_reduce<float, SUM, 1, 1, 64, XM=1, PF=3, ORD=2, XC=256>",
                 "kernel_avg_us": round(avg_us, 3),
                 "kernel_avg_us_batches": [round(b, 2) for b in batch_us],
                 "kernel_median_us_single_launches": round(median_us, 3),

@@ -1109,6 +1109,39 @@ XCD_NVECS = [3, 7 * 64 + 5, 512 * 64, 1677 * 64 - 34, (8 * 64 * 5 + 8 * 13 + 3) 
              (8 * 64 * 2) * 64 + 1]
 
 
+# the same branches for the 2-operand combine's 256-tile chunks (dev_launch.h
+# kReduceChunkSmall, below 1 GiB per operand)
+XCD256_NVECS = [3, 7 * 64 + 5, 2048 * 64, (8 * 256 * 2) * 64, (8 * 256 * 3 + 8 * 13 + 3) * 64,
+                (8 * 256 * 2 + 5) * 64 - 17, 1677 * 64 - 34]
+
+
+@pytest.mark.gpu
+def test_reduce_xcd_chunk_map_every_branch(dev_ctx):
+    """The in-phase 2-operand combine on 256-tile XCD chunks (round 6): whole
+    chunk rows, chunk rows plus a remainder row, a ragged last round and tile,
+    fewer tiles than a round - every element bit-exact against the oracle, src
+    and dst in phase with a ragged head and tail."""
+    dt, st = "float32", np.float32
+    cap = max(XCD256_NVECS) * 16 + 256
+    src, dst = dev_ctx.alloc(cap), dev_ctx.alloc(cap)
+    try:
+        for nvec in XCD256_NVECS:
+            count = nvec * 4 + 3 + 2          # 8 B into a vector: head 2, tail 3
+            xs = O.fill(dt, "round", 500 + nvec % 991, count)
+            ys = O.fill(dt, "round", 700 + nvec % 983, count)
+            src.upload(xs, 8)
+            dst.upload(ys, 8)
+            rc = dev_ctx.reduce("sum", dt, dst.ptr + 8, src.ptr + 8, count)
+            assert rc == 0, _lib.last_error()
+            dev_ctx.sync()
+            got = dst.download(st, count, 8)
+            bad = np.flatnonzero(O.bits(got) != O.bits(O.reduce("sum", dt, xs, ys)))
+            assert bad.size == 0, (nvec, bad[:8])
+    finally:
+        src.free()
+        dst.free()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("kernel", ["reduce", "multi", "tree"])
 def test_realigning_kernels_xcd_tile_map(dev_ctx, kernel):

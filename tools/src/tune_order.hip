@@ -107,6 +107,39 @@ k_pf_sleep(T *dst, const T *src, size_t nvec)
     }
 }
 
+/* the same body (ORD 2) on XCD chunks of C tiles (the product: 64) */
+template <typename T, int OP, unsigned C>
+__global__ void __launch_bounds__(kReduceBlock)
+k_pf_chunk(T *dst, const T *src, size_t nvec)
+{
+    const u32x4 *s4 = reinterpret_cast<const u32x4*>(src);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    const size_t i  = (size_t)xcd_tile<C>(blockIdx.x, gridDim.x) * kReduceBlock + threadIdx.x;
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const unsigned k = kReduceBlock - 1 - threadIdx.x;
+    const size_t want = (i - threadIdx.x + kReduceBlock) + (size_t)k * 8;
+    const u32x4 *at   = s4 + (k < 3u && want < nvec ? want : nvec - 1);
+    const u32x4 pf = ld16<0>(at);
+    __builtin_amdgcn_sched_barrier(0);
+    const u32x4 a = ld16<1>(s4 + ic);
+    __builtin_amdgcn_sched_barrier(0);
+    const u32x4 b = ld16<1>(d4 + ic);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("" :: "v"(pf[0]));
+    if (i < nvec) {
+        st16<1>(d4 + i, vapply<T, OP>(a, b));
+    }
+}
+
+template <typename T, int OP, unsigned C>
+static void run_chunk(void *dst, const void *src, size_t nvec, hipStream_t q)
+{
+    hipLaunchKernelGGL((k_pf_chunk<T, OP, C>),
+                       dim3((unsigned)((nvec + kReduceBlock - 1) / kReduceBlock)),
+                       dim3(kReduceBlock), 0, q, static_cast<T*>(dst),
+                       static_cast<const T*>(src), nvec);
+}
+
 template <typename T, int OP, int ORD, int SLP>
 static void run_sleep(void *dst, const void *src, size_t nvec, hipStream_t q)
 {
@@ -155,6 +188,12 @@ int main(int argc, char **argv)
     PAIR(int16_t, UCG_DEV_OP_MIN, "int16 min");
     PAIR(int64_t, UCG_DEV_OP_SUM, "int64 sum");
     PAIR(int8_t, UCG_DEV_OP_LXOR, "int8 lxor");
+    /* XCD chunk size with the lines first, fp32 SUM (pair 0) */
+    vs.push_back({"fp32 sum ORD 2, XCD chunk 16", 0, run_chunk<float, UCG_DEV_OP_SUM, 16>, {}});
+    vs.push_back({"fp32 sum ORD 2, XCD chunk 32", 0, run_chunk<float, UCG_DEV_OP_SUM, 32>, {}});
+    vs.push_back({"fp32 sum ORD 2, XCD chunk 64", 0, run_chunk<float, UCG_DEV_OP_SUM, 64>, {}});
+    vs.push_back({"fp32 sum ORD 2, XCD chunk 128", 0, run_chunk<float, UCG_DEV_OP_SUM, 128>, {}});
+    vs.push_back({"fp32 sum ORD 2, XCD chunk 256", 0, run_chunk<float, UCG_DEV_OP_SUM, 256>, {}});
     /* prefetch depth with the lines first, fp32 SUM (pair 0) */
     vs.push_back({"fp32 sum ORD 2, PF 1 line", 0, run_pf<float, UCG_DEV_OP_SUM, 1>, {}});
     vs.push_back({"fp32 sum ORD 2, PF 2 lines", 0, run_pf<float, UCG_DEV_OP_SUM, 2>, {}});

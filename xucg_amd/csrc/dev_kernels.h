@@ -132,9 +132,12 @@ __device__ __forceinline__ unsigned xcd_tile(unsigned b, unsigned ntiles)
  * (tools/tune_misalign, profiles/r04/r04q-r04v). Loads are
  * clamped and unmasked behind a sched barrier, as in k_reduce_shift. ORD
  * fixes the order the three loads issue in (the product's kLoadOrder = 2:
- * those lines first, then src, then dst; round 6, tools/tune_order).
+ * those lines first, then src, then dst; round 6, tools/tune_order). XC is
+ * the XCD map's chunk of tiles (kXcdChunk, or launch_vec's kReduceChunkSmall
+ * below 1 GiB per operand).
  */
-template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0, int ORD = 0>
+template <typename T, int OP, int U, int NT, int BS, int XM = 0, int PF = 0, int ORD = 0,
+          unsigned XC = kXcdChunk>
 __global__ void __launch_bounds__(BS)
 k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
 {
@@ -158,8 +161,7 @@ k_reduce(T *dst, const T *src, size_t head, size_t nvec, size_t tail)
         if (nvec == 0) {
             return;
         }
-        const size_t i  = (size_t)xcd_tile<kXcdChunk>(blockIdx.x, gridDim.x) * BS +
-                          threadIdx.x;
+        const size_t i  = (size_t)xcd_tile<XC>(blockIdx.x, gridDim.x) * BS + threadIdx.x;
         const size_t ic = i < nvec ? i : nvec - 1;
         /* the last PF lanes take one 128-B line (8 vectors) each of the next
          * tile's src, lane 63 its first; every other lane reloads the last

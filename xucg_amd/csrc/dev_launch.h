@@ -87,6 +87,17 @@ constexpr int kPrefetchLines = 3;
  * 1 GiB within 0.4 of the best (tools/tune_order, profiles/r06/order/) */
 constexpr int kLoadOrder = 2;
 
+/* ... and its XCD map's chunk: 256 tiles per XCD chunk below 1 GiB per
+ * operand, the common 64 from there (tools/tune_order, profiles/r06/order/
+ * r06zl_*, r06zm_*, fp32 SUM with the order above, one process per size):
+ * 256-tile chunks read 86.8 against 83.7 % of 8 TB/s at 64 MiB, 87.9
+ * against 86.9 % at 128 MiB, 89.3-89.4 against 88.5 % at 256 MiB (two
+ * boxes), 90.1 against 89.0 % at 512 MiB, but 86.1 against 87.1 % at 1 GiB
+ * (round 4 found the same with 128-tile chunks: +0.2-0.5 at 256 MiB, -1.4
+ * at 1 GiB). */
+constexpr unsigned kReduceChunkSmall = 256;
+constexpr size_t kReduceChunkSmallMaxVecs = (size_t)1 << 26;   /* 1 GiB per operand */
+
 /* The in-phase multi-operand kernels' PF form (round 5):
  * one line of the next tile per prefetched operand (tools/tune_multi_pf,
  * profiles/r05/pf, 64 MiB per operand, A/B in one process): N = 8 and 16,
@@ -161,10 +172,16 @@ void launch_vec(T *d, const T *s, size_t head, size_t nvec, size_t tail, hipStre
         if (first && div_up(head, kReduceBlock) > grid) {
             grid = (unsigned)div_up(head, kReduceBlock);
         }
-        hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, kPrefetchLines, kLoadOrder>),
-                           dim3(grid),
-                           dim3(kReduceBlock), 0, st, d + off, s + off, first ? head : 0,
-                           chunk, last ? tail : 0);
+        if (chunk < kReduceChunkSmallMaxVecs) {
+            hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, kPrefetchLines, kLoadOrder,
+                                         kReduceChunkSmall>),
+                               dim3(grid), dim3(kReduceBlock), 0, st, d + off, s + off,
+                               first ? head : 0, chunk, last ? tail : 0);
+        } else {
+            hipLaunchKernelGGL((k_reduce<T, OP, 1, 1, kReduceBlock, 1, kPrefetchLines, kLoadOrder>),
+                               dim3(grid), dim3(kReduceBlock), 0, st, d + off, s + off,
+                               first ? head : 0, chunk, last ? tail : 0);
+        }
         done += chunk;
     } while (done < nvec);
 }
