@@ -2,7 +2,7 @@
 # Round-6 evidence on the GPU box, one step per argument, each under its own
 # time limit, stopping at the first crash or time limit:
 #   suite    pytest -m gpu (test failures recorded, the script goes on)
-#   tests:EXPR  a pytest -m gpu subset (-k EXPR)
+#   tests:A,B   a pytest -m gpu subset (-k "A or B")
 #   bench    the driver's command (python bench.py), then smoke()
 #   profile  rocprofv3 trace + FETCH_SIZE / WRITE_SIZE passes of bench.py and the
 #            per-launch HBM traffic keyed to the device code object
@@ -26,7 +26,7 @@ for s in "$@"; do
     [ $rc -le 1 ] || exit 1 ;;
   tests:*)
     timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
-        -p no:cacheprovider -k "${s#tests:}" > $OUT/pytest_subset.log 2>&1
+        -p no:cacheprovider -k "$(echo "${s#tests:}" | sed 's/,/ or /g')" > $OUT/pytest_subset.log 2>&1
     rc=$?; echo "pytest rc $rc" >> $OUT/steps.log
     [ $rc -le 1 ] || exit 1 ;;
   bench)
