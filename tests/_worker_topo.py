@@ -385,9 +385,14 @@ def main():
         coll.close()
     if rank == 0:
         print(f"stats {group.stats()} combine {cmb.stats()}", flush=True)
+    # teardown: a member that stalls here names its step (the Python stack on
+    # stderr after 60 s; the peers' last barrier gives up after 90)
+    import faulthandler
+    faulthandler.dump_traceback_later(60, exit=False)
     group.close()
     iface.close()
     cmb.close()
+    faulthandler.cancel_dump_traceback_later()
     if dctx is not None:
         dctx.close()
     if rc == 0:
