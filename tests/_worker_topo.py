@@ -362,6 +362,11 @@ def main():
             free_buf(sbuf, "send buffer")
             free_buf(rbuf, "recv buffer")
 
+    # the last cases and the teardown take a second: a member that stalls in
+    # them names its step (the Python stack on stderr after 60 s; the peers'
+    # last barrier gives up after 90)
+    import faulthandler
+    faulthandler.dump_traceback_later(60, exit=False)
     # rounded fp32: tolerance against the fp64 sum, digests for identity
     for ci, count in enumerate((4096, 1000)):
         xs = [O.fill("float32", "round", 7000 + 11 * ci + m, count) for m in range(n)]
@@ -385,10 +390,6 @@ def main():
         coll.close()
     if rank == 0:
         print(f"stats {group.stats()} combine {cmb.stats()}", flush=True)
-    # teardown: a member that stalls here names its step (the Python stack on
-    # stderr after 60 s; the peers' last barrier gives up after 90)
-    import faulthandler
-    faulthandler.dump_traceback_later(60, exit=False)
     group.close()
     iface.close()
     cmb.close()

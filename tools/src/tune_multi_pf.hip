@@ -241,6 +241,43 @@ k_multi_pffirst(float *dst, SrcList srcs, size_t nvec)
     }
 }
 
+/* Round 6 (r06zq): the product's PF form (all operands' lines D tiles
+ * ahead, after the loads or - PFO - before them) on XCD chunks of C tiles
+ * (the product: 64; the 2-operand combine gained from 256 below 1 GiB) */
+template <int N, int D, int PFO, unsigned C>
+__global__ void __launch_bounds__(kReduceBlock)
+k_multi_chunk(float *dst, SrcList srcs, size_t nvec)
+{
+    UCG_MULTI_CAP_CLOBBER();
+    const size_t i  = (size_t)xcd_tile<C>(blockIdx.x, gridDim.x) * kReduceBlock + threadIdx.x;
+    const size_t ic = i < nvec ? i : nvec - 1;
+    const u32x4 *op[N];
+    u32x4 val[N];
+#pragma unroll
+    for (int m = 0; m < N; m++) {
+        op[m] = reinterpret_cast<const u32x4*>(srcs.p[m]);
+    }
+    if constexpr (PFO) {
+        u32x4 pf[N];
+        tile_lines_issue<1, N, D>(op, i, nvec, pf);
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            val[m] = ld16<1>(op[m] + ic);
+        }
+        tile_lines_keep<N>(pf);
+    } else {
+#pragma unroll
+        for (int m = 0; m < N; m++) {
+            val[m] = ld16<1>(op[m] + ic);
+        }
+        next_tile_lines<1, N, D>(op, i, nvec);
+    }
+    auto fv = [](u32x4 a, u32x4 b) { return vapply<float, 0>(a, b); };
+    if (i < nvec) {
+        st16<1>(reinterpret_cast<u32x4*>(dst) + i, rd_tree<N>(val, fv));
+    }
+}
+
 /* the N operands read and dst written with zeros: the traffic of the
  * combine, no dependency of a store on its loads */
 template <int N>
@@ -449,6 +486,18 @@ static void add_multi(std::vector<Variant> &vs)
     PV("persistent 16/CU, pipelined, 4 ahead", 4096, 4, 1, 0);
     PV("persistent 16/CU, no pipeline, 4 ahead", 4096, 4, 0, 0);
 #undef PV
+#define CV(label, D, PFO, C)                                                             \
+    vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
+        hipLaunchKernelGGL((k_multi_chunk<N, D, PFO, C>), dim3(tiles(nv)),               \
+                           dim3(kReduceBlock), 0, q, d, s, nv);                           \
+    }, true, {}})
+    CV("chunk 64, lines after, 4 ahead", 4, 0, 64);
+    CV("chunk 128, lines after, 4 ahead", 4, 0, 128);
+    CV("chunk 256, lines after, 4 ahead", 4, 0, 256);
+    CV("chunk 64, lines first, 4 ahead", 4, 1, 64);
+    CV("chunk 128, lines first, 4 ahead", 4, 1, 128);
+    CV("chunk 256, lines first, 4 ahead", 4, 1, 256);
+#undef CV
 #define FV(label, D, PFM)                                                                \
     vs.push_back({label, [](float *d, SrcList s, size_t nv, hipStream_t q) {             \
         hipLaunchKernelGGL((k_multi_pffirst<N, D, PFM>), dim3(tiles(nv)),                 \
