@@ -140,6 +140,51 @@ static void run_chunk(void *dst, const void *src, size_t nvec, hipStream_t q)
                        static_cast<const T*>(src), nvec);
 }
 
+/* the realigning combine's aligned body (src 4 B past dst's phase: Q = 1,
+ * rb = 0; no ragged edges) on XCD chunks of C tiles (the product: 64) */
+template <typename T, int OP, unsigned C>
+__global__ void __launch_bounds__(kReduceBlock)
+k_shift_chunk(T *dst, const T *src, size_t nvec)
+{
+    const u32x4 *a4 = reinterpret_cast<const u32x4*>(reinterpret_cast<const char*>(src) + 4 - 4);
+    u32x4 *d4       = reinterpret_cast<u32x4*>(dst);
+    const size_t i  = (size_t)xcd_tile<C>(blockIdx.x, gridDim.x) * kReduceBlock + threadIdx.x;
+    const bool last_lane = threadIdx.x == kReduceBlock - 1;
+    const u32x4 b  = ld16<1>(d4 + (i < nvec ? i : nvec - 1));
+    const u32x4 lo = ld16<1>(a4 + (i < nvec ? i : nvec));
+    const unsigned k  = kReduceBlock - 1 - threadIdx.x;
+    const size_t want = (i - threadIdx.x + kReduceBlock) + (size_t)k * 8;
+    const u32x4 ex = ld16<0>(a4 + (k < 3u && want <= nvec ? want : nvec));
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 hi;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        hi[q] = from_next_lane(lo[q]);
+    }
+    if (last_lane) {
+        hi = ex;
+    }
+    if (i < nvec) {
+        const uint32_t w[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        u32x4 sv;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            sv[q] = __builtin_amdgcn_alignbyte(w[q + 2], w[q + 1], 0u);
+        }
+        st16<1>(d4 + i, vapply<T, OP>(sv, b));
+    }
+}
+
+template <typename T, int OP, unsigned C>
+static void run_shift_chunk(void *dst, const void *src, size_t nvec, hipStream_t q)
+{
+    /* src + 4 B: its aligned vectors A[0..nvec] start at src; one vector fewer */
+    hipLaunchKernelGGL((k_shift_chunk<T, OP, C>),
+                       dim3((unsigned)((nvec - 1 + kReduceBlock - 1) / kReduceBlock)),
+                       dim3(kReduceBlock), 0, q, static_cast<T*>(dst), static_cast<const T*>(src),
+                       nvec - 1);
+}
+
 template <typename T, int OP, int ORD, int SLP>
 static void run_sleep(void *dst, const void *src, size_t nvec, hipStream_t q)
 {
@@ -188,6 +233,11 @@ int main(int argc, char **argv)
     PAIR(int16_t, UCG_DEV_OP_MIN, "int16 min");
     PAIR(int64_t, UCG_DEV_OP_SUM, "int64 sum");
     PAIR(int8_t, UCG_DEV_OP_LXOR, "int8 lxor");
+    /* the realigning kernel's XCD chunk (its own pair) */
+    vs.push_back({"shift fp32 sum chunk 64 ORD 0", np, run_shift_chunk<float, UCG_DEV_OP_SUM, 64>, {}});
+    vs.push_back({"shift fp32 sum chunk 128", np, run_shift_chunk<float, UCG_DEV_OP_SUM, 128>, {}});
+    vs.push_back({"shift fp32 sum chunk 256", np, run_shift_chunk<float, UCG_DEV_OP_SUM, 256>, {}});
+    np++;
     /* XCD chunk size with the lines first, fp32 SUM (pair 0) */
     vs.push_back({"fp32 sum ORD 2, XCD chunk 16", 0, run_chunk<float, UCG_DEV_OP_SUM, 16>, {}});
     vs.push_back({"fp32 sum ORD 2, XCD chunk 32", 0, run_chunk<float, UCG_DEV_OP_SUM, 32>, {}});
